@@ -1,0 +1,273 @@
+/*
+ * ketogpu.h — C ABI of the MI355X batched permission-check engine (libketogpu.so).
+ *
+ * This is the drop-in boundary for Ory Keto's evaluation engines.  Every entry
+ * point below replaces a reference interface (paths relative to the reference
+ * repository); the Go side binds it through cgo.
+ *
+ *   ketogpu_builder_*      new persistence-side snapshot loader; replaces the
+ *                          per-node SQL reads of (*Persister).GetRelationTuples
+ *                          internal/persistence/sql/relationtuples.go:203-258
+ *   ketogpu_check          (*check.Engine).SubjectIsAllowed
+ *                          internal/check/engine.go:93-95 (recursion :33-91)
+ *   ketogpu_resolve /      the same, split into host resolution (strings -> node
+ *   ketogpu_check_ids /    ids) and a batched device traversal over ids with
+ *   ketogpu_queries_*      inputs resident in HBM
+ *   ketogpu_expand         (*expand.Engine).BuildTree internal/expand/engine.go:30-98
+ *   ketogpu_tree_*         expand.Tree / its JSON codec internal/expand/tree.go:26-30,85-91,156-162
+ *
+ * Conventions: plain C types only; all input memory is copied (cgo pointer rules);
+ * opaque handles are owned by the library; result buffers are caller-allocated.
+ * Functions return KETOGPU_OK or a positive KETOGPU_E* code; ketogpu_last_error()
+ * returns a thread-local message for the last failure on the calling thread.
+ * Error mapping (herodot): ENOTFOUND -> ErrNotFound (404), EINVAL -> ErrBadRequest
+ * (400), EDEVICE/ENOMEM -> ErrInternalServerError (500).
+ */
+#ifndef KETOGPU_H
+#define KETOGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KETOGPU_ABI_VERSION 1
+
+#define KETOGPU_OK 0
+#define KETOGPU_ENOTFOUND 1 /* unknown namespace (herodot.ErrNotFound)              */
+#define KETOGPU_EINVAL 2    /* malformed input, nil subject, unsorted rows          */
+#define KETOGPU_EDEVICE 3   /* HIP runtime / device failure                          */
+#define KETOGPU_ENOMEM 4    /* host or device allocation failure                    */
+
+#define KETOGPU_SUBJECT_ID 0
+#define KETOGPU_SUBJECT_SET 1
+#define KETOGPU_SUBJECT_NIL (-1)
+
+#define KETOGPU_NODE_NONE 0xFFFFFFFFu /* no such node / root with no tuples      */
+
+/* builder flags */
+#define KETOGPU_BUILD_SORT 1u /* rows are NOT in ORDER BY order: sort them with SQLite
+                                  semantics (NULLs first, BINARY collation) */
+
+typedef struct ketogpu_builder ketogpu_builder;
+typedef struct ketogpu_snapshot ketogpu_snapshot;
+typedef struct ketogpu_engine ketogpu_engine;
+typedef struct ketogpu_queries ketogpu_queries;
+typedef struct ketogpu_tree ketogpu_tree;
+
+/* namespace.Namespace{ID, Name} (internal/namespace/definitons.go:8-12), config order */
+typedef struct {
+    int32_t id;
+    const char *name;
+} ketogpu_namespace;
+
+/* A batch of keto_relation_tuples rows, columnar (one row per index; string column c of
+ * row i is c_data[c_off[i] .. c_off[i+1]), offsets have n+1 entries).  Row layout follows
+ * RelationTuple (internal/persistence/sql/relationtuples.go:18-31): subject_kind 0 =
+ * subject_id row (ss_* ignored), 1 = subject-set row (subject_id ignored).
+ * Rows of one snapshot must arrive in the backend's
+ *   ORDER BY nid, namespace_id, object, relation, subject_id, subject_set_namespace_id,
+ *            subject_set_object, subject_set_relation, commit_time   (relationtuples.go:215)
+ * order across all append calls, for ONE nid (persister.go:117-119), unless the builder
+ * was created with KETOGPU_BUILD_SORT. */
+typedef struct {
+    size_t n;
+    const int32_t *namespace_id;
+    const char *object_data;
+    const uint64_t *object_off;
+    const char *relation_data;
+    const uint64_t *relation_off;
+    const uint8_t *subject_kind;
+    const char *subject_id_data;
+    const uint64_t *subject_id_off;
+    const int32_t *ss_namespace_id;
+    const char *ss_object_data;
+    const uint64_t *ss_object_off;
+    const char *ss_relation_data;
+    const uint64_t *ss_relation_off;
+} ketogpu_row_batch;
+
+typedef struct {
+    int32_t page_size; /* GetRelationTuples page size; 0 -> 100 (persister.go:68-70) */
+    uint32_t flags;    /* KETOGPU_BUILD_* */
+} ketogpu_build_opts;
+
+typedef struct {
+    uint64_t num_rows;           /* rows appended                                  */
+    uint64_t num_bad_rows;       /* rows whose namespace ids are not configured    */
+    uint64_t num_groups;         /* distinct (namespace_id, object, relation)      */
+    uint64_t num_nodes;          /* N: subject nodes (subject ids + subject sets)  */
+    uint64_t num_expandable;     /* Nx: nodes whose query returns >= 1 row         */
+    uint64_t num_interior;       /* Ni: expandable nodes that are also subjects    */
+    uint64_t num_edges;          /* rows kept after page-poison truncation         */
+    uint64_t num_interior_edges; /* deduplicated edges into interior nodes         */
+    uint64_t num_rev_edges;      /* deduplicated reverse edges                     */
+    uint64_t num_wildcard_nodes; /* subject sets with an empty field (R5)           */
+    uint64_t num_ambiguous_nodes;/* nodes sharing a Subject.String() key (R4)      */
+    double build_seconds;
+} ketogpu_snapshot_stats;
+
+/* ----------------------------------------------------------------- snapshot */
+int ketogpu_builder_new(const ketogpu_namespace *namespaces, size_t num_namespaces,
+                        const ketogpu_build_opts *opts, ketogpu_builder **out);
+int ketogpu_builder_append(ketogpu_builder *b, const ketogpu_row_batch *rows);
+/* consumes b (also on failure) */
+int ketogpu_builder_finish(ketogpu_builder *b, ketogpu_snapshot **out);
+void ketogpu_builder_free(ketogpu_builder *b);
+void ketogpu_snapshot_free(ketogpu_snapshot *s);
+int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats *out);
+
+/* Read-only view of the device graph as built on the host (for tools and tests; the
+ * pointers live as long as the snapshot).  Node ids: [0, num_interior) interior,
+ * [num_interior, num_expandable) other expandable nodes, the rest never expand. */
+typedef struct {
+    uint32_t num_nodes, num_expandable, num_interior;
+    const uint64_t *fint_off; /* num_expandable + 1 */
+    const uint32_t *fint_col; /* interior successors of each expandable node */
+    const uint64_t *rev_off;  /* num_nodes + 1 */
+    const uint32_t *rev_col;  /* expandable predecessors of each node */
+} ketogpu_graph_view;
+int ketogpu_snapshot_graph(const ketogpu_snapshot *s, ketogpu_graph_view *out);
+
+/* ------------------------------------------------------------------- check */
+/* relationtuple.Subject: SubjectID{ID} or SubjectSet{Namespace, Object, Relation}
+ * (internal/relationtuple/definitions.go:39-41,103-118) */
+typedef struct {
+    int32_t kind; /* KETOGPU_SUBJECT_* */
+    const char *id;
+    const char *ns;
+    const char *obj;
+    const char *rel;
+} ketogpu_subject;
+
+/* InternalRelationTuple used as a check request (definitions.go:95-100); an empty
+ * namespace/object/relation is "no filter", as in GetRelationTuples. */
+typedef struct {
+    const char *ns;
+    const char *obj;
+    const char *rel;
+    ketogpu_subject subject;
+} ketogpu_check_request;
+
+/* Host resolution of one request to node ids.  *root is an expandable node or
+ * KETOGPU_NODE_NONE (the query returns no tuples, or its namespace is unknown: false);
+ * *target is a node or KETOGPU_NODE_NONE (the subject appears in no tuple: false).
+ * Returns KETOGPU_EINVAL for a nil subject; returns KETOGPU_ENOTFOUND with *root =
+ * KETOGPU_NODE_NONE when the root is a wildcard query that matches no snapshot node
+ * (use ketogpu_check for those). */
+int ketogpu_resolve(const ketogpu_snapshot *s, const ketogpu_check_request *req, uint32_t *root,
+                    uint32_t *target);
+
+/* A batch of check requests, columnar like ketogpu_row_batch (string column c of request
+ * i is c_data[c_off[i] .. c_off[i+1])).  subject_kind: 0 subject id (sid columns), 1
+ * subject set (ss_* columns), 255 nil subject; NULL means all subject ids. */
+typedef struct {
+    size_t n;
+    const char *ns_data;
+    const uint64_t *ns_off;
+    const char *obj_data;
+    const uint64_t *obj_off;
+    const char *rel_data;
+    const uint64_t *rel_off;
+    const uint8_t *subject_kind;
+    const char *sid_data;
+    const uint64_t *sid_off;
+    const char *ss_ns_data;
+    const uint64_t *ss_ns_off;
+    const char *ss_obj_data;
+    const uint64_t *ss_obj_off;
+    const char *ss_rel_data;
+    const uint64_t *ss_rel_off;
+} ketogpu_request_batch;
+
+/* ketogpu_resolve for a whole batch; status[i] as ketogpu_resolve's return value
+ * (KETOGPU_OK, KETOGPU_EINVAL for nil subjects, KETOGPU_ENOTFOUND for wildcard roots
+ * without a node).  status may be NULL. */
+int ketogpu_resolve_batch(const ketogpu_snapshot *s, const ketogpu_request_batch *reqs, uint32_t *roots,
+                          uint32_t *targets, int32_t *status);
+
+typedef struct {
+    int32_t device;             /* HIP device ordinal                                */
+    uint32_t max_words_per_round; /* 64-check words traversed together; 0 = auto      */
+    uint64_t state_budget_bytes;  /* HBM for traversal state; 0 = auto (<= 1/3 free)  */
+} ketogpu_engine_opts;
+
+/* uploads the snapshot's device graph (forward interior CSR + reverse CSR) to HBM */
+int ketogpu_engine_new(const ketogpu_snapshot *s, const ketogpu_engine_opts *opts,
+                       ketogpu_engine **out);
+void ketogpu_engine_free(ketogpu_engine *e);
+
+/* SubjectIsAllowed for n requests: allowed[i] in {0,1}; status[i] = KETOGPU_OK or
+ * KETOGPU_EINVAL (nil subject).  Unknown namespaces yield allowed = 0 (engine.go:75-77).
+ * The function itself fails only on device/alloc errors. */
+int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n, uint8_t *allowed,
+                  int32_t *status);
+
+/* id-level batch: roots/targets from ketogpu_resolve; allowed_bits / flagged_bits have
+ * ceil(n/64) words, bit i%64 of word i/64 for request i.  A flagged request touched a
+ * node whose Subject.String() key is shared with another node (R4 in DESIGN.md): its bit
+ * is only exact after re-evaluation with the sequential semantics (ketogpu_check does
+ * that itself).  flagged_bits may be NULL. */
+int ketogpu_check_ids(ketogpu_engine *e, const uint32_t *roots, const uint32_t *targets, size_t n,
+                      uint64_t *allowed_bits, uint64_t *flagged_bits);
+
+/* device-resident query sets: upload once, run many times (results stay in HBM) */
+int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint32_t *targets,
+                           size_t n, ketogpu_queries **out);
+int ketogpu_queries_run(ketogpu_engine *e, ketogpu_queries *q);
+int ketogpu_queries_download(ketogpu_engine *e, const ketogpu_queries *q, uint64_t *allowed_bits,
+                             uint64_t *flagged_bits);
+void ketogpu_queries_free(ketogpu_queries *q);
+
+/* statistics of the last run on this engine (for the roofline report) */
+typedef struct {
+    uint64_t checks;
+    uint64_t rounds;
+    uint64_t levels;            /* BFS levels summed over rounds                  */
+    uint64_t frontier_entries;  /* (word, node) entries expanded                  */
+    uint64_t interior_edges;    /* interior edges scanned by the push kernel      */
+    uint64_t rev_edges;         /* reverse edges scanned by the pull kernel       */
+    uint64_t touched;           /* (word, node) visited entries reset             */
+    uint64_t bytes_push;        /* algorithmic bytes of the push (expand) kernel  */
+    uint64_t bytes_pull;        /* algorithmic bytes of the pull kernel           */
+    uint64_t bytes_total;       /* algorithmic bytes of all kernels               */
+    double ms_push;             /* summed device time of push launches (hipEvent) */
+    double ms_pull;
+    double ms_total;            /* device time, first to last kernel              */
+    uint64_t push_launches;
+    uint64_t overflow_retries;
+} ketogpu_run_stats;
+int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
+
+/* ------------------------------------------------------------------ expand */
+/* BuildTree(subject, rest_depth).  *out = NULL is the nil tree (JSON null).
+ * KETOGPU_ENOTFOUND when a fetched page references an unknown namespace. */
+int ketogpu_expand(const ketogpu_snapshot *s, const ketogpu_subject *subject, int32_t rest_depth,
+                   ketogpu_tree **out);
+
+#define KETOGPU_NODE_UNION 0
+#define KETOGPU_NODE_LEAF 1
+/* flattened tree in preorder; strings are owned by the tree */
+typedef struct {
+    int32_t type;         /* KETOGPU_NODE_UNION / KETOGPU_NODE_LEAF                */
+    uint32_t num_children;/* the children follow in preorder                      */
+    ketogpu_subject subject;
+} ketogpu_tree_node;
+int ketogpu_tree_nodes(const ketogpu_tree *t, const ketogpu_tree_node **nodes, size_t *n);
+/* MarshalJSON of the tree (tree.go:156-162); free with ketogpu_free */
+int ketogpu_tree_json(const ketogpu_tree *t, char **json);
+void ketogpu_tree_free(ketogpu_tree *t);
+
+/* ------------------------------------------------------------------- misc */
+const char *ketogpu_last_error(void);
+int ketogpu_abi_version(void);
+void ketogpu_free(void *p);
+/* number of visible HIP devices (0 without a GPU) */
+int ketogpu_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

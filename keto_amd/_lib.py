@@ -1,0 +1,158 @@
+"""ctypes binding of libketogpu.so (include/ketogpu.h).
+
+The library is built in-tree by `python -m keto_amd.build` (or
+__graft_entry__.build()).  Loading fails loudly when it is missing: there is no
+fallback implementation of any entry point.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libketogpu.so")
+
+OK, ENOTFOUND, EINVAL, EDEVICE, ENOMEM = 0, 1, 2, 3, 4
+SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
+NODE_NONE = 0xFFFFFFFF
+BUILD_SORT = 1
+NODE_UNION, NODE_LEAF = 0, 1
+
+
+class KetoError(Exception):
+    """A failing libketogpu call; .code is the KETOGPU_E* code."""
+
+    NAMES = {ENOTFOUND: "not_found", EINVAL: "invalid", EDEVICE: "device", ENOMEM: "nomem"}
+
+    def __init__(self, code, msg=""):
+        super().__init__(f"{self.NAMES.get(code, code)}: {msg}")
+        self.code = code
+        self.kind = self.NAMES.get(code, "error")
+
+
+class Namespace(C.Structure):
+    _fields_ = [("id", C.c_int32), ("name", C.c_char_p)]
+
+
+class RowBatch(C.Structure):
+    _fields_ = [
+        ("n", C.c_size_t),
+        ("namespace_id", C.c_void_p),
+        ("object_data", C.c_void_p), ("object_off", C.c_void_p),
+        ("relation_data", C.c_void_p), ("relation_off", C.c_void_p),
+        ("subject_kind", C.c_void_p),
+        ("subject_id_data", C.c_void_p), ("subject_id_off", C.c_void_p),
+        ("ss_namespace_id", C.c_void_p),
+        ("ss_object_data", C.c_void_p), ("ss_object_off", C.c_void_p),
+        ("ss_relation_data", C.c_void_p), ("ss_relation_off", C.c_void_p),
+    ]
+
+
+class BuildOpts(C.Structure):
+    _fields_ = [("page_size", C.c_int32), ("flags", C.c_uint32)]
+
+
+class SnapshotStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "num_rows", "num_bad_rows", "num_groups", "num_nodes", "num_expandable", "num_interior", "num_edges",
+        "num_interior_edges", "num_rev_edges", "num_wildcard_nodes", "num_ambiguous_nodes")] + [
+        ("build_seconds", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class Subject(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("id", C.c_char_p), ("ns", C.c_char_p), ("obj", C.c_char_p),
+                ("rel", C.c_char_p)]
+
+
+class CheckRequest(C.Structure):
+    _fields_ = [("ns", C.c_char_p), ("obj", C.c_char_p), ("rel", C.c_char_p), ("subject", Subject)]
+
+
+class EngineOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_words_per_round", C.c_uint32), ("state_budget_bytes", C.c_uint64)]
+
+
+class RunStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "checks", "rounds", "levels", "frontier_entries", "interior_edges", "rev_edges", "touched", "bytes_push",
+        "bytes_pull", "bytes_total")] + [("ms_push", C.c_double), ("ms_pull", C.c_double), ("ms_total", C.c_double)] + [
+        ("push_launches", C.c_uint64), ("overflow_retries", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class RequestBatch(C.Structure):
+    _fields_ = [("n", C.c_size_t)] + [(n, C.c_void_p) for n in (
+        "ns_data", "ns_off", "obj_data", "obj_off", "rel_data", "rel_off", "subject_kind", "sid_data", "sid_off",
+        "ss_ns_data", "ss_ns_off", "ss_obj_data", "ss_obj_off", "ss_rel_data", "ss_rel_off")]
+
+
+class GraphView(C.Structure):
+    _fields_ = [("num_nodes", C.c_uint32), ("num_expandable", C.c_uint32), ("num_interior", C.c_uint32),
+                ("fint_off", C.POINTER(C.c_uint64)), ("fint_col", C.POINTER(C.c_uint32)),
+                ("rev_off", C.POINTER(C.c_uint64)), ("rev_col", C.POINTER(C.c_uint32))]
+
+
+class TreeNode(C.Structure):
+    _fields_ = [("type", C.c_int32), ("num_children", C.c_uint32), ("subject", Subject)]
+
+
+# every symbol declared in include/ketogpu.h, with its ctypes signature
+vp, i32, u32, sz = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
+SIGNATURES = {
+    "ketogpu_builder_new": (C.c_int, [C.POINTER(Namespace), sz, C.POINTER(BuildOpts), C.POINTER(vp)]),
+    "ketogpu_builder_append": (C.c_int, [vp, C.POINTER(RowBatch)]),
+    "ketogpu_builder_finish": (C.c_int, [vp, C.POINTER(vp)]),
+    "ketogpu_builder_free": (None, [vp]),
+    "ketogpu_snapshot_free": (None, [vp]),
+    "ketogpu_snapshot_stats_get": (C.c_int, [vp, C.POINTER(SnapshotStats)]),
+    "ketogpu_snapshot_graph": (C.c_int, [vp, C.POINTER(GraphView)]),
+    "ketogpu_resolve": (C.c_int, [vp, C.POINTER(CheckRequest), C.POINTER(u32), C.POINTER(u32)]),
+    "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
+    "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),
+    "ketogpu_engine_free": (None, [vp]),
+    "ketogpu_check": (C.c_int, [vp, C.POINTER(CheckRequest), sz, vp, vp]),
+    "ketogpu_check_ids": (C.c_int, [vp, vp, vp, sz, vp, vp]),
+    "ketogpu_queries_upload": (C.c_int, [vp, vp, vp, sz, C.POINTER(vp)]),
+    "ketogpu_queries_run": (C.c_int, [vp, vp]),
+    "ketogpu_queries_download": (C.c_int, [vp, vp, vp, vp]),
+    "ketogpu_queries_free": (None, [vp]),
+    "ketogpu_engine_last_stats": (C.c_int, [vp, C.POINTER(RunStats)]),
+    "ketogpu_expand": (C.c_int, [vp, C.POINTER(Subject), i32, C.POINTER(vp)]),
+    "ketogpu_tree_nodes": (C.c_int, [vp, C.POINTER(C.POINTER(TreeNode)), C.POINTER(sz)]),
+    "ketogpu_tree_json": (C.c_int, [vp, C.POINTER(vp)]),
+    "ketogpu_tree_free": (None, [vp]),
+    "ketogpu_last_error": (C.c_char_p, []),
+    "ketogpu_abi_version": (C.c_int, []),
+    "ketogpu_free": (None, [vp]),
+    "ketogpu_device_count": (C.c_int, []),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m keto_amd.build` "
+                               "(there is no non-native fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != OK:
+        msg = lib().ketogpu_last_error()
+        raise KetoError(rc, msg.decode("utf-8", "replace") if msg else "")
+
+
+def b(s):
+    return None if s is None else s.encode("utf-8")

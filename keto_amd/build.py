@@ -1,0 +1,69 @@
+"""Build libketogpu.so (HIP for gfx950 + host C++) in-tree with hipcc.
+
+    python -m keto_amd.build            # builds keto_amd/libketogpu.so
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libketogpu.so")
+SYNTH_LIB = os.path.join(HERE, "libketosynth.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
+
+SOURCES = ["snapshot.cpp", "host_engine.cpp", "device_engine.hip"]
+HEADERS = ["ketogpu_internal.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build(force=False, jobs=4):
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS]
+    objs = []
+    procs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(objdir, src + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            cmd = [HIPCC, "-c", "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+                   "-I", os.path.join(ROOT, "include"), s, "-o", o]
+            if src.endswith(".cpp"):
+                cmd = [HIPCC, "-c", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(ROOT, "include"), s,
+                       "-o", o]
+            print("+", " ".join(cmd), flush=True)
+            procs.append(subprocess.Popen(cmd))
+            if len(procs) >= jobs:
+                for p in procs:
+                    if p.wait():
+                        raise SystemExit(f"compile failed: {p.args}")
+                procs = []
+    for p in procs:
+        if p.wait():
+            raise SystemExit(f"compile failed: {p.args}")
+    if force or _stale(LIB, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs +
+             ["-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
+    synth_src = os.path.join(CSRC, "synth.cpp")
+    if os.path.exists(synth_src) and (force or _stale(SYNTH_LIB, [synth_src])):
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", SYNTH_LIB, synth_src, "-lpthread"])
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

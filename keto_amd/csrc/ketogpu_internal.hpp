@@ -1,0 +1,195 @@
+// ketogpu_internal.hpp — shared host-side data structures of libketogpu.
+//
+// The snapshot is the device-ready restatement of the reference's tuple table:
+//   * rows are grouped per (namespace_id, object, relation) in the backend's ORDER BY
+//     order (internal/persistence/sql/relationtuples.go:215),
+//   * every subject becomes an interned node (SubjectID or SubjectSet,
+//     internal/relationtuple/definitions.go:39-41,103-118),
+//   * a subject set expands into the rows its query returns, with empty fields acting
+//     as "no filter" (relationtuples.go:218-236) and page-poison truncation for rows
+//     whose namespace ids are not configured (relationtuples.go:43-80,248-255),
+//   * node ids are ordered interior | source | non-expandable so the device traversal
+//     state only covers interior nodes (DESIGN.md "Data layout in HBM").
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../../include/ketogpu.h"
+
+namespace ketogpu {
+
+constexpr uint32_t NONE = KETOGPU_NODE_NONE;
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string &msg);
+
+inline uint64_t hash_bytes(const char *p, size_t n) {
+    // 64-bit FNV-1a with a final avalanche; good enough for interning.
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; i++) h = (h ^ (unsigned char)p[i]) * 1099511628211ull;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    return h;
+}
+
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+// Interned byte strings with stable storage.  id 0 is always "".
+class StrPool {
+  public:
+    StrPool() { intern("", 0); }
+    uint32_t intern(const char *p, size_t n);
+    uint32_t find(const char *p, size_t n) const;
+    uint32_t find(std::string_view s) const { return find(s.data(), s.size()); }
+    std::string_view get(uint32_t id) const { return std::string_view(ptr_[id], len_[id]); }
+    size_t size() const { return ptr_.size(); }
+
+  private:
+    void rehash();
+    std::vector<std::unique_ptr<char[]>> chunks_;
+    size_t used_ = 0, cap_ = 0;
+    std::vector<const char *> ptr_;
+    std::vector<uint32_t> len_;
+    std::vector<uint64_t> slot_hash_;
+    std::vector<uint32_t> slot_id_;  // id+1, 0 = empty
+    size_t mask_ = 0;
+};
+
+// Open-addressing map from a 96-bit key (int32 namespace id, u32 object id, u32 relation id)
+// to a u32 value.
+class TripleMap {
+  public:
+    TripleMap() { resize(1024); }
+    uint32_t get(int32_t ns, uint32_t obj, uint32_t rel) const;
+    // returns existing value or inserts `v` and returns it
+    uint32_t get_or_insert(int32_t ns, uint32_t obj, uint32_t rel, uint32_t v);
+    void remap(const std::vector<uint32_t> &perm);
+    size_t size() const { return n_; }
+
+  private:
+    struct Slot {
+        int32_t ns;
+        uint32_t obj, rel, val;  // val == NONE: empty
+    };
+    static uint64_t h(int32_t ns, uint32_t obj, uint32_t rel) {
+        return mix64(((uint64_t)(uint32_t)ns << 32 | obj) ^ mix64(rel + 0x9e3779b97f4a7c15ull));
+    }
+    void resize(size_t cap);
+    std::vector<Slot> slots_;
+    size_t n_ = 0, mask_ = 0;
+};
+
+struct Namespace {
+    int32_t id;
+    std::string name;
+};
+
+// One (namespace_id, object, relation) group of rows, in DB order.
+struct Group {
+    int32_t ns;
+    uint32_t obj, rel;       // StrPool ids
+    uint64_t begin;          // into Snapshot::group_col (valid prefix only)
+    uint32_t valid;          // rows before the first bad row
+    uint32_t full_len;       // all rows of the group
+    int64_t first_bad;       // index of the first row with an unknown namespace, or -1
+};
+
+// Query result of one subject set / root query after page-poison truncation.
+struct RowRef {
+    uint64_t off = 0;        // into Snapshot::row_col
+    uint32_t len = 0;        // rows returned to the check engine (truncated)
+    uint32_t full_len = 0;   // rows of the query (for expand)
+    int64_t first_bad = -1;  // index of first bad row in query order, -1 if none
+};
+
+struct Snapshot {
+    // ---- configuration
+    std::vector<Namespace> namespaces;  // config order, unique names and ids
+    int page_size = 100;
+    int32_t empty_name_ns = 0;          // id of the namespace named "" (if has_empty_name_ns)
+    bool has_empty_name_ns = false;
+
+    // ---- strings and groups
+    StrPool pool;
+    std::vector<Group> groups;          // DB order
+    std::vector<uint32_t> group_col;    // subjects (node ids) of the groups' valid prefixes
+
+    // ---- nodes: [0, Ni) interior, [Ni, Nx) source-expandable, [Nx, N) non-expandable
+    uint32_t N = 0, Ni = 0, Nx = 0;
+    std::vector<uint8_t> node_kind;     // KETOGPU_SUBJECT_ID / _SET
+    std::vector<int32_t> node_ns;       // set: namespace id
+    std::vector<uint32_t> node_a;       // id: StrPool id of the subject id; set: object id
+    std::vector<uint32_t> node_b;       // set: relation id
+    std::vector<uint32_t> sid_node;     // StrPool id -> subject-id node (NONE)
+    TripleMap set_node;                 // (ns, obj, rel) -> subject-set node
+    std::vector<RowRef> node_row;       // per node: its query's rows (host DFS)
+    std::vector<uint32_t> row_col;      // rows of wildcard queries (materialized) + copies
+    std::vector<uint32_t> key_id;       // Subject.String() identity per node
+    std::vector<uint8_t> ambiguous;     // key shared with another node (R4)
+    StrPool key_pool;                   // keys that may collide (see snapshot.cpp)
+    bool has_ambiguous = false;
+
+    // ---- device graph (built on host, uploaded by the engine)
+    std::vector<uint64_t> fint_off;     // Nx + 1
+    std::vector<uint32_t> fint_col;     // interior successors, sorted, unique
+    std::vector<uint64_t> rev_off;      // N + 1
+    std::vector<uint32_t> rev_col;      // expandable predecessors, sorted, unique
+    std::vector<uint32_t> row_amb;      // bitmap over Nx: row contains an ambiguous node
+
+    ketogpu_snapshot_stats stats{};
+
+    // ---- helpers
+    const Namespace *ns_by_name(std::string_view name) const {
+        for (auto &n : namespaces)
+            if (n.name == name) return &n;
+        return nullptr;
+    }
+    const Namespace *ns_by_id(int32_t id) const {
+        for (auto &n : namespaces)
+            if (n.id == id) return &n;
+        return nullptr;
+    }
+    const uint32_t *row_ptr(uint32_t v) const { return row_col.data() + node_row[v].off; }
+    std::string key_string(uint32_t v) const;
+    // Materialize the rows of a query with "" = no filter.  ns_filter < 0 = any.
+    RowRef materialize(bool any_ns, int32_t ns, uint32_t obj, bool any_obj, uint32_t rel,
+                       bool any_rel, std::vector<uint32_t> &out) const;
+};
+
+// ---- host engine entry points (host_engine.cpp)
+struct ResolvedRoot {
+    enum Kind { EMPTY, NODE, DYNAMIC, UNKNOWN_NS } kind = EMPTY;
+    uint32_t node = NONE;
+    // DYNAMIC: the query, to materialize
+    bool any_ns = false, any_obj = false, any_rel = false;
+    int32_t ns = 0;
+    uint32_t obj = 0, rel = 0;
+};
+ResolvedRoot resolve_root(const Snapshot &s, std::string_view ns, std::string_view obj, std::string_view rel);
+uint32_t resolve_subject(const Snapshot &s, int kind, std::string_view id, std::string_view ns, std::string_view obj,
+                         std::string_view rel);
+uint32_t resolve_subject(const Snapshot &s, const ketogpu_subject &subj);
+inline std::string_view sv(const char *p) { return p ? std::string_view(p) : std::string_view(); }
+// exact sequential check (reference DFS with Subject.String() visited keys)
+bool exact_check(const Snapshot &s, const uint32_t *root_rows, uint32_t root_len,
+                 const ketogpu_subject &req, uint32_t target);
+
+}  // namespace ketogpu

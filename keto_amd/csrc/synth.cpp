@@ -1,0 +1,318 @@
+// synth.cpp — synthetic workloads of BASELINE.json (tooling for bench.py and tests,
+// not part of the engine ABI).  Config #2: synthetic RBAC,
+//   users u0..u{U-1}; groups g0..g{G-1} in 4 levels (1% / 4% / 15% / 80%), every group
+//   below the top has 1-2 parents one level up (groups:gP#member@(groups:gC#member));
+//   memberships groups:g#member@u, Poisson(mean) per user into leaf groups chosen by
+//   Zipf(s) ; the remaining tuples are grants docs:dK#viewer@(groups:g#member) (80%) or
+//   @u (20%) over D docs.  Longest path doc -> g0 -> g1 -> g2 -> g3 -> user = 5 edges.
+//   Checks docs:d#viewer@u: 50% constructed positives (a sampled grant path), 50%
+//   uniform random pairs.
+// Rows are emitted already in the reference's ORDER BY order under SQLite semantics
+// (namespace id, then BINARY object, relation, NULL subject_id first, ...), i.e. what
+// the snapshot loader reads from the database.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Rng {  // splitmix64
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed) {}
+    uint64_t next() {
+        uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    }
+    uint64_t below(uint64_t n) { return n ? next() % n : 0; }
+    double unit() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+};
+
+// ranks of 0..n-1 in the lexicographic order of their decimal strings
+std::vector<uint32_t> lex_order(uint64_t n) {
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    if (!n) return order;
+    order.push_back(0);
+    std::vector<uint64_t> st;
+    for (int d = 9; d >= 1; d--)
+        if ((uint64_t)d < n) st.push_back(d);
+    while (!st.empty()) {
+        uint64_t v = st.back();
+        st.pop_back();
+        order.push_back((uint32_t)v);
+        for (int e = 9; e >= 0; e--) {
+            uint64_t c = v * 10 + e;
+            if (c < n) st.push_back(c);
+        }
+    }
+    return order;
+}
+
+struct Col {
+    std::vector<char> data;
+    std::vector<uint64_t> off{0};
+    void put(const char *p, size_t n) {
+        data.insert(data.end(), p, p + n);
+        off.push_back(data.size());
+    }
+    void put_num(char prefix, uint64_t v) {
+        char b[24];
+        int n = snprintf(b, sizeof b, "%c%llu", prefix, (unsigned long long)v);
+        put(b, (size_t)n);
+    }
+    void empty() { off.push_back(data.size()); }
+};
+
+}  // namespace
+
+struct ks_rbac {
+    // rows (columnar, ketogpu_row_batch layout)
+    std::vector<int32_t> ns, ss_ns;
+    std::vector<uint8_t> kind;
+    Col obj, rel, sid, ss_obj, ss_rel;
+    // checks: doc index, user index, constructed-positive flag
+    std::vector<uint32_t> chk_doc, chk_user;
+    std::vector<uint8_t> chk_pos;
+    // request columns for the checks
+    Col rq_ns, rq_obj, rq_rel, rq_sid;
+    uint64_t n_parent = 0, n_member = 0, n_grant = 0;
+};
+
+extern "C" {
+
+typedef struct {
+    uint64_t users, groups, docs, tuples, checks, seed;
+    double zipf_s, member_mean;
+} ks_rbac_params;
+
+typedef struct {
+    uint64_t n;
+    const int32_t *namespace_id;
+    const char *object_data;
+    const uint64_t *object_off;
+    const char *relation_data;
+    const uint64_t *relation_off;
+    const uint8_t *subject_kind;
+    const char *subject_id_data;
+    const uint64_t *subject_id_off;
+    const int32_t *ss_namespace_id;
+    const char *ss_object_data;
+    const uint64_t *ss_object_off;
+    const char *ss_relation_data;
+    const uint64_t *ss_relation_off;
+    // checks
+    uint64_t n_checks;
+    const uint32_t *chk_doc, *chk_user;
+    const uint8_t *chk_pos;
+    const char *rq_ns_data;
+    const uint64_t *rq_ns_off;
+    const char *rq_obj_data;
+    const uint64_t *rq_obj_off;
+    const char *rq_rel_data;
+    const uint64_t *rq_rel_off;
+    const char *rq_sid_data;
+    const uint64_t *rq_sid_off;
+    uint64_t n_parent, n_member, n_grant;
+} ks_rbac_view;
+
+ks_rbac *ks_rbac_generate(const ks_rbac_params *p) {
+    auto *w = new ks_rbac();
+    Rng rng(p->seed);
+    const uint64_t U = p->users, G = p->groups, D = p->docs;
+    // ---- group levels
+    uint64_t lv[4];
+    lv[0] = std::max<uint64_t>(1, G / 100);
+    lv[1] = std::max<uint64_t>(1, G * 4 / 100);
+    lv[2] = std::max<uint64_t>(1, G * 15 / 100);
+    lv[3] = G - lv[0] - lv[1] - lv[2];
+    uint64_t base[5] = {0, lv[0], lv[0] + lv[1], lv[0] + lv[1] + lv[2], G};
+    // children[g] = child groups of g (edge g -> child)
+    std::vector<std::vector<uint32_t>> children(G);
+    for (int l = 1; l < 4; l++)
+        for (uint64_t c = base[l]; c < base[l + 1]; c++) {
+            int np = 1 + (int)rng.below(2);
+            uint32_t p0 = (uint32_t)(base[l - 1] + rng.below(lv[l - 1]));
+            children[p0].push_back((uint32_t)c);
+            if (np == 2 && lv[l - 1] > 1) {
+                uint32_t p1;
+                do p1 = (uint32_t)(base[l - 1] + rng.below(lv[l - 1]));
+                while (p1 == p0);
+                children[p1].push_back((uint32_t)c);
+            }
+            w->n_parent += np == 2 && lv[l - 1] > 1 ? 2 : 1;
+        }
+    // ---- memberships: Poisson(mean) per user into leaf groups by Zipf(s)
+    const uint64_t L = lv[3];
+    std::vector<double> cdf(L);
+    {
+        double acc = 0;
+        for (uint64_t k = 0; k < L; k++) acc += 1.0 / std::pow((double)(k + 1), p->zipf_s), cdf[k] = acc;
+        for (auto &x : cdf) x /= acc;
+    }
+    // leaf rank k -> leaf group id (a fixed random permutation so hubs are spread)
+    std::vector<uint32_t> leaf_perm(L);
+    std::iota(leaf_perm.begin(), leaf_perm.end(), (uint32_t)base[3]);
+    for (uint64_t i = L; i > 1; i--) std::swap(leaf_perm[i - 1], leaf_perm[rng.below(i)]);
+    std::vector<std::vector<uint32_t>> members(G);
+    std::poisson_distribution<int> pois(p->member_mean);
+    std::mt19937_64 mt(p->seed ^ 0x5bd1e995);
+    for (uint64_t u = 0; u < U; u++) {
+        int k = pois(mt);
+        for (int j = 0; j < k; j++) {
+            uint64_t r = std::lower_bound(cdf.begin(), cdf.end(), rng.unit()) - cdf.begin();
+            if (r >= L) r = L - 1;
+            members[leaf_perm[r]].push_back((uint32_t)u);
+            w->n_member++;
+        }
+    }
+    // ---- grants fill the tuple budget
+    uint64_t used = w->n_parent + w->n_member;
+    uint64_t n_grant = p->tuples > used ? p->tuples - used : D;
+    std::vector<std::vector<uint32_t>> doc_groups(D), doc_users(D);
+    for (uint64_t i = 0; i < n_grant; i++) {
+        uint64_t d = rng.below(D);
+        if (rng.unit() < 0.8)
+            doc_groups[d].push_back((uint32_t)rng.below(G));
+        else
+            doc_users[d].push_back((uint32_t)rng.below(U));
+    }
+    w->n_grant = n_grant;
+    // ---- emit rows in ORDER BY order (SQLite: BINARY strings, NULL subject_id first)
+    std::vector<uint32_t> urank(U), grank(G);
+    {
+        auto o = lex_order(U);
+        for (uint64_t i = 0; i < U; i++) urank[o[i]] = (uint32_t)i;
+        auto og = lex_order(G);
+        for (uint64_t i = 0; i < G; i++) grank[og[i]] = (uint32_t)i;
+    }
+    auto by_u = [&](uint32_t a, uint32_t b) { return urank[a] < urank[b]; };
+    auto by_g = [&](uint32_t a, uint32_t b) { return grank[a] < grank[b]; };
+    uint64_t total = w->n_parent + w->n_member + n_grant;
+    w->ns.reserve(total);
+    w->kind.reserve(total);
+    w->ss_ns.reserve(total);
+    auto row_set = [&](int32_t ns, char op, uint64_t o, const char *rel, char sp, uint64_t so, int32_t sns,
+                       const char *srel) {
+        w->ns.push_back(ns);
+        w->kind.push_back(1);
+        w->ss_ns.push_back(sns);
+        w->obj.put_num(op, o);
+        w->rel.put(rel, strlen(rel));
+        w->sid.empty();
+        w->ss_obj.put_num(sp, so);
+        w->ss_rel.put(srel, strlen(srel));
+    };
+    auto row_id = [&](int32_t ns, char op, uint64_t o, const char *rel, uint64_t u) {
+        w->ns.push_back(ns);
+        w->kind.push_back(0);
+        w->ss_ns.push_back(0);
+        w->obj.put_num(op, o);
+        w->rel.put(rel, strlen(rel));
+        w->sid.put_num('u', u);
+        w->ss_obj.empty();
+        w->ss_rel.empty();
+    };
+    // namespace 1: groups (ordered by object string)
+    for (uint32_t g : lex_order(G)) {
+        auto &ch = children[g];
+        std::sort(ch.begin(), ch.end(), by_g);
+        for (uint32_t c : ch) row_set(1, 'g', g, "member", 'g', c, 1, "member");
+        auto &m = members[g];
+        std::sort(m.begin(), m.end(), by_u);
+        for (uint32_t u : m) row_id(1, 'g', g, "member", u);
+    }
+    // namespace 2: docs
+    for (uint32_t d : lex_order(D)) {
+        auto &dg = doc_groups[d];
+        std::sort(dg.begin(), dg.end(), by_g);
+        for (uint32_t g : dg) row_set(2, 'd', d, "viewer", 'g', g, 1, "member");
+        auto &du = doc_users[d];
+        std::sort(du.begin(), du.end(), by_u);
+        for (uint32_t u : du) row_id(2, 'd', d, "viewer", u);
+    }
+    // ---- checks
+    const uint64_t C = p->checks;
+    w->chk_doc.resize(C);
+    w->chk_user.resize(C);
+    w->chk_pos.resize(C);
+    for (uint64_t i = 0; i < C; i++) {
+        uint64_t d = rng.below(D);
+        uint64_t u = rng.below(U);
+        bool pos = false;
+        if (rng.unit() < 0.5) {
+            // constructed positive: sample a grant path from a doc that has grants
+            for (int tries = 0; tries < 64 && !pos; tries++) {
+                uint64_t dd = rng.below(D);
+                uint64_t ng = doc_groups[dd].size(), nu = doc_users[dd].size();
+                if (!ng && !nu) continue;
+                uint64_t pick = rng.below(ng + nu);
+                if (pick >= ng) {
+                    d = dd, u = doc_users[dd][pick - ng], pos = true;
+                    break;
+                }
+                uint32_t g = doc_groups[dd][pick];
+                for (int hop = 0; hop < 8; hop++) {  // walk down to a member
+                    uint64_t nc = children[g].size(), nm = members[g].size();
+                    if (!nc && !nm) break;
+                    uint64_t k = rng.below(nc + nm);
+                    if (k >= nc) {
+                        d = dd, u = members[g][k - nc], pos = true;
+                        break;
+                    }
+                    g = children[g][k];
+                }
+            }
+        }
+        w->chk_doc[i] = (uint32_t)d;
+        w->chk_user[i] = (uint32_t)u;
+        w->chk_pos[i] = pos;
+        w->rq_ns.put("docs", 4);
+        w->rq_obj.put_num('d', d);
+        w->rq_rel.put("viewer", 6);
+        w->rq_sid.put_num('u', u);
+    }
+    return w;
+}
+
+void ks_rbac_view_get(const ks_rbac *w, ks_rbac_view *v) {
+    v->n = w->ns.size();
+    v->namespace_id = w->ns.data();
+    v->object_data = w->obj.data.data();
+    v->object_off = w->obj.off.data();
+    v->relation_data = w->rel.data.data();
+    v->relation_off = w->rel.off.data();
+    v->subject_kind = w->kind.data();
+    v->subject_id_data = w->sid.data.data();
+    v->subject_id_off = w->sid.off.data();
+    v->ss_namespace_id = w->ss_ns.data();
+    v->ss_object_data = w->ss_obj.data.data();
+    v->ss_object_off = w->ss_obj.off.data();
+    v->ss_relation_data = w->ss_rel.data.data();
+    v->ss_relation_off = w->ss_rel.off.data();
+    v->n_checks = w->chk_doc.size();
+    v->chk_doc = w->chk_doc.data();
+    v->chk_user = w->chk_user.data();
+    v->chk_pos = w->chk_pos.data();
+    v->rq_ns_data = w->rq_ns.data.data();
+    v->rq_ns_off = w->rq_ns.off.data();
+    v->rq_obj_data = w->rq_obj.data.data();
+    v->rq_obj_off = w->rq_obj.off.data();
+    v->rq_rel_data = w->rq_rel.data.data();
+    v->rq_rel_off = w->rq_rel.off.data();
+    v->rq_sid_data = w->rq_sid.data.data();
+    v->rq_sid_off = w->rq_sid.off.data();
+    v->n_parent = w->n_parent;
+    v->n_member = w->n_member;
+    v->n_grant = w->n_grant;
+}
+
+void ks_rbac_free(ks_rbac *w) { delete w; }
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+"""Snapshot of keto_relation_tuples for one network, built by libketogpu.
+
+The persistence-side loader of DESIGN.md: rows arrive in the backend's ORDER BY
+order (internal/persistence/sql/relationtuples.go:215) and become the ordered host
+rows (expand) plus the device graph (check).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from . import persistence
+from .relationtuple import SubjectID, SubjectSet
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def subject_struct(subject):
+    if subject is None:
+        return L.Subject(L.SUBJECT_NIL, None, None, None, None)
+    if isinstance(subject, SubjectID):
+        return L.Subject(L.SUBJECT_ID, L.b(subject.id), None, None, None)
+    return L.Subject(L.SUBJECT_SET, None, L.b(subject.namespace), L.b(subject.object), L.b(subject.relation))
+
+
+class Snapshot:
+    def __init__(self, namespaces, page_size=100, sort=False):
+        self.L = L.lib()
+        self.namespaces = [(n, int(i)) for n, i in namespaces]
+        arr = (L.Namespace * max(len(self.namespaces), 1))(*[L.Namespace(i, L.b(n)) for n, i in self.namespaces])
+        opts = L.BuildOpts(page_size, L.BUILD_SORT if sort else 0)
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_builder_new(arr, len(self.namespaces), C.byref(opts), C.byref(h)))
+        self._builder = h
+        self.h = None
+
+    def append(self, cols):
+        keep = cols  # arrays must stay alive during the call
+        rb = L.RowBatch(len(cols["namespace_id"]), _ptr(cols["namespace_id"]), _ptr(cols["object_data"]),
+                        _ptr(cols["object_off"]), _ptr(cols["relation_data"]), _ptr(cols["relation_off"]),
+                        _ptr(cols["subject_kind"]), _ptr(cols["subject_id_data"]), _ptr(cols["subject_id_off"]),
+                        _ptr(cols["ss_namespace_id"]), _ptr(cols["ss_object_data"]), _ptr(cols["ss_object_off"]),
+                        _ptr(cols["ss_relation_data"]), _ptr(cols["ss_relation_off"]))
+        L.check(self.L.ketogpu_builder_append(self._builder, C.byref(rb)))
+        del keep
+        return self
+
+    def finish(self):
+        h = C.c_void_p()
+        b, self._builder = self._builder, None
+        L.check(self.L.ketogpu_builder_finish(b, C.byref(h)))
+        self.h = h
+        return self
+
+    def __del__(self):
+        lib = getattr(self, "L", None)
+        if lib is None:
+            return
+        if getattr(self, "_builder", None):
+            lib.ketogpu_builder_free(self._builder)
+        if getattr(self, "h", None):
+            lib.ketogpu_snapshot_free(self.h)
+            self.h = None
+
+    # ---- constructors
+    @classmethod
+    def from_store(cls, store: persistence.TupleStore, batch_rows=1 << 16):
+        s = cls(store.namespaces, store.page_size)
+        for cols in store.iter_ordered_batches(batch_rows):
+            s.append(cols)
+        return s.finish()
+
+    @classmethod
+    def from_rows(cls, namespaces, rows, page_size=100, sort=True):
+        s = cls(namespaces, page_size, sort=sort)
+        if rows:
+            s.append(persistence.columnar(rows))
+        return s.finish()
+
+    @classmethod
+    def from_tuples(cls, namespaces, tuples, page_size=100):
+        return cls.from_rows(namespaces, persistence.rows_from_tuples(namespaces, tuples), page_size, sort=True)
+
+    @classmethod
+    def from_columns(cls, namespaces, cols, page_size=100, sort=False):
+        s = cls(namespaces, page_size, sort=sort)
+        s.append(cols)
+        return s.finish()
+
+    # ---- queries
+    def stats(self):
+        st = L.SnapshotStats()
+        L.check(self.L.ketogpu_snapshot_stats_get(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def graph(self):
+        """numpy copies of the device graph (ketogpu_snapshot_graph)"""
+        v = L.GraphView()
+        L.check(self.L.ketogpu_snapshot_graph(self.h, C.byref(v)))
+        nx, n = v.num_expandable, v.num_nodes
+        fo = np.ctypeslib.as_array(v.fint_off, (nx + 1,)).copy()
+        ro = np.ctypeslib.as_array(v.rev_off, (n + 1,)).copy()
+        fc = np.ctypeslib.as_array(v.fint_col, (max(int(fo[-1]), 1),))[:int(fo[-1])].copy()
+        rc = np.ctypeslib.as_array(v.rev_col, (max(int(ro[-1]), 1),))[:int(ro[-1])].copy()
+        return {"N": n, "Nx": nx, "Ni": v.num_interior, "fint_off": fo, "fint_col": fc, "rev_off": ro, "rev_col": rc}
+
+    def resolve(self, namespace, obj, relation, subject):
+        """-> (root, target) node ids (KETOGPU_NODE_NONE when absent)"""
+        req = L.CheckRequest(L.b(namespace), L.b(obj), L.b(relation), subject_struct(subject))
+        r, t = C.c_uint32(), C.c_uint32()
+        L.check(self.L.ketogpu_resolve(self.h, C.byref(req), C.byref(r), C.byref(t)))
+        return r.value, t.value
+
+    def resolve_many(self, requests):
+        roots = np.empty(len(requests), dtype=np.uint32)
+        targets = np.empty(len(requests), dtype=np.uint32)
+        for i, (ns, obj, rel, subj) in enumerate(requests):
+            roots[i], targets[i] = self.resolve(ns, obj, rel, subj)
+        return roots, targets

@@ -1,0 +1,114 @@
+"""Synthetic workloads of BASELINE.json (driver of keto_amd/csrc/synth.cpp).
+
+Config #2 — synthetic RBAC: 10M users, 100k nested groups,
+50M tuples, 1M checks docs:d#viewer@u (half constructed positives), seed 0x4B45544F.
+Rows come out in the reference's ORDER BY order (SQLite semantics), i.e. exactly what
+the snapshot loader would read from the database.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib as L
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEED = 0x4B45544F
+_slib = None
+
+
+class Params(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("users", "groups", "docs", "tuples", "checks", "seed")] + [
+        ("zipf_s", C.c_double), ("member_mean", C.c_double)]
+
+
+class View(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(n, C.c_void_p) for n in (
+        "namespace_id", "object_data", "object_off", "relation_data", "relation_off", "subject_kind",
+        "subject_id_data", "subject_id_off", "ss_namespace_id", "ss_object_data", "ss_object_off",
+        "ss_relation_data", "ss_relation_off")] + [("n_checks", C.c_uint64)] + [(n, C.c_void_p) for n in (
+        "chk_doc", "chk_user", "chk_pos", "rq_ns_data", "rq_ns_off", "rq_obj_data", "rq_obj_off", "rq_rel_data",
+        "rq_rel_off", "rq_sid_data", "rq_sid_off")] + [(n, C.c_uint64) for n in ("n_parent", "n_member", "n_grant")]
+
+
+def slib():
+    global _slib
+    if _slib is None:
+        path = os.path.join(HERE, "libketosynth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `python -m keto_amd.build`")
+        _slib = C.CDLL(path)
+        _slib.ks_rbac_generate.restype = C.c_void_p
+        _slib.ks_rbac_generate.argtypes = [C.POINTER(Params)]
+        _slib.ks_rbac_view_get.argtypes = [C.c_void_p, C.POINTER(View)]
+        _slib.ks_rbac_free.argtypes = [C.c_void_p]
+    return _slib
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    ct = np.ctypeslib.as_ctypes_type(np.dtype(dtype))
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), (n,))
+
+
+class Workload:
+    """rows (columnar, ORDER BY order) + check requests; arrays view C++ memory"""
+
+    namespaces = [("groups", 1), ("docs", 2)]
+
+    def __init__(self, params: Params):
+        self.params = params
+        self.h = slib().ks_rbac_generate(C.byref(params))
+        v = View()
+        slib().ks_rbac_view_get(self.h, C.byref(v))
+        self.v = v
+        n = v.n
+        off = lambda p: _arr(p, n + 1, np.uint64)
+        data = lambda p, o: _arr(p, int(o[-1]), np.uint8) if int(o[-1]) else np.zeros(1, np.uint8)
+        cols = {"namespace_id": _arr(v.namespace_id, n, np.int32), "subject_kind": _arr(v.subject_kind, n, np.uint8),
+                "ss_namespace_id": _arr(v.ss_namespace_id, n, np.int32)}
+        for c in ("object", "relation", "subject_id", "ss_object", "ss_relation"):
+            o = off(getattr(v, c + "_off"))
+            cols[c + "_off"] = o
+            cols[c + "_data"] = data(getattr(v, c + "_data"), o)
+        cols["commit_time"] = None
+        self.columns = cols
+        m = v.n_checks
+        self.n_checks = m
+        self.chk_doc = _arr(v.chk_doc, m, np.uint32)
+        self.chk_user = _arr(v.chk_user, m, np.uint32)
+        self.chk_pos = _arr(v.chk_pos, m, np.uint8)
+        self.counts = {"parent": v.n_parent, "member": v.n_member, "grant": v.n_grant, "tuples": n}
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            slib().ks_rbac_free(self.h)
+            self.h = None
+
+    def request_batch(self):
+        v, m = self.v, self.n_checks
+        return L.RequestBatch(m, v.rq_ns_data, v.rq_ns_off, v.rq_obj_data, v.rq_obj_off, v.rq_rel_data, v.rq_rel_off,
+                              None, v.rq_sid_data, v.rq_sid_off, None, None, None, None, None, None)
+
+    def resolve(self, snap):
+        """host resolution of all checks -> (roots, targets) node ids"""
+        m = self.n_checks
+        roots = np.empty(m, dtype=np.uint32)
+        targets = np.empty(m, dtype=np.uint32)
+        status = np.empty(m, dtype=np.int32)
+        rb = self.request_batch()
+        L.check(L.lib().ketogpu_resolve_batch(snap.h, C.byref(rb), roots.ctypes.data, targets.ctypes.data,
+                                              status.ctypes.data))
+        assert not status.any()
+        return roots, targets
+
+    def requests(self, idx):
+        """(ns, obj, rel, subject dict) for the oracle"""
+        return [("docs", f"d{int(self.chk_doc[i])}", "viewer", {"subject_id": f"u{int(self.chk_user[i])}"})
+                for i in idx]
+
+
+def rbac(users=10_000_000, groups=100_000, docs=2_000_000, tuples=50_000_000, checks=1_000_000, seed=SEED,
+         zipf_s=1.1, member_mean=3.0):
+    return Workload(Params(users, groups, docs, tuples, checks, seed, zipf_s, member_mean))

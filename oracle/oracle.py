@@ -1,0 +1,186 @@
+"""ctypes wrapper of the C oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  It loads oracle/build/libketo_oracle.so (built by `make -C oracle`)
+and exposes the reference semantics restated in keto_oracle.c.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libketo_oracle.so")
+_lib = None
+
+OK, ENOTFOUND, EINVAL, ENOMEM = 0, -1, -2, -3
+SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        vp, cp, i32, i64, u64p = C.c_void_p, C.c_char_p, C.c_int32, C.c_int64, C.POINTER(C.c_uint64)
+        L.ko_store_new.restype = vp
+        L.ko_store_free.argtypes = [vp]
+        L.ko_add_namespace.argtypes = [vp, i32, cp]
+        L.ko_set_page_size.argtypes = [vp, C.c_int]
+        L.ko_add_row.argtypes = [vp, i32, cp, cp, cp, i32, cp, cp, i64]
+        L.ko_add_rows_columnar.argtypes = [vp, C.c_size_t] + [vp] * 14
+        L.ko_finalize.argtypes = [vp, C.c_int]
+        L.ko_num_rows.argtypes = [vp]
+        L.ko_num_rows.restype = C.c_size_t
+        L.ko_check.argtypes = [vp, cp, cp, cp, C.c_int, cp, cp, cp, cp, C.POINTER(C.c_int)]
+        L.ko_check_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp]
+        L.ko_expand.argtypes = [vp, C.c_int, cp, cp, cp, cp, C.c_int, C.POINTER(C.c_void_p)]
+        L.ko_get_page.argtypes = [vp, cp, cp, cp, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
+        L.ko_free.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _b(s):
+    return None if s is None else s.encode("utf-8")
+
+
+class OracleError(Exception):
+    def __init__(self, code):
+        super().__init__({ENOTFOUND: "not_found", EINVAL: "invalid", ENOMEM: "nomem"}.get(code, str(code)))
+        self.code = code
+        self.kind = {ENOTFOUND: "not_found", EINVAL: "invalid"}.get(code, "error")
+
+
+def subject_args(d):
+    """subject of a fixture dict -> (kind, id, ns, obj, rel)"""
+    if d.get("subject_id") is not None:
+        return SUBJECT_ID, d["subject_id"], None, None, None
+    if d.get("subject_set") is not None:
+        s = d["subject_set"]
+        return SUBJECT_SET, None, s["namespace"], s["object"], s["relation"]
+    return SUBJECT_NIL, None, None, None, None
+
+
+class Store:
+    """keto_relation_tuples + namespace config, read through the reference's queries."""
+
+    def __init__(self, namespaces, page_size=100):
+        self.L = lib()
+        self.h = self.L.ko_store_new()
+        self.namespaces = list(namespaces)  # [(name, id)] in config order
+        for name, nid in self.namespaces:
+            self.L.ko_add_namespace(self.h, nid, _b(name))
+        self.L.ko_set_page_size(self.h, page_size)
+        self._ct = 0
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ko_store_free(self.h)
+            self.h = None
+
+    def ns_id(self, name):
+        for n, i in self.namespaces:  # GetNamespaceByName: first match
+            if n == name:
+                return i
+        raise KeyError(name)
+
+    def add_row(self, namespace_id, obj, rel, subject_id=None, ss_ns_id=0, ss_obj=None, ss_rel=None, commit_time=None):
+        if commit_time is None:
+            commit_time = self._ct
+        self._ct += 1
+        rc = self.L.ko_add_row(self.h, namespace_id, _b(obj), _b(rel), _b(subject_id), ss_ns_id, _b(ss_obj),
+                               _b(ss_rel), commit_time)
+        if rc:
+            raise OracleError(rc)
+
+    def add_tuple(self, t):
+        """InsertRelationTuple: namespace names resolved to ids (relationtuples.go:82-126)"""
+        kind, sid, sns, sobj, srel = subject_args(t)
+        if kind == SUBJECT_ID:
+            self.add_row(self.ns_id(t["namespace"]), t["object"], t["relation"], subject_id=sid)
+        else:
+            self.add_row(self.ns_id(t["namespace"]), t["object"], t["relation"], ss_ns_id=self.ns_id(sns),
+                         ss_obj=sobj, ss_rel=srel)
+
+    def add_columnar(self, cols):
+        """cols: dict of numpy arrays in the ketogpu_row_batch layout"""
+        n = len(cols["namespace_id"])
+        p = lambda a: None if a is None else a.ctypes.data
+        rc = self.L.ko_add_rows_columnar(
+            self.h, n, p(cols["namespace_id"]), p(cols["object_data"]), p(cols["object_off"]),
+            p(cols["relation_data"]), p(cols["relation_off"]), p(cols["subject_kind"]),
+            p(cols["subject_id_data"]), p(cols["subject_id_off"]), p(cols["ss_namespace_id"]),
+            p(cols["ss_object_data"]), p(cols["ss_object_off"]), p(cols["ss_relation_data"]),
+            p(cols["ss_relation_off"]), p(cols.get("commit_time")))
+        if rc:
+            raise OracleError(rc)
+
+    def finalize(self, presorted=False):
+        rc = self.L.ko_finalize(self.h, 1 if presorted else 0)
+        if rc:
+            raise OracleError(rc)
+        return self
+
+    def check(self, ns, obj, rel, subject):
+        kind, sid, sns, sobj, srel = subject_args(subject)
+        out = C.c_int(0)
+        rc = self.L.ko_check(self.h, _b(ns), _b(obj), _b(rel), kind, _b(sid), _b(sns), _b(sobj), _b(srel),
+                             C.byref(out))
+        if rc:
+            raise OracleError(rc)
+        return bool(out.value)
+
+    def check_batch(self, reqs, nthreads=1):
+        """reqs: list of (ns, obj, rel, subject dict) -> list of bools"""
+        import numpy as np
+        n = len(reqs)
+        keep = []
+
+        def arr(vals):
+            a = (C.c_char_p * n)(*[_b(v) for v in vals])
+            keep.append(a)
+            return a
+
+        subj = [subject_args(r[3]) for r in reqs]
+        kinds = (C.c_int * n)(*[s[0] for s in subj])
+        allowed = np.zeros(n, dtype=np.uint8)
+        status = np.zeros(n, dtype=np.int32)
+        self.L.ko_check_batch(self.h, n, arr([r[0] for r in reqs]), arr([r[1] for r in reqs]),
+                              arr([r[2] for r in reqs]), kinds, arr([s[1] for s in subj]), arr([s[2] for s in subj]),
+                              arr([s[3] for s in subj]), arr([s[4] for s in subj]), nthreads,
+                              allowed.ctypes.data, status.ctypes.data)
+        if status.any():
+            raise OracleError(int(status[status != 0][0]))
+        return allowed.astype(bool)
+
+    def expand(self, subject, max_depth):
+        kind, sid, sns, sobj, srel = subject_args(subject)
+        out = C.c_void_p()
+        rc = self.L.ko_expand(self.h, kind, _b(sid), _b(sns), _b(sobj), _b(srel), max_depth, C.byref(out))
+        if rc:
+            raise OracleError(rc)
+        s = C.string_at(out.value).decode("utf-8")
+        self.L.ko_free(out)
+        return json.loads(s)
+
+    def get_page(self, ns, obj, rel, page=1):
+        out, nxt = C.c_void_p(), C.c_int(0)
+        rc = self.L.ko_get_page(self.h, _b(ns), _b(obj), _b(rel), page, C.byref(out), C.byref(nxt))
+        if rc:
+            raise OracleError(rc)
+        s = C.string_at(out.value).decode("utf-8")
+        self.L.ko_free(out)
+        return json.loads(s), bool(nxt.value)
+
+
+def store_from_case(case):
+    st = Store([(n["name"], n["id"]) for n in case["namespaces"]], case.get("page_size", 100))
+    for t in case["tuples"]:
+        st.add_tuple(t)
+    return st.finalize()

@@ -1,0 +1,162 @@
+"""CPU tests of the product's host side: the C ABI loads and exports every symbol
+include/ketogpu.h declares; the snapshot loader; BuildTree; and the check formula
+over the snapshot's device graph (X(root) ∩ rev(target)) against the
+oracle.  No GPU work is launched here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from keto_amd import _lib as L
+from keto_amd import expand, persistence
+from keto_amd import relationtuple as rt
+from keto_amd.snapshot import Snapshot
+from oracle import oracle as O
+from tests import randgraph
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "ketogpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ketogpu_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in L.SIGNATURES, f"{s} lacks a ctypes signature"
+    assert lib.ketogpu_abi_version() == 1
+
+
+def test_builder_rejects_unsorted_rows_and_duplicate_namespaces():
+    rows = [(1, "b", "r", "u", None, None, None), (1, "a", "r", "u", None, None, None),
+            (1, "b", "r", "v", None, None, None)]
+    with pytest.raises(L.KetoError) as e:
+        Snapshot.from_rows([("n", 1)], rows, sort=False)
+    assert e.value.code == L.EINVAL
+    Snapshot.from_rows([("n", 1)], rows, sort=True)  # KETOGPU_BUILD_SORT accepts any order
+    with pytest.raises(L.KetoError):
+        Snapshot([("n", 1), ("n", 2)])
+    with pytest.raises(L.KetoError):
+        Snapshot([("n", 1), ("m", 1)])
+
+
+def _snapshot_from_case(c):
+    ns = [(n["name"], n["id"]) for n in c["namespaces"]]
+    store = persistence.TupleStore(ns, page_size=c["page_size"])
+    for t in c["tuples"]:
+        store.insert(rt.InternalRelationTuple.from_dict(t))
+    return Snapshot.from_store(store, batch_rows=2)  # tiny batches exercise streaming
+
+
+def test_expand_matches_reference_assertions(golden_cases):
+    for c in golden_cases:
+        ex = expand.Engine(_snapshot_from_case(c))
+        for e in c["expands"]:
+            subj = rt.subject_from_dict(e)
+            if e["expected_error"]:
+                with pytest.raises(expand.NotFound):
+                    ex.BuildTree(subj, e["max_depth"])
+                continue
+            t = ex.BuildTree(subj, e["max_depth"])
+            assert (t.to_node() if t else None) == e["expected"], (c["name"], e)
+            import json
+            assert json.loads(ex.build_tree_json(subj, e["max_depth"])) == e["expected"]
+
+
+def _reach(g, root):
+    fo, fc = g["fint_off"], g["fint_col"]
+    seen, stack = set(), list(fc[fo[root]:fo[root + 1]])
+    while stack:
+        v = int(stack.pop())
+        if v in seen:
+            continue
+        seen.add(v)
+        stack.extend(fc[fo[v]:fo[v + 1]])
+    return seen
+
+
+def formula(snap, g, ns, o, r, subj):
+    try:
+        root, target = snap.resolve(ns, o, r, rt.subject_from_dict(subj))
+    except L.KetoError as e:
+        assert e.code == L.ENOTFOUND  # dynamic root: evaluated by the engine only
+        return None
+    if root == L.NODE_NONE or target == L.NODE_NONE:
+        return False
+    rev = g["rev_col"][g["rev_off"][target]:g["rev_off"][target + 1]]
+    if root in set(int(x) for x in rev):
+        return True
+    x = _reach(g, root)
+    return any(int(v) in x for v in rev)
+
+
+@pytest.mark.parametrize("seed,page_size,poison,empty_ns", [(11, 100, False, False), (12, 3, True, False),
+                                                             (13, 2, True, True), (14, 1, False, True)])
+def test_check_formula_over_snapshot_graph(seed, page_size, poison, empty_ns):
+    namespaces, rows = randgraph.make_graph(seed, n_rows=250, poison=poison, empty_ns=empty_ns)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=page_size, sort=True)
+    assert snap.stats()["num_ambiguous_nodes"] == 0
+    g = snap.graph()
+    orc = randgraph.oracle_store(namespaces, rows, page_size)
+    checked = 0
+    for (ns, o, r, subj) in randgraph.make_requests(seed, namespaces, rows, n=300):
+        got = formula(snap, g, ns, o, r, subj)
+        if got is None:
+            continue
+        assert got == orc.check(ns, o, r, subj), (ns, o, r, subj)
+        checked += 1
+    assert checked > 200
+
+
+@pytest.mark.parametrize("seed,page_size,poison,collide", [(21, 100, False, False), (22, 2, True, False),
+                                                            (23, 3, True, True), (24, 1, False, True)])
+def test_expand_matches_oracle_on_random_tables(seed, page_size, poison, collide):
+    namespaces, rows = randgraph.make_graph(seed, n_rows=200, poison=poison, collide=collide)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=page_size, sort=True)
+    orc = randgraph.oracle_store(namespaces, rows, page_size)
+    ex = expand.Engine(snap)
+    for (ns, o, r, subj) in randgraph.make_requests(seed, namespaces, rows, n=80):
+        for s in (subj, {"subject_set": {"namespace": ns, "object": o, "relation": r}}):
+            for depth in (0, 1, 2, 3, 100):
+                try:
+                    want, werr = orc.expand(s, depth), None
+                except O.OracleError as e:
+                    want, werr = None, e.kind
+                try:
+                    t = ex.BuildTree(rt.subject_from_dict(s), depth)
+                    got, gerr = (t.to_node() if t else None), None
+                except expand.NotFound:
+                    got, gerr = None, "not_found"
+                assert (got, gerr) == (want, werr), (s, depth)
+
+
+def test_snapshot_stats_and_classes():
+    ns = [("n", 1)]
+    rows = [(1, "doc", "viewer", None, 1, "g", "member"), (1, "doc", "viewer", "alice", None, None, None),
+            (1, "g", "member", "bob", None, None, None), (1, "g", "member", None, 1, "h", "member"),
+            (1, "h", "member", "carol", None, None, None)]
+    snap = Snapshot.from_rows(ns, rows)
+    st = snap.stats()
+    assert st["num_rows"] == 5 and st["num_groups"] == 3
+    assert st["num_expandable"] == 3 and st["num_interior"] == 2  # g, h interior; doc a source
+    g = snap.graph()
+    assert g["Ni"] == 2 and g["Nx"] == 3
+    root, target = snap.resolve("n", "doc", "viewer", rt.SubjectID("carol"))
+    assert root != L.NODE_NONE and target != L.NODE_NONE
+    assert snap.resolve("n", "doc", "viewer", rt.SubjectID("nobody"))[1] == L.NODE_NONE
+    assert snap.resolve("zz", "doc", "viewer", rt.SubjectID("carol"))[0] == L.NODE_NONE
+    with pytest.raises(L.KetoError):
+        snap.resolve("n", "doc", "viewer", None)
+    # fint rows are sorted and interior-only; rev lists sorted
+    fo, fc = g["fint_off"], g["fint_col"]
+    for v in range(g["Nx"]):
+        row = fc[fo[v]:fo[v + 1]]
+        assert np.all(row < g["Ni"]) and np.all(np.diff(row.astype(np.int64)) > 0)
