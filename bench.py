@@ -1,0 +1,205 @@
+"""bench.py — batched permission checks on MI355X (BASELINE.json metric, config #2).
+
+Workload (BASELINE.json configs[1]): synthetic RBAC, 10M users, 100k
+nested groups, 50M tuples, 1M checks docs:d#viewer@u per GPU (half constructed
+positives), seed 0x4B45544F.  The graph is replicated on every GPU (it fits 288 GB many
+times over) and each rank checks its own 1M requests: no data-path collective, weak
+scaling.  A step = one ketogpu_queries_run over the rank's 1M HBM-resident requests.
+
+    python bench.py [--gpus N --steps K --warmup W] [--small] [--no-cpu-baseline]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (see the contract in README/DESIGN.md).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch  # first: one HIP runtime in the process (libketogpu binds to torch's)
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "permission checks/sec (batched, whole node) + traversal HBM GB/s vs roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--small", action="store_true", help="1/100-size graph for quick runs (not the metric)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU work of the baseline sample")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                   help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
+    return p.parse_args()
+
+
+def dist_init(n):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    a = parse()
+    rank, world, local = dist_init(a.gpus)
+    from keto_amd import check, synth
+    from keto_amd.snapshot import Snapshot
+
+    scale = 100 if a.small else 1
+    sizes = dict(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
+                 tuples=50_000_000 // scale, checks=1_000_000 // (10 if a.small else 1))
+    t0 = time.time()
+    # every rank builds the same graph (same seed) and draws its own 1M requests
+    w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1 + rank)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    t_snap = time.time() - t0
+    roots, targets = w.resolve(snap)
+    eng = check.Engine(snap, device=local)
+    t0 = time.time()
+    q = eng.upload(roots, targets)
+    t_h2d = time.time() - t0
+
+    for _ in range(a.warmup):
+        q.run()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        q.run()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt = max_over_ranks(dt, world)
+    st = eng.last_stats()
+    allowed = q.download()
+
+    # PCIe-inclusive rate of one full host-to-host call (not `value`)
+    t0 = time.perf_counter()
+    eng.check_ids(roots, targets)
+    t_host = time.perf_counter() - t0
+
+    n = len(roots)
+    value = n * world * a.steps / dt
+    out = None
+    if rank == 0:
+        push_gbps = st["bytes_push"] / (st["ms_push"] * 1e-3) / 1e9 if st["ms_push"] > 0 else 0.0
+        pull_gbps = st["bytes_pull"] / (st["ms_pull"] * 1e-3) / 1e9 if st["ms_pull"] > 0 else 0.0
+        dominant = "push" if st["ms_push"] >= st["ms_pull"] else "pull"
+        achieved = push_gbps if dominant == "push" else pull_gbps
+        n_launch = st["push_launches"] if dominant == "push" else st["rounds"]
+        traffic = None
+        if os.path.exists(a.traffic):
+            try:
+                tr = json.load(open(a.traffic))
+                traffic = tr.get("kernels", {}).get(f"{dominant}_kernel_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": "expand_kernel" if dominant == "push" else "pull_kernel",
+                "bytes_per_launch": int((st["bytes_push"] if dominant == "push" else st["bytes_pull"]) / max(n_launch, 1)),
+                "ms_per_launch": round((st["ms_push"] if dominant == "push" else st["ms_pull"]) / max(n_launch, 1), 4),
+                "push": {"GBps": round(push_gbps, 1), "ms": round(st["ms_push"], 3), "bytes": st["bytes_push"],
+                         "launches": st["push_launches"]},
+                "pull": {"GBps": round(pull_gbps, 1), "ms": round(st["ms_pull"], 3), "bytes": st["bytes_pull"]}}
+        cpu = None
+        parity = None
+        if not a.no_cpu_baseline:
+            cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds)
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 ids / u64 bitmasks (integer)",
+            "data": "synthetic: config #2 RBAC generator (keto_amd/csrc/synth.cpp), seed 0x4B45544F",
+            "config": {"workload": "config2_rbac" + ("_small" if a.small else ""), **sizes,
+                       "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
+                       "parallelism": f"query-shard x{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "parity": parity,
+            "engine": {k: st[k] for k in ("rounds", "levels", "frontier_entries", "interior_edges", "rev_edges",
+                                          "touched", "ms_total")},
+            "allowed_fraction": round(float(allowed.mean()), 4),
+            "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2), "h2d_queries": round(t_h2d, 4)},
+            "pcie_inclusive_checks_per_s": round(n / t_host, 1),
+            "snapshot": {k: v for k, v in snap.stats().items() if k.startswith("num_")},
+        }
+        print(json.dumps(out), flush=True)
+    barrier(world)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def cpu_baseline(w, gpu_allowed, seconds):
+    """The oracle (exact restatement of the reference DFS) on host cores over a bounded
+    sample of the same requests; its answers double as a bit-exact parity sample."""
+    from oracle import oracle as O
+    from tests import randgraph
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
+    t_build = time.time() - t0
+    rng = np.random.default_rng(1)
+    idx = rng.permutation(w.n_checks)
+    probe = idx[:2000]
+    t0 = time.perf_counter()
+    ans = orc.check_batch(w.requests(probe), nthreads=threads)
+    tp = time.perf_counter() - t0
+    rate = len(probe) / tp
+    m = int(min(len(idx), max(len(probe), rate * seconds)))
+    sample = idx[:m]
+    t0 = time.perf_counter()
+    ans = orc.check_batch(w.requests(sample), nthreads=threads)
+    ts = time.perf_counter() - t0
+    mism = int((ans != gpu_allowed[sample]).sum())
+    del O
+    return ({"value": round(len(sample) / ts, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+             "sample": f"{len(sample)} of the {w.n_checks} config-2 requests (uniform sample), full 50M-tuple graph; "
+                       f"oracle/keto_oracle.c on {threads} threads of {cpu_model()}; store build {t_build:.1f}s"},
+            {"sample": len(sample), "mismatches": mism})
+
+
+if __name__ == "__main__":
+    main()

@@ -90,6 +90,7 @@ extern "C" {
 typedef struct {
     uint64_t users, groups, docs, tuples, checks, seed;
     double zipf_s, member_mean;
+    uint64_t check_seed; /* 0: checks continue the graph's random stream */
 } ks_rbac_params;
 
 typedef struct {
@@ -238,6 +239,7 @@ ks_rbac *ks_rbac_generate(const ks_rbac_params *p) {
         for (uint32_t u : du) row_id(2, 'd', d, "viewer", u);
     }
     // ---- checks
+    if (p->check_seed) rng = Rng(p->check_seed);
     const uint64_t C = p->checks;
     w->chk_doc.resize(C);
     w->chk_user.resize(C);

@@ -19,7 +19,7 @@ _slib = None
 
 class Params(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("users", "groups", "docs", "tuples", "checks", "seed")] + [
-        ("zipf_s", C.c_double), ("member_mean", C.c_double)]
+        ("zipf_s", C.c_double), ("member_mean", C.c_double), ("check_seed", C.c_uint64)]
 
 
 class View(C.Structure):
@@ -110,5 +110,6 @@ class Workload:
 
 
 def rbac(users=10_000_000, groups=100_000, docs=2_000_000, tuples=50_000_000, checks=1_000_000, seed=SEED,
-         zipf_s=1.1, member_mean=3.0):
-    return Workload(Params(users, groups, docs, tuples, checks, seed, zipf_s, member_mean))
+         zipf_s=1.1, member_mean=3.0, check_seed=0):
+    """check_seed = 0: checks drawn from the graph's own random stream"""
+    return Workload(Params(users, groups, docs, tuples, checks, seed, zipf_s, member_mean, check_seed))
