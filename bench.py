@@ -72,6 +72,11 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -95,9 +100,11 @@ def main():
     # every rank builds the same graph (same seed) and draws its own 1M requests
     w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1 + rank)
     t_gen = time.time() - t0
+    log(f"generated {w.counts} in {t_gen:.1f}s")
     t0 = time.time()
     snap = Snapshot.from_columns(w.namespaces, w.columns)
     t_snap = time.time() - t0
+    log(f"snapshot built in {t_snap:.1f}s")
     roots, targets = w.resolve(snap)
     eng = check.Engine(snap, device=local)
     t0 = time.time()
@@ -113,6 +120,7 @@ def main():
     barrier(world)
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world)
+    log(f"{a.steps} steps in {dt:.4f}s")
     st = eng.last_stats()
     allowed = q.download()
 
@@ -181,6 +189,7 @@ def cpu_baseline(w, gpu_allowed, seconds):
     t0 = time.time()
     orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
     t_build = time.time() - t0
+    log(f"oracle store built in {t_build:.1f}s")
     rng = np.random.default_rng(1)
     idx = rng.permutation(w.n_checks)
     probe = idx[:2000]
