@@ -133,26 +133,29 @@ def main():
     value = n * world * a.steps / dt
     out = None
     if rank == 0:
-        push_gbps = st["bytes_push"] / (st["ms_push"] * 1e-3) / 1e9 if st["ms_push"] > 0 else 0.0
-        pull_gbps = st["bytes_pull"] / (st["ms_pull"] * 1e-3) / 1e9 if st["ms_pull"] > 0 else 0.0
-        dominant = "push" if st["ms_push"] >= st["ms_pull"] else "pull"
-        achieved = push_gbps if dominant == "push" else pull_gbps
-        n_launch = st["push_launches"] if dominant == "push" else st["rounds"]
+        # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time
+        fam = {
+            "unit_kernel": (st["bytes_unit"], st["ms_unit"], 1 if st["ms_unit"] > 0 else 0),
+            "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - (1 if st["ms_unit"] > 0 else 0)),
+            "pull_kernel": (st["bytes_pull"], st["ms_pull"], st["rounds"]),
+        }
+        gbps = {k: (b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0) for k, (b, ms, _) in fam.items()}
+        dominant = max(fam, key=lambda k: fam[k][1])
+        b_dom, ms_dom, n_launch = fam[dominant]
+        achieved = gbps[dominant]
         traffic = None
         if os.path.exists(a.traffic):
             try:
                 tr = json.load(open(a.traffic))
-                traffic = tr.get("kernels", {}).get(f"{dominant}_kernel_bytes_per_launch")
+                if tr.get("workload") == ("config2_rbac" + ("_small" if a.small else "")):
+                    traffic = tr.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": "expand_kernel" if dominant == "push" else "pull_kernel",
-                "bytes_per_launch": int((st["bytes_push"] if dominant == "push" else st["bytes_pull"]) / max(n_launch, 1)),
-                "ms_per_launch": round((st["ms_push"] if dominant == "push" else st["ms_pull"]) / max(n_launch, 1), 4),
-                "push": {"GBps": round(push_gbps, 1), "ms": round(st["ms_push"], 3), "bytes": st["bytes_push"],
-                         "launches": st["push_launches"]},
-                "pull": {"GBps": round(pull_gbps, 1), "ms": round(st["ms_pull"], 3), "bytes": st["bytes_pull"]}}
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": dominant,
+                "bytes_per_launch": int(b_dom / max(n_launch, 1)), "ms_per_launch": round(ms_dom / max(n_launch, 1), 4),
+                "kernels": {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": b, "launches": n}
+                            for k, (b, ms, n) in fam.items() if ms > 0}}
         cpu = None
         parity = None
         if not a.no_cpu_baseline:
@@ -166,8 +169,8 @@ def main():
                        "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
                        "parallelism": f"query-shard x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
-            "engine": {k: st[k] for k in ("rounds", "levels", "frontier_entries", "interior_edges", "rev_edges",
-                                          "touched", "ms_total")},
+            "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
+                                          "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total")},
             "allowed_fraction": round(float(allowed.mean()), 4),
             "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2), "h2d_queries": round(t_h2d, 4)},
             "pcie_inclusive_checks_per_s": round(n / t_host, 1),

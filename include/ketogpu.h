@@ -238,6 +238,14 @@ typedef struct {
     double ms_total;            /* device time, first to last kernel              */
     uint64_t push_launches;
     uint64_t overflow_retries;
+    /* LDS unit path (one launch: whole BFS + pull per 16-request unit in LDS) */
+    uint64_t spilled_units;     /* units that spilled out of an LDS table (all passes) */
+    uint64_t unit_rows;         /* rows opened (forward offsets + reverse offsets) */
+    uint64_t unit_edges;        /* interior edges scanned                         */
+    uint64_t unit_rev;          /* reverse entries scanned                        */
+    uint64_t bytes_unit;        /* algorithmic HBM bytes of the unit kernel       */
+    double ms_unit;             /* device time of the unit kernels (hipEvent)     */
+    uint64_t spilled_requests;  /* single requests run on the global path         */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

@@ -346,6 +346,576 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(uint64_t *vis, uint32_t N
     vis[(size_t)(k >> 32) * Ni + (uint32_t)k] = 0;
 }
 
+// ------------------------------------------------------- LDS unit traversal
+// The fast path.  One 256-thread workgroup takes a UNIT of U consecutive requests and
+// runs the whole check for them — seed, every BFS level over the interior subgraph,
+// and the rev(t) pull — with the unit's visited and pending bits in an LDS hash table
+// (node -> U visited bits | U pending bits).  HBM only serves read-only graph rows: no
+// global atomics, no state to reset, no host round trip per level.  Units whose
+// closure outgrows the table (or that have a dynamic root) SPILL: 16-request units are
+// re-run as 4-request units, those as single requests, and only single requests whose
+// closure exceeds the table go to the global multi-word engine.
+constexpr int kHashLog = 11;
+constexpr int kHash = 1 << kHashLog;
+constexpr int kHashMax = kHash * 3 / 4;
+constexpr int kChunk = kBlock;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr int kUnitMax = 16;
+
+struct UnitShared {
+    uint32_t key[kHash];
+    uint32_t st[kHash];  // visited bits (low 16) | pending bits (high 16)
+    uint16_t cur_slot[kHash], cur_mask[kHash], nxt_slot[kHash];
+    uint64_t c_begin[kChunk];
+    uint32_t c_pre[kChunk + 1];
+    uint16_t c_mask[kChunk];
+    uint32_t wave_sum[kBlock / 64];
+    uint32_t root[kUnitMax], target[kUnitMax];
+    uint32_t n_used, n_nxt, spill, res;
+    unsigned long long cnt_rows, cnt_edges, cnt_rev;
+};
+
+__device__ __forceinline__ uint32_t hslot(uint32_t u) { return (u * 2654435761u) >> (32 - kHashLog); }
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t bal) {
+    return (uint32_t)__popcll(bal & ((1ull << (threadIdx.x & 63)) - 1));
+}
+
+// exclusive block scan of one u32 per thread; returns the total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *out_pre, UnitShared &S) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+    }
+    if (lane == 63) S.wave_sum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; i++) {
+        uint32_t s = S.wave_sum[i];
+        base += i < wv ? s : 0;
+        total += s;
+    }
+    out_pre[tid] = base + x - v;
+    if (tid == 0) out_pre[kBlock] = total;
+    __syncthreads();
+    return total;
+}
+
+// Insert u with mask m (want = this lane has an edge).  Called by whole waves: the
+// occupancy counter and the next-frontier list are advanced with one LDS atomic per wave.
+__device__ __forceinline__ void unit_push(const DevGraph &g, UnitShared &S, bool want, uint32_t u, uint32_t m,
+                                          const uint32_t *has_kids, uint64_t *flag_word, int shift) {
+    int h = -1;
+    bool inserted = false;
+    if (want) {
+        uint32_t hh = hslot(u);
+        for (int p = 0; p < kHash; p++, hh = (hh + 1) & (kHash - 1)) {
+            uint32_t kv = S.key[hh];
+            if (kv == kEmpty) {
+                uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
+                if (prev == kEmpty) {
+                    inserted = true;
+                    h = (int)hh;
+                    break;
+                }
+                kv = prev;
+            }
+            if (kv == u) {
+                h = (int)hh;
+                break;
+            }
+        }
+        if (h < 0) S.spill = 1;  // table full
+    }
+    uint64_t bal = __ballot(inserted);
+    if (bal && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)bal) - 1))
+        if (atomicAdd(&S.n_used, (uint32_t)__popcll(bal)) + (uint32_t)__popcll(bal) > (uint32_t)kHashMax) S.spill = 1;
+    bool app = false;
+    if (h >= 0) {
+        uint32_t old = atomicOr(&S.st[h], m);
+        uint32_t newly = m & ~old & 0xFFFFu;
+        if (newly) {
+            if (g.row_amb && bit_of(g.row_amb, u))
+                atomicOr((unsigned long long *)flag_word, (unsigned long long)newly << shift);
+            if (bit_of(has_kids, u)) {
+                uint32_t o2 = atomicOr(&S.st[h], newly << 16);
+                app = !(o2 >> 16);
+            }
+        }
+    }
+    uint64_t ab = __ballot(app);
+    if (ab) {
+        int leader = __ffsll((unsigned long long)ab) - 1;
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&S.n_nxt, (uint32_t)__popcll(ab));
+        base = __shfl(base, leader, 64);
+        if (app) S.nxt_slot[base + lanes_below(ab)] = (uint16_t)h;
+    }
+}
+
+__device__ __forceinline__ int unit_lookup(const UnitShared &S, uint32_t v) {
+    uint32_t h = hslot(v);
+    for (int p = 0; p < kHash; p++, h = (h + 1) & (kHash - 1)) {
+        uint32_t kv = S.key[h];
+        if (kv == v) return (int)h;
+        if (kv == kEmpty) return -1;
+    }
+    return -1;
+}
+
+// expand the chunk held in S.c_begin / S.c_pre / S.c_mask (entries [0, k)); the loop
+// count is block-uniform so every wave reaches the aggregated atomics together
+__device__ __forceinline__ void unit_expand_chunk(const DevGraph &g, UnitShared &S, uint32_t k, uint32_t total,
+                                                  const uint32_t *has_kids, uint64_t *flag_word, int shift,
+                                                  uint64_t &edges) {
+    for (uint32_t base = 0; base < total; base += kBlock) {
+        uint32_t e = base + threadIdx.x;
+        bool want = e < total;
+        uint32_t u = 0, m = 0;
+        if (want) {
+            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (S.c_pre[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            u = g.fint_col[S.c_begin[lo] + (e - S.c_pre[lo])];
+            m = S.c_mask[lo];
+            edges++;
+        }
+        unit_push(g, S, want, u, m, has_kids, flag_word, shift);
+    }
+}
+
+// U requests per unit.  Pass 1 (parents == nullptr): unit b = requests [U*b, U*b+U).
+// Later passes split the spilled units of the previous pass (size U*fan) into `fan`
+// units each: unit b = child fan*parents[b/fan] + b%fan.  Spilled units are appended to
+// spill_out (in units of U).
+template <int U>
+__global__ __launch_bounds__(kBlock) void unit_kernel(DevGraph g, const uint32_t *has_kids, const uint32_t *roots,
+                                                      const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                      uint64_t *flags, const uint32_t *parents, uint32_t fan,
+                                                      uint32_t *spill_out, unsigned int *spill_count,
+                                                      unsigned long long *stats, unsigned long long *stamps) {
+    __shared__ UnitShared S;
+    const int tid = threadIdx.x;
+    // diagnostic build only (stamps != nullptr): s_memtime at phase boundaries
+    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    uint32_t n_levels = 0;
+    if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
+    const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
+    const uint64_t c0 = unit * U;
+    uint64_t *flag_word = &flags[c0 >> 6];
+    const int shift = (int)(c0 & 63);
+    const unsigned long long unit_bits = (U == 64 ? ~0ull : ((1ull << U) - 1)) << shift;
+    for (int i = tid; i < kHash; i += kBlock) {
+        S.key[i] = kEmpty;
+        S.st[i] = 0;
+    }
+    if (tid == 0) {
+        S.n_used = S.n_nxt = S.spill = S.res = 0;
+        S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
+    }
+    if (tid < U) {
+        uint64_t c = c0 + tid;
+        uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+        if (c < n) {
+            r = roots[c];
+            t = targets[c];
+        }
+        if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;  // nothing can match
+        S.root[tid] = r;
+        S.target[tid] = t;
+    }
+    __syncthreads();
+    if (tid < U && S.root[tid] != KETOGPU_NODE_NONE && S.root[tid] >= kDynBase) S.spill = 1;
+    __syncthreads();
+    if (S.spill) {
+        if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    uint64_t rows = 0, edges = 0, rev = 0;
+    if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
+    // level 0: the roots' interior successors (roots themselves are not visited)
+    {
+        uint32_t d = 0;
+        if (tid < U) {
+            uint32_t r = S.root[tid];
+            uint64_t b = 0;
+            if (r != KETOGPU_NODE_NONE) {
+                b = g.fint_off[r];
+                d = (uint32_t)(g.fint_off[r + 1] - b);
+                rows++;
+                if (g.row_amb && bit_of(g.row_amb, r))
+                    atomicOr((unsigned long long *)flag_word, (unsigned long long)1 << (shift + tid));
+            }
+            S.c_begin[tid] = b;
+            S.c_mask[tid] = (uint16_t)(1u << tid);
+        }
+        uint32_t total = block_excl_scan(d, S.c_pre, S);
+        unit_expand_chunk(g, S, U, total, has_kids, flag_word, shift, edges);
+    }
+    if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
+    // levels until no request of the unit gains a bit (no depth cutoff)
+    for (;;) {
+        __syncthreads();
+        uint32_t cnt = S.n_nxt;
+        if (S.spill || !cnt) break;
+        n_levels++;
+        for (uint32_t i = tid; i < cnt; i += kBlock) {
+            uint16_t s = S.nxt_slot[i];
+            S.cur_slot[i] = s;
+            S.cur_mask[i] = (uint16_t)(atomicAnd(&S.st[s], 0xFFFFu) >> 16);
+        }
+        __syncthreads();
+        if (tid == 0) S.n_nxt = 0;
+        for (uint32_t base = 0; base < cnt; base += kChunk) {
+            uint32_t k = cnt - base < (uint32_t)kChunk ? cnt - base : (uint32_t)kChunk;
+            uint32_t d = 0;
+            if ((uint32_t)tid < k) {
+                uint32_t v = S.key[S.cur_slot[base + tid]];
+                uint64_t b = g.fint_off[v];
+                d = (uint32_t)(g.fint_off[v + 1] - b);
+                S.c_begin[tid] = b;
+                S.c_mask[tid] = S.cur_mask[base + tid];
+                rows++;
+            }
+            uint32_t total = block_excl_scan(d, S.c_pre, S);
+            unit_expand_chunk(g, S, k, total, has_kids, flag_word, shift, edges);
+            __syncthreads();
+        }
+    }
+    if (S.spill) {
+        if (tid == 0) {
+            spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+            atomicAnd((unsigned long long *)flag_word, ~unit_bits);
+        }
+        return;
+    }
+    if (stamp) stamp[3] = __builtin_amdgcn_s_memtime();
+    // pull: kBlock / U lanes per request over rev(target)
+    {
+        constexpr int L = kBlock / U;
+        const int j = tid / L, l = tid % L;
+        bool ok = false;
+        uint32_t r = S.root[j], t = S.target[j];
+        if (r != KETOGPU_NODE_NONE) {
+            uint64_t b = g.rev_off[t], e = g.rev_off[t + 1];
+            if (l == 0) rows++;
+            for (uint64_t p = b + l; p < e && !ok; p += L) {
+                uint32_t v = g.rev_col[p];
+                rev++;
+                if (v == r) {
+                    ok = true;
+                } else if (v < g.Ni) {
+                    int s = unit_lookup(S, v);
+                    ok = s >= 0 && ((S.st[s] >> j) & 1u);
+                }
+            }
+        }
+        if (ok) atomicOr(&S.res, 1u << j);
+    }
+    atomicAdd(&S.cnt_rows, (unsigned long long)rows);
+    atomicAdd(&S.cnt_edges, (unsigned long long)edges);
+    atomicAdd(&S.cnt_rev, (unsigned long long)rev);
+    __syncthreads();
+    if (stamp) {
+        stamp[4] = __builtin_amdgcn_s_memtime();
+        stamp[5] = n_levels;
+        stamp[6] = S.n_used;
+        stamp[7] = 1;  // completed (not spilled)
+    }
+    if (tid == 0) {
+        if (S.res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)S.res << shift);
+        atomicAdd(&stats[1], S.cnt_rows);
+        atomicAdd(&stats[2], S.cnt_edges);
+        atomicAdd(&stats[3], S.cnt_rev);
+    }
+}
+
+// ------------------------------------------------- wave-synchronous units
+// Same algorithm as unit_kernel with ONE WAVE per unit: the four waves of a workgroup
+// own four independent LDS partitions, so a BFS level needs no workgroup barrier, only
+// in-order wave execution (wave_sync orders the LDS traffic between phases).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int U, int HLOG>
+struct WaveLDS {
+    static constexpr int H = 1 << HLOG;
+    static constexpr int F = H / 2;  // frontier list capacity
+    uint32_t key[H];
+    uint32_t st[H];  // visited bits [0, U) | pending bits [16, 16 + U)
+    uint16_t cur_slot[F], nxt_slot[F], cur_mask[F];
+    uint64_t c_begin[64];
+    uint32_t c_pre[65];
+    uint16_t c_mask[64];
+    uint32_t root[U], target[U];
+    uint32_t n_used, n_nxt, spill, pad;
+};
+
+template <int U, int HLOG>
+__device__ __forceinline__ uint32_t wslot(uint32_t u) {
+    return (u * 2654435761u) >> (32 - HLOG);
+}
+
+template <int U, int HLOG>
+__device__ __forceinline__ void wave_push(const DevGraph &g, WaveLDS<U, HLOG> &S, bool want, uint32_t u, uint32_t m,
+                                          const uint32_t *has_kids, uint64_t *flag_word, int shift, int lane) {
+    constexpr int H = 1 << HLOG;
+    int h = -1;
+    bool inserted = false;
+    if (want) {
+        uint32_t hh = wslot<U, HLOG>(u);
+        for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
+            uint32_t kv = S.key[hh];
+            if (kv == kEmpty) {
+                uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
+                if (prev == kEmpty) {
+                    inserted = true;
+                    h = (int)hh;
+                    break;
+                }
+                kv = prev;
+            }
+            if (kv == u) {
+                h = (int)hh;
+                break;
+            }
+        }
+        if (h < 0) S.spill = 1;
+    }
+    uint64_t bal = __ballot(inserted);
+    if (bal && lane == 0) {
+        uint32_t c = (uint32_t)__popcll(bal);
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)(H * 3 / 4)) S.spill = 1;
+    }
+    bool app = false;
+    if (h >= 0) {
+        uint32_t old = atomicOr(&S.st[h], m);
+        uint32_t newly = m & ~old & ((1u << U) - 1);
+        if (newly) {
+            if (g.row_amb && bit_of(g.row_amb, u))
+                atomicOr((unsigned long long *)flag_word, (unsigned long long)newly << shift);
+            if (bit_of(has_kids, u)) {
+                uint32_t o2 = atomicOr(&S.st[h], newly << 16);
+                app = !(o2 >> 16);
+            }
+        }
+    }
+    uint64_t ab = __ballot(app);
+    if (ab) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&S.n_nxt, (uint32_t)__popcll(ab));
+        base = __shfl(base, 0, 64);
+        uint32_t idx = base + (uint32_t)__popcll(ab & ((1ull << lane) - 1));
+        if (app) {
+            if (idx < (uint32_t)WaveLDS<U, HLOG>::F)
+                S.nxt_slot[idx] = (uint16_t)h;
+            else
+                S.spill = 1;
+        }
+    }
+}
+
+// expand up to 64 entries held by the lanes (lane < k: node v, mask m); all lanes call
+template <int U, int HLOG>
+__device__ __forceinline__ void wave_expand(const DevGraph &g, WaveLDS<U, HLOG> &S, uint32_t k, bool have, uint32_t v,
+                                            uint32_t m, const uint32_t *has_kids, uint64_t *flag_word, int shift,
+                                            int lane, uint64_t &rows, uint64_t &edges) {
+    uint32_t d = 0;
+    uint64_t b = 0;
+    if (have) {
+        b = g.fint_off[v];
+        d = (uint32_t)(g.fint_off[v + 1] - b);
+        rows++;
+    }
+    uint32_t x = d;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        uint32_t t = __shfl_up(x, s, 64);
+        if (lane >= s) x += t;
+    }
+    uint32_t total = __shfl(x, 63, 64);
+    S.c_begin[lane] = b;
+    S.c_pre[lane] = x - d;
+    S.c_mask[lane] = (uint16_t)m;
+    wave_sync();
+    for (uint32_t base = 0; base < total; base += 64) {
+        uint32_t e = base + lane;
+        bool want = e < total;
+        uint32_t u = 0, mm = 0;
+        if (want) {
+            uint32_t lo = 0, hi = k;
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (S.c_pre[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            u = g.fint_col[S.c_begin[lo] + (e - S.c_pre[lo])];
+            mm = S.c_mask[lo];
+            edges++;
+        }
+        wave_push<U, HLOG>(g, S, want, u, mm, has_kids, flag_word, shift, lane);
+    }
+    wave_sync();
+}
+
+template <int U, int HLOG>
+__global__ __launch_bounds__(kBlock) void wave_unit_kernel(DevGraph g, const uint32_t *has_kids, const uint32_t *roots,
+                                                           const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                           uint64_t *flags, uint32_t *spill_out,
+                                                           unsigned int *spill_count, unsigned long long *stats) {
+    using L = WaveLDS<U, HLOG>;
+    constexpr int H = L::H;
+    __shared__ L lds[kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    L &S = lds[wv];
+    const uint64_t unit = (uint64_t)blockIdx.x * (kBlock / 64) + wv;
+    const uint64_t c0 = unit * U;
+    if (c0 >= n) return;
+    uint64_t *flag_word = &flags[c0 >> 6];
+    const int shift = (int)(c0 & 63);
+    const unsigned long long unit_bits = ((1ull << U) - 1) << shift;
+    for (int i = lane; i < H; i += 64) {
+        S.key[i] = kEmpty;
+        S.st[i] = 0;
+    }
+    if (lane == 0) S.n_used = S.n_nxt = S.spill = 0;
+    bool dyn = false;
+    uint32_t r = KETOGPU_NODE_NONE;
+    if (lane < U) {
+        uint64_t c = c0 + lane;
+        uint32_t t = KETOGPU_NODE_NONE;
+        if (c < n) {
+            r = roots[c];
+            t = targets[c];
+        }
+        if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
+        dyn = r != KETOGPU_NODE_NONE && r >= kDynBase;
+        S.root[lane] = r;
+        S.target[lane] = t;
+    }
+    if (__ballot(dyn)) {
+        if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    wave_sync();
+    uint64_t rows = 0, edges = 0, rev = 0;
+    {
+        bool have = lane < U && r != KETOGPU_NODE_NONE;
+        if (have && g.row_amb && bit_of(g.row_amb, r))
+            atomicOr((unsigned long long *)flag_word, (unsigned long long)1 << (shift + lane));
+        wave_expand<U, HLOG>(g, S, U, have, r, 1u << (lane & 31), has_kids, flag_word, shift, lane, rows, edges);
+    }
+    for (;;) {
+        uint32_t cnt = S.n_nxt;
+        if (S.spill || !cnt) break;
+        for (uint32_t i = lane; i < cnt; i += 64) {
+            uint16_t s = S.nxt_slot[i];
+            S.cur_slot[i] = s;
+            S.cur_mask[i] = (uint16_t)((atomicAnd(&S.st[s], 0xFFFFu) >> 16) & ((1u << U) - 1));
+        }
+        wave_sync();
+        if (lane == 0) S.n_nxt = 0;
+        wave_sync();
+        for (uint32_t base = 0; base < cnt; base += 64) {
+            uint32_t k = cnt - base < 64u ? cnt - base : 64u;
+            bool have = (uint32_t)lane < k;
+            uint32_t v = 0, m = 0;
+            if (have) {
+                v = S.key[S.cur_slot[base + lane]];
+                m = S.cur_mask[base + lane];
+            }
+            wave_expand<U, HLOG>(g, S, k, have, v, m, has_kids, flag_word, shift, lane, rows, edges);
+        }
+    }
+    if (S.spill) {
+        if (lane == 0) {
+            spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+            atomicAnd((unsigned long long *)flag_word, ~unit_bits);
+        }
+        return;
+    }
+    // pull: 64 / U lanes per request
+    constexpr int LPC = 64 / U;
+    const int j = lane / LPC, l = lane % LPC;
+    bool ok = false;
+    {
+        uint32_t rr = S.root[j], t = S.target[j];
+        if (rr != KETOGPU_NODE_NONE) {
+            uint64_t b = g.rev_off[t], e = g.rev_off[t + 1];
+            if (l == 0) rows++;
+            for (uint64_t p = b + l; p < e && !ok; p += LPC) {
+                uint32_t v = g.rev_col[p];
+                rev++;
+                if (v == rr) {
+                    ok = true;
+                } else if (v < g.Ni) {
+                    uint32_t h = wslot<U, HLOG>(v);
+                    for (int q = 0; q < H; q++, h = (h + 1) & (H - 1)) {
+                        uint32_t kv = S.key[h];
+                        if (kv == v) {
+                            ok = (S.st[h] >> j) & 1u;
+                            break;
+                        }
+                        if (kv == kEmpty) break;
+                    }
+                }
+            }
+        }
+    }
+    uint64_t bal = __ballot(ok);
+    // per-wave statistics
+    for (int s = 32; s; s >>= 1) {
+        rows += __shfl_down(rows, s, 64);
+        edges += __shfl_down(edges, s, 64);
+        rev += __shfl_down(rev, s, 64);
+    }
+    if (lane == 0) {
+        uint32_t res = 0;
+        const uint64_t lm = LPC == 64 ? ~0ull : ((1ull << LPC) - 1);
+        for (int q = 0; q < U; q++)
+            if ((bal >> (q * LPC)) & lm) res |= 1u << q;
+        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << shift);
+        atomicAdd(&stats[1], (unsigned long long)rows);
+        atomicAdd(&stats[2], (unsigned long long)edges);
+        atomicAdd(&stats[3], (unsigned long long)rev);
+    }
+}
+
+// requests of the final spill list (single requests) -> a dense batch for the global path
+__global__ __launch_bounds__(kBlock) void spill_gather_kernel(const uint32_t *ids, uint64_t cnt, const uint32_t *roots,
+                                                              const uint32_t *targets, uint64_t n, uint32_t *sr,
+                                                              uint32_t *stt) {
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= cnt) return;
+    uint64_t c = ids[i];
+    sr[i] = c < n ? roots[c] : KETOGPU_NODE_NONE;
+    stt[i] = c < n ? targets[c] : KETOGPU_NODE_NONE;
+}
+
+__global__ __launch_bounds__(kBlock) void spill_scatter_kernel(const uint32_t *ids, uint64_t cnt, const uint64_t *sa,
+                                                               const uint64_t *sf, uint64_t *allowed, uint64_t *flags) {
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= cnt) return;
+    uint64_t c = ids[i];
+    unsigned long long bit = 1ull << (c & 63);
+    if ((sa[i >> 6] >> (i & 63)) & 1ull) atomicOr((unsigned long long *)&allowed[c >> 6], bit);
+    if ((sf[i >> 6] >> (i & 63)) & 1ull) atomicOr((unsigned long long *)&flags[c >> 6], bit);
+}
+
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 #define HIP_CHECK(x)                                                                                   \
@@ -374,6 +944,16 @@ T *dupload(const std::vector<T> &v) {
 }  // namespace
 
 // --------------------------------------------------------------------- engine
+// A batch as the traversal kernels see it (device pointers)
+struct Batch {
+    const uint32_t *roots = nullptr, *targets = nullptr;
+    uint64_t n = 0;
+    uint64_t *allowed = nullptr, *flags = nullptr;
+    const uint64_t *dyn_int_off = nullptr, *dyn_full_off = nullptr;
+    const uint32_t *dyn_int = nullptr, *dyn_full = nullptr, *dyn_amb = nullptr;
+    bool has_dyn = false;
+};
+
 struct ketogpu_queries {
     uint64_t n = 0;
     uint32_t *d_roots = nullptr, *d_targets = nullptr;
@@ -382,6 +962,21 @@ struct ketogpu_queries {
     uint64_t *d_dyn_int_off = nullptr, *d_dyn_full_off = nullptr;
     uint32_t *d_dyn_int = nullptr, *d_dyn_full = nullptr, *d_dyn_amb = nullptr;
     bool has_dyn = false;
+    Batch batch() const {
+        Batch b;
+        b.roots = d_roots;
+        b.targets = d_targets;
+        b.n = n;
+        b.allowed = d_allowed;
+        b.flags = d_flags;
+        b.dyn_int_off = d_dyn_int_off;
+        b.dyn_full_off = d_dyn_full_off;
+        b.dyn_int = d_dyn_int;
+        b.dyn_full = d_dyn_full;
+        b.dyn_amb = d_dyn_amb;
+        b.has_dyn = has_dyn;
+        return b;
+    }
     ~ketogpu_queries() {
         for (void *p : {(void *)d_roots, (void *)d_targets, (void *)d_allowed, (void *)d_flags, (void *)d_dyn_int_off,
                         (void *)d_dyn_full_off, (void *)d_dyn_int, (void *)d_dyn_full, (void *)d_dyn_amb})
@@ -396,12 +991,45 @@ struct ketogpu_engine {
     std::mutex mu;
     DevGraph g{};
     DevState st{};
+    const uint32_t *has_kids = nullptr;  // bitmap over Ni: interior node with interior successors
     uint64_t Wmax = 0;
     uint64_t *h_ctr = nullptr;  // pinned
     std::vector<void *> owned;
     ketogpu_run_stats last{};
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    bool use_units = true;
+    int wave_u = 8;
+    unsigned long long *stamps = nullptr;  // KETOGPU_STAMPS=1 diagnostic build
+
+    void report_stamps() {
+        std::vector<unsigned long long> h((size_t)65536 * 8);
+        HIP_CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+        double ph[4] = {0, 0, 0, 0}, lv = 0, used = 0;
+        std::vector<double> tot;
+        for (size_t b = 0; b < 65536; b++) {
+            const unsigned long long *s = &h[b * 8];
+            if (s[7] != 1) continue;
+            for (int k = 0; k < 4; k++) ph[k] += (double)(s[k + 1] - s[k]);
+            lv += (double)s[5];
+            used += (double)s[6];
+            tot.push_back((double)(s[4] - s[0]));
+        }
+        if (tot.empty()) return;
+        std::sort(tot.begin(), tot.end());
+        double n = (double)tot.size();
+        fprintf(stderr,
+                "[stamps] units %zu  cycles/unit: init %.0f seed %.0f levels %.0f pull %.0f | total p50 %.0f p90 %.0f "
+                "p99 %.0f max %.0f | levels %.2f slots %.0f\n",
+                tot.size(), ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, tot[tot.size() / 2], tot[tot.size() * 9 / 10],
+                tot[tot.size() * 99 / 100], tot.back(), lv / n, used / n);
+        HIP_CHECK(hipMemset(stamps, 0, h.size() * 8));
+    }
+    // spill batch buffers (grown on demand)
+    uint64_t spill_cap = 0;
+    uint32_t *spill_units = nullptr, *spill_roots = nullptr, *spill_targets = nullptr;
+    uint64_t *spill_allowed = nullptr, *spill_flags = nullptr;
+    unsigned int *spill_count = nullptr;
 
     hipEvent_t ev() {
         if (ev_used == ev_pool.size()) {
@@ -419,6 +1047,9 @@ struct ketogpu_engine {
         }
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         for (void *p : owned) (void)hipFree(p);
+        for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
+                        (void *)spill_flags})
+            if (p) (void)hipFree(p);
         if (h_ctr) (void)hipHostFree(h_ctr);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -432,6 +1063,18 @@ struct ketogpu_engine {
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
+        const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
+        use_units = !(mode && std::string(mode) == "global");
+        // first LDS pass: "w4" / "w8" / "w16" = one wave per 4/8/16 requests, "b16" =
+        // one workgroup per 16 requests (then 4, then 1)
+        const char *plan = getenv("KETOGPU_UNITS");
+        std::string p = plan ? plan : "w8";
+        wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
+        if (getenv("KETOGPU_STAMPS")) {
+            stamps = dalloc<unsigned long long>((size_t)65536 * 8);
+            owned.push_back(stamps);
+            HIP_CHECK(hipMemset(stamps, 0, (size_t)65536 * 8 * 8));
+        }
         auto up = [&](auto &vec) {
             auto *p = dupload(vec);
             owned.push_back((void *)p);
@@ -445,6 +1088,12 @@ struct ketogpu_engine {
         g.Ni = s.Ni;
         g.Nx = s.Nx;
         g.N = s.N;
+        {
+            std::vector<uint32_t> hk(((size_t)s.Ni + 31) / 32 + 1, 0);
+            for (uint32_t v = 0; v < s.Ni; v++)
+                if (s.fint_off[v + 1] > s.fint_off[v]) hk[v >> 5] |= 1u << (v & 31);
+            has_kids = up(hk);
+        }
 
         size_t free_b = 0, total_b = 0;
         HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -474,9 +1123,104 @@ struct ketogpu_engine {
         st.ctr = dalloc<unsigned long long>(8);
         st.overflow = dalloc<unsigned int>(4);
         st.stats = dalloc<unsigned long long>(8);
-        for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats}) owned.push_back(p);
+        spill_count = dalloc<unsigned int>(4);
+        for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats, (void *)spill_count}) owned.push_back(p);
         HIP_CHECK(hipHostMalloc((void **)&h_ctr, 16 * sizeof(uint64_t), hipHostMallocDefault));
         HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    // spill lists hold unit ids (at most one per request); spill_units has two halves
+    // used as the ping-pong lists of the cascade
+    void ensure_spill(uint64_t n) {
+        if (n <= spill_cap) return;
+        for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
+                        (void *)spill_flags})
+            if (p) (void)hipFree(p);
+        spill_cap = std::max<uint64_t>(n, 1024);
+        spill_units = dalloc<uint32_t>(2 * spill_cap);
+        spill_roots = dalloc<uint32_t>(spill_cap);
+        spill_targets = dalloc<uint32_t>(spill_cap);
+        spill_allowed = dalloc<uint64_t>(spill_cap / 64 + 1);
+        spill_flags = dalloc<uint64_t>(spill_cap / 64 + 1);
+    }
+
+    uint32_t read_spill_count() {
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 12, spill_count, sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+        return (uint32_t)h_ctr[12];
+    }
+
+    // The LDS cascade: 16-request units, then 4-request and 1-request units for what
+    // spilled.  Returns the number of single requests left in spill_units[0..) for the
+    // global path.
+    uint64_t run_units(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &unit_ev) {
+        ensure_spill(q.n);
+        uint32_t *list[2] = {spill_units, spill_units + spill_cap};
+        if (wave_u) {
+            // pass 1: one wave per unit of wave_u requests; pass 2: spilled units as
+            // single requests with a workgroup-wide table
+            uint64_t units = (q.n + wave_u - 1) / wave_u;
+            unsigned grid = (unsigned)((units + 3) / 4);
+            HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
+            hipEvent_t a = ev(), b = ev();
+            HIP_CHECK(hipEventRecord(a, stream));
+            if (wave_u == 4)
+                hipLaunchKernelGGL((wave_unit_kernel<4, 9>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                                   q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
+            else if (wave_u == 8)
+                hipLaunchKernelGGL((wave_unit_kernel<8, 10>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
+                                   q.roots, q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
+            else
+                hipLaunchKernelGGL((wave_unit_kernel<16, 11>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
+                                   q.roots, q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
+            HIP_CHECK(hipEventRecord(b, stream));
+            unit_ev.push_back({a, b});
+            uint64_t left = read_spill_count();
+            rs.spilled_units += left;
+            rs.push_launches++;
+            if (!left) return 0;
+            HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
+            a = ev();
+            b = ev();
+            HIP_CHECK(hipEventRecord(a, stream));
+            hipLaunchKernelGGL(unit_kernel<1>, dim3((unsigned)(left * wave_u)), dim3(kBlock), 0, stream, g, has_kids,
+                               q.roots, q.targets, q.n, q.allowed, q.flags, list[0], (uint32_t)wave_u, list[1],
+                               spill_count, st.stats, nullptr);
+            HIP_CHECK(hipEventRecord(b, stream));
+            unit_ev.push_back({a, b});
+            left = read_spill_count();
+            rs.spilled_units += left;
+            rs.push_launches++;
+            if (left)
+                HIP_CHECK(hipMemcpyAsync(list[0], list[1], left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+            return left;
+        }
+        uint64_t units = (q.n + 15) / 16;
+        uint64_t left = 0;
+        for (int pass = 0; pass < 3; pass++) {
+            uint64_t grid = pass == 0 ? units : left * 4;
+            if (!grid) return 0;
+            uint32_t *in = pass == 0 ? nullptr : list[(pass - 1) & 1], *out = list[pass & 1];
+            HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
+            hipEvent_t a = ev(), b = ev();
+            HIP_CHECK(hipEventRecord(a, stream));
+            if (pass == 0)
+                hipLaunchKernelGGL(unit_kernel<16>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                                   q.targets, q.n, q.allowed, q.flags, nullptr, 1u, out, spill_count, st.stats, stamps);
+            else if (pass == 1)
+                hipLaunchKernelGGL(unit_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                                   q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+            else
+                hipLaunchKernelGGL(unit_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                                   q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+            HIP_CHECK(hipEventRecord(b, stream));
+            unit_ev.push_back({a, b});
+            left = read_spill_count();
+            rs.spilled_units += left;
+            rs.push_launches++;
+        }
+        // the last pass wrote single requests into list[0]
+        return left;
     }
 
     // read ctr[0..2] and overflow into h_ctr[0..3]
@@ -486,9 +1230,10 @@ struct ketogpu_engine {
         HIP_CHECK(hipStreamSynchronize(stream));
     }
 
-    // One round over requests [c0, c0 + n) (c0 multiple of 64).  Returns false on list
-    // overflow (state is then dense-reset and the caller splits the round).
-    bool round(ketogpu_queries &q, uint64_t c0, uint64_t n, ketogpu_run_stats &rs,
+    // Global multi-word engine, one round over requests [c0, c0 + n) of batch q (c0 a
+    // multiple of 64).  Returns false on list overflow (state is then dense-reset and
+    // the caller splits the round).
+    bool round(const Batch &q, uint64_t c0, uint64_t n, ketogpu_run_stats &rs,
                std::vector<std::pair<hipEvent_t, hipEvent_t>> &push_ev,
                std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev) {
         const uint64_t W = (n + 63) / 64;
@@ -496,17 +1241,16 @@ struct ketogpu_engine {
         HIP_CHECK(hipMemsetAsync(st.ctr, 0, 3 * sizeof(uint64_t), stream));
         HIP_CHECK(hipMemsetAsync(st.overflow, 0, sizeof(unsigned int), stream));
         *(uint64_t *)&h_ctr[3] = 0;
-        hipLaunchKernelGGL(seed_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.d_roots, q.d_targets,
-                           c0, n, q.d_flags);
+        hipLaunchKernelGGL(seed_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
+                           q.flags);
         read_counters();
         uint64_t cnt = h_ctr[0] >> kCntShift, edges = h_ctr[0] & kPreMask;
         std::vector<uint64_t> level_begin{0};
         uint64_t lb = 0;
         int cur = 0;  // ctr index of the current level
         if (q.has_dyn) {
-            hipLaunchKernelGGL(seed_dynamic_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.d_roots,
-                               q.d_targets, c0, n, q.d_dyn_int_off, q.d_dyn_int, q.d_dyn_amb, q.d_flags, lb + cnt,
-                               &st.ctr[1]);
+            hipLaunchKernelGGL(seed_dynamic_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots,
+                               q.targets, c0, n, q.dyn_int_off, q.dyn_int, q.dyn_amb, q.flags, lb + cnt, &st.ctr[1]);
         }
         bool overflow = (uint32_t)h_ctr[3] != 0;
         for (uint64_t level = 0; !overflow; level++) {
@@ -522,7 +1266,7 @@ struct ketogpu_engine {
                 hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
                 hipLaunchKernelGGL(expand_kernel, dim3(grid), dim3(kBlock), 0, stream, g, st, lb, cnt, edges, lb + cnt,
-                                   &st.ctr[nxt], q.d_flags, wg0);
+                                   &st.ctr[nxt], q.flags, wg0);
                 HIP_CHECK(hipEventRecord(b, stream));
                 push_ev.push_back({a, b});
                 rs.push_launches++;
@@ -546,15 +1290,14 @@ struct ketogpu_engine {
             size_t state = (size_t)Wmax * std::max<uint32_t>(g.Ni, 1);
             HIP_CHECK(hipMemsetAsync(st.vis, 0, state * 8, stream));
             HIP_CHECK(hipMemsetAsync(st.nxt, 0, state * 8, stream));
-            HIP_CHECK(hipMemsetAsync(q.d_flags + wg0, 0, W * 8, stream));
+            HIP_CHECK(hipMemsetAsync(q.flags + wg0, 0, W * 8, stream));
             HIP_CHECK(hipStreamSynchronize(stream));
             return false;
         }
-        // pull: one thread per request
         hipEvent_t a = ev(), b = ev();
         HIP_CHECK(hipEventRecord(a, stream));
-        hipLaunchKernelGGL(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.d_roots, q.d_targets, c0, n,
-                           q.d_dyn_full_off, q.d_dyn_full, q.d_allowed);
+        hipLaunchKernelGGL(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
+                           q.dyn_full_off, q.dyn_full, q.allowed);
         HIP_CHECK(hipEventRecord(b, stream));
         pull_ev.push_back({a, b});
         // reset every visited entry recorded in this round (levels >= 1 and touch list)
@@ -571,17 +1314,9 @@ struct ketogpu_engine {
         return true;
     }
 
-    void run(ketogpu_queries &q) {
-        HIP_CHECK(hipSetDevice(device));
-        ketogpu_run_stats rs{};
-        rs.checks = q.n;
-        ev_used = 0;
-        std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
-        hipEvent_t t_begin = ev(), t_end = ev();
+    void run_global(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &push_ev,
+                    std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev) {
         uint64_t words = (q.n + 63) / 64;
-        HIP_CHECK(hipMemsetAsync(st.stats, 0, 8 * sizeof(uint64_t), stream));
-        HIP_CHECK(hipMemsetAsync(q.d_flags, 0, std::max<uint64_t>(words, 1) * 8, stream));
-        HIP_CHECK(hipEventRecord(t_begin, stream));
         uint64_t W = Wmax;
         for (uint64_t w0 = 0; w0 < words;) {
             uint64_t wn = std::min<uint64_t>(W, words - w0);
@@ -594,17 +1329,64 @@ struct ketogpu_engine {
             }
             w0 += wn;
         }
+    }
+
+    void run(ketogpu_queries &qq) {
+        HIP_CHECK(hipSetDevice(device));
+        Batch q = qq.batch();
+        ketogpu_run_stats rs{};
+        rs.checks = q.n;
+        ev_used = 0;
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
+        hipEvent_t t_begin = ev(), t_end = ev();
+        uint64_t words = (q.n + 63) / 64;
+        HIP_CHECK(hipMemsetAsync(st.stats, 0, 8 * sizeof(uint64_t), stream));
+        HIP_CHECK(hipMemsetAsync(q.flags, 0, std::max<uint64_t>(words, 1) * 8, stream));
+        HIP_CHECK(hipMemsetAsync(q.allowed, 0, std::max<uint64_t>(words, 1) * 8, stream));
+        HIP_CHECK(hipEventRecord(t_begin, stream));
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
+        if (use_units && q.n) {
+            uint64_t ns = run_units(q, rs, unit_ev);
+            rs.spilled_requests = ns;
+            if (ns) {  // single requests whose closure exceeds an LDS table: global path
+                hipLaunchKernelGGL(spill_gather_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
+                                   q.roots, q.targets, q.n, spill_roots, spill_targets);
+                Batch sb = q;
+                sb.roots = spill_roots;
+                sb.targets = spill_targets;
+                sb.n = ns;
+                sb.allowed = spill_allowed;
+                sb.flags = spill_flags;
+                HIP_CHECK(hipMemsetAsync(spill_flags, 0, (ns / 64 + 1) * 8, stream));
+                HIP_CHECK(hipMemsetAsync(spill_allowed, 0, (ns / 64 + 1) * 8, stream));
+                run_global(sb, rs, push_ev, pull_ev);
+                hipLaunchKernelGGL(spill_scatter_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
+                                   spill_allowed, spill_flags, q.allowed, q.flags);
+            }
+        } else {
+            run_global(q, rs, push_ev, pull_ev);
+        }
         HIP_CHECK(hipEventRecord(t_end, stream));
-        uint64_t examined = 0;
-        HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
-        examined = h_ctr[8];
-        rs.rev_edges = examined;
-        // pull bytes: 16 per request row open (rev_off), 4 per reverse entry, 8 per
-        // visited-word read, 8 per result word
-        rs.bytes_pull = 16 * q.n + 4 * examined + 8 * examined + 8 * words;
-        rs.bytes_total = rs.bytes_push + rs.bytes_pull + 8 * 2 * rs.touched;
+        uint64_t examined = h_ctr[8];
+        // unit path: 16 B per row opened (offset pair), 4 B per interior edge, 4 B per
+        // reverse entry, 4+4 B per request (root, target), 8 B per result word
+        rs.unit_rows = h_ctr[9];
+        rs.unit_edges = h_ctr[10];
+        rs.unit_rev = h_ctr[11];
+        rs.bytes_unit = 16 * rs.unit_rows + 4 * rs.unit_edges + 4 * rs.unit_rev + 8 * q.n + 8 * words;
+        rs.rev_edges = examined + rs.unit_rev;
+        rs.interior_edges += rs.unit_edges;
+        // global path pull bytes: 16 per request row open (rev_off), 4 per reverse entry,
+        // 8 per visited-word read, 8 per result word
+        rs.bytes_pull = examined ? 16 * q.n + 4 * examined + 8 * examined + 8 * words : 0;
+        rs.bytes_total = rs.bytes_unit + rs.bytes_push + rs.bytes_pull + 8 * 2 * rs.touched;
         float ms = 0;
+        for (auto &p : unit_ev) {
+            HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
+            rs.ms_unit += ms;
+        }
         for (auto &p : push_ev) {
             HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
             rs.ms_push += ms;
@@ -616,6 +1398,7 @@ struct ketogpu_engine {
         HIP_CHECK(hipEventElapsedTime(&ms, t_begin, t_end));
         rs.ms_total = ms;
         last = rs;
+        if (stamps && use_units && !wave_u) report_stamps();
     }
 
     ketogpu_queries *upload(const uint32_t *roots, const uint32_t *targets, uint64_t n) {
