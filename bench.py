@@ -135,8 +135,10 @@ def main():
     if rank == 0:
         # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time
         fam = {
-            "unit_kernel": (st["bytes_unit"], st["ms_unit"], 1 if st["ms_unit"] > 0 else 0),
-            "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - (1 if st["ms_unit"] > 0 else 0)),
+            "unit2_kernel<16>": (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
+            "unit2_kernel<4>+<1> (spill passes)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
+                                                   max(st["unit_launches"] - 1, 0)),
+            "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - st["unit_launches"]),
             "pull_kernel": (st["bytes_pull"], st["ms_pull"], st["rounds"]),
         }
         gbps = {k: (b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0) for k, (b, ms, _) in fam.items()}

@@ -246,6 +246,9 @@ typedef struct {
     uint64_t bytes_unit;        /* algorithmic HBM bytes of the unit kernel       */
     double ms_unit;             /* device time of the unit kernels (hipEvent)     */
     uint64_t spilled_requests;  /* single requests run on the global path         */
+    uint64_t unit_launches;     /* unit-kernel launches (cascade passes)          */
+    uint64_t main_bytes;        /* algorithmic HBM bytes of the first unit pass   */
+    double main_ms;             /* its device time (hipEvent)                     */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

@@ -79,7 +79,8 @@ class RunStats(C.Structure):
         "bytes_pull", "bytes_total")] + [("ms_push", C.c_double), ("ms_pull", C.c_double), ("ms_total", C.c_double)] + [
         ("push_launches", C.c_uint64), ("overflow_retries", C.c_uint64)] + [(n, C.c_uint64) for n in (
         "spilled_units", "unit_rows", "unit_edges", "unit_rev", "bytes_unit")] + [("ms_unit", C.c_double)] + [
-        ("spilled_requests", C.c_uint64)]
+        ("spilled_requests", C.c_uint64), ("unit_launches", C.c_uint64), ("main_bytes", C.c_uint64),
+        ("main_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -457,6 +457,16 @@ __device__ __forceinline__ void unit_push(const DevGraph &g, UnitShared &S, bool
     }
 }
 
+__device__ __forceinline__ int key_lookup(const uint32_t *key, uint32_t v) {
+    uint32_t h = hslot(v);
+    for (int p = 0; p < kHash; p++, h = (h + 1) & (kHash - 1)) {
+        uint32_t kv = key[h];
+        if (kv == v) return (int)h;
+        if (kv == kEmpty) return -1;
+    }
+    return -1;
+}
+
 __device__ __forceinline__ int unit_lookup(const UnitShared &S, uint32_t v) {
     uint32_t h = hslot(v);
     for (int p = 0; p < kHash; p++, h = (h + 1) & (kHash - 1)) {
@@ -465,6 +475,31 @@ __device__ __forceinline__ int unit_lookup(const UnitShared &S, uint32_t v) {
         if (kv == kEmpty) return -1;
     }
     return -1;
+}
+
+// Unit statistics are summed into kStatSlots spread slots (4 u64 each, from stats[8]):
+// tens of thousands of workgroups adding to ONE address serialize at the memory side
+// (~12 ns per atomic) and that alone cost ~2 ms per 1M requests.
+constexpr int kStatSlots = 1024;
+__device__ __forceinline__ unsigned long long *stat_slot(unsigned long long *stats) {
+    return stats + 8 + (size_t)(blockIdx.x & (kStatSlots - 1)) * 4;
+}
+
+// per-wave reduction of three counters, then one LDS atomic each per wave (all 256
+// threads hitting one address serializes ~768 atomics per unit)
+__device__ __forceinline__ void wave_stats_add(uint64_t a, uint64_t b, uint64_t c, unsigned long long *pa,
+                                               unsigned long long *pb, unsigned long long *pc) {
+#pragma unroll
+    for (int s = 32; s; s >>= 1) {
+        a += __shfl_down(a, s, 64);
+        b += __shfl_down(b, s, 64);
+        c += __shfl_down(c, s, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(pa, (unsigned long long)a);
+        atomicAdd(pb, (unsigned long long)b);
+        atomicAdd(pc, (unsigned long long)c);
+    }
 }
 
 // expand the chunk held in S.c_begin / S.c_pre / S.c_mask (entries [0, k)); the loop
@@ -621,9 +656,7 @@ __global__ __launch_bounds__(kBlock) void unit_kernel(DevGraph g, const uint32_t
         }
         if (ok) atomicOr(&S.res, 1u << j);
     }
-    atomicAdd(&S.cnt_rows, (unsigned long long)rows);
-    atomicAdd(&S.cnt_edges, (unsigned long long)edges);
-    atomicAdd(&S.cnt_rev, (unsigned long long)rev);
+    wave_stats_add(rows, edges, rev, &S.cnt_rows, &S.cnt_edges, &S.cnt_rev);
     __syncthreads();
     if (stamp) {
         stamp[4] = __builtin_amdgcn_s_memtime();
@@ -633,9 +666,292 @@ __global__ __launch_bounds__(kBlock) void unit_kernel(DevGraph g, const uint32_t
     }
     if (tid == 0) {
         if (S.res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)S.res << shift);
-        atomicAdd(&stats[1], S.cnt_rows);
-        atomicAdd(&stats[2], S.cnt_edges);
-        atomicAdd(&stats[3], S.cnt_rev);
+        atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
+        atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
+        atomicAdd(&stat_slot(stats)[2], S.cnt_rev);
+    }
+}
+
+// ------------------------------------------------------ unit traversal v2
+// Measured (s_memtime stamps, config #2): a unit lived ~60k cycles, 24k of them in the
+// pull (rev_off -> rev_col, two dependent HBM misses) and ~11k per BFS level (row
+// offsets -> row entries, two dependent loads + scan/barriers).  v2 removes one
+// dependent load per level and hides the pull's:
+//   * edge RECORDS {node, interior degree, row begin}: pushing a node yields the row
+//     of the next level, so a level costs one dependent global load (the records);
+//   * each request's reverse row is prefetched into LDS (first kRevCache entries) while
+//     the BFS runs; the pull is then LDS-only for targets with <= kRevCache entries.
+struct FRec {
+    uint32_t node, deg, begin, pad;
+};
+constexpr int kFront = 512;  // frontier entries per level (spill beyond)
+constexpr int kRevCache = 16;
+
+template <int U>
+struct Unit2Shared {
+    uint32_t key[kHash];
+    uint32_t st[kHash];  // visited bits (low 16) | pending bits (high 16)
+    uint16_t cur_slot[kFront], cur_mask[kFront], nxt_slot[kFront];
+    uint32_t cur_begin[kFront], cur_deg[kFront], nxt_begin[kFront], nxt_deg[kFront];
+    uint32_t c_pre[kChunk + 1];
+    uint32_t wave_sum[kBlock / 64];
+    uint32_t root[U], target[U], rev_n[U];
+    uint64_t rev_b[U];
+    uint32_t rev_c[U][kRevCache];
+    uint32_t n_used, n_nxt, spill, res;
+    unsigned long long cnt_rows, cnt_edges, cnt_rev;
+};
+
+template <int U>
+__device__ __forceinline__ uint32_t block_excl_scan2(uint32_t v, Unit2Shared<U> &S) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+    }
+    if (lane == 63) S.wave_sum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; i++) {
+        uint32_t s = S.wave_sum[i];
+        base += i < wv ? s : 0;
+        total += s;
+    }
+    S.c_pre[tid] = base + x - v;
+    if (tid == 0) S.c_pre[kBlock] = total;
+    __syncthreads();
+    return total;
+}
+
+template <int U>
+__device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S, bool want, const FRec &rc, uint32_t m,
+                                           uint64_t *flag_word, int shift) {
+    const uint32_t u = rc.node;
+    int h = -1;
+    bool inserted = false;
+    if (want) {
+        uint32_t hh = hslot(u);
+        for (int p = 0; p < kHash; p++, hh = (hh + 1) & (kHash - 1)) {
+            uint32_t kv = S.key[hh];
+            if (kv == kEmpty) {
+                uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
+                if (prev == kEmpty) {
+                    inserted = true;
+                    h = (int)hh;
+                    break;
+                }
+                kv = prev;
+            }
+            if (kv == u) {
+                h = (int)hh;
+                break;
+            }
+        }
+        if (h < 0) S.spill = 1;
+    }
+    const int lane = threadIdx.x & 63;
+    uint64_t bal = __ballot(inserted);
+    if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
+        uint32_t c = (uint32_t)__popcll(bal);
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)kHashMax) S.spill = 1;
+    }
+    bool app = false;
+    if (h >= 0) {
+        uint32_t old = atomicOr(&S.st[h], m);
+        uint32_t newly = m & ~old & 0xFFFFu;
+        if (newly) {
+            if (g.row_amb && bit_of(g.row_amb, u))
+                atomicOr((unsigned long long *)flag_word, (unsigned long long)newly << shift);
+            if (rc.deg) {
+                uint32_t o2 = atomicOr(&S.st[h], newly << 16);
+                app = !(o2 >> 16);
+            }
+        }
+    }
+    uint64_t ab = __ballot(app);
+    if (ab) {
+        int leader = __ffsll((unsigned long long)ab) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&S.n_nxt, (uint32_t)__popcll(ab));
+        base = __shfl(base, leader, 64);
+        if (app) {
+            uint32_t idx = base + lanes_below(ab);
+            if (idx < (uint32_t)kFront) {
+                S.nxt_slot[idx] = (uint16_t)h;
+                S.nxt_begin[idx] = rc.begin;
+                S.nxt_deg[idx] = rc.deg;
+            } else {
+                S.spill = 1;
+            }
+        }
+    }
+}
+
+// expand cur entries [base, base + k) whose row begins/degrees are in cur_begin/cur_deg
+template <int U>
+__device__ __forceinline__ void unit2_expand(const DevGraph &g, const FRec *frec, Unit2Shared<U> &S,
+                                             const uint32_t *begin, const uint32_t *deg, const uint16_t *mask,
+                                             uint32_t k, uint64_t *flag_word, int shift, uint64_t &rows,
+                                             uint64_t &edges) {
+    uint32_t d = 0;
+    if ((uint32_t)threadIdx.x < k) d = deg[threadIdx.x];
+    uint32_t total = block_excl_scan2<U>(d, S);
+    for (uint32_t base = 0; base < total; base += kBlock) {
+        uint32_t e = base + threadIdx.x;
+        bool want = e < total;
+        FRec rc{0, 0, 0, 0};
+        uint32_t m = 0;
+        if (want) {
+            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (S.c_pre[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            rc = frec[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
+            m = mask[lo];
+            edges++;
+        }
+        unit2_push<U>(g, S, want, rc, m, flag_word, shift);
+    }
+}
+
+// Pass 1 (parents == nullptr): unit b = requests [U*b, U*b+U).  Later passes split the
+// spilled units of the previous pass (size U*fan) into `fan` units each.
+template <int U>
+__global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *frec, const uint32_t *roots,
+                                                       const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                       uint64_t *flags, const uint32_t *parents, uint32_t fan,
+                                                       uint32_t *spill_out, unsigned int *spill_count,
+                                                       unsigned long long *stats, unsigned long long *stamps) {
+    __shared__ Unit2Shared<U> S;
+    const int tid = threadIdx.x;
+    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    uint32_t n_levels = 0;
+    if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
+    const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
+    const uint64_t c0 = unit * U;
+    uint64_t *flag_word = &flags[c0 >> 6];
+    const int shift = (int)(c0 & 63);
+    const unsigned long long unit_bits = ((1ull << U) - 1) << shift;
+    for (int i = tid; i < kHash; i += kBlock) {
+        S.key[i] = kEmpty;
+        S.st[i] = 0;
+    }
+    if (tid == 0) {
+        S.n_used = S.n_nxt = S.spill = S.res = 0;
+        S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
+    }
+    uint64_t rows = 0, edges = 0, rev = 0;
+    if (tid < U) {
+        // the request, its root row (seed) and its reverse row (pull): independent loads
+        uint64_t c = c0 + tid;
+        uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+        if (c < n) {
+            r = roots[c];
+            t = targets[c];
+        }
+        if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
+        uint64_t fb = 0, fe = 0, rb = 0, re = 0;
+        if (r != KETOGPU_NODE_NONE && r < kDynBase) {
+            fb = g.fint_off[r];
+            fe = g.fint_off[r + 1];
+            rb = g.rev_off[t];
+            re = g.rev_off[t + 1];
+            rows += 2;
+            if (g.row_amb && bit_of(g.row_amb, r))
+                atomicOr((unsigned long long *)flag_word, (unsigned long long)1 << (shift + tid));
+        }
+        if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
+        S.root[tid] = r;
+        S.target[tid] = t;
+        S.cur_begin[tid] = (uint32_t)fb;
+        S.cur_deg[tid] = (uint32_t)(fe - fb);
+        S.cur_mask[tid] = (uint16_t)(1u << tid);
+        S.rev_b[tid] = rb;
+        S.rev_n[tid] = (uint32_t)(re - rb);
+    }
+    __syncthreads();
+    if (S.spill) {
+        if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    // reverse-row prefetch: issued now, stored after the seed level
+    const int rj = tid / (kBlock / U), rl = tid % (kBlock / U);
+    uint32_t rv = 0;
+    const bool rpre = rl < kRevCache && (uint32_t)rl < S.rev_n[rj] && S.root[rj] != KETOGPU_NODE_NONE;
+    if (rpre) rv = g.rev_col[S.rev_b[rj] + rl];
+    if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
+    unit2_expand<U>(g, frec, S, S.cur_begin, S.cur_deg, S.cur_mask, U, flag_word, shift, rows, edges);
+    if (rpre) S.rev_c[rj][rl] = rv;
+    if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
+    for (;;) {
+        __syncthreads();
+        uint32_t cnt = S.n_nxt;
+        if (S.spill || !cnt) break;
+        n_levels++;
+        for (uint32_t i = tid; i < cnt; i += kBlock) {
+            uint16_t s = S.nxt_slot[i];
+            S.cur_slot[i] = s;
+            S.cur_mask[i] = (uint16_t)(atomicAnd(&S.st[s], 0xFFFFu) >> 16);
+            S.cur_begin[i] = S.nxt_begin[i];
+            S.cur_deg[i] = S.nxt_deg[i];
+        }
+        __syncthreads();
+        if (tid == 0) S.n_nxt = 0;
+        for (uint32_t base = 0; base < cnt; base += kChunk) {
+            uint32_t k = cnt - base < (uint32_t)kChunk ? cnt - base : (uint32_t)kChunk;
+            unit2_expand<U>(g, frec, S, S.cur_begin + base, S.cur_deg + base, S.cur_mask + base, k, flag_word, shift,
+                            rows, edges);
+            __syncthreads();
+        }
+    }
+    if (S.spill) {
+        if (tid == 0) {
+            spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+            atomicAnd((unsigned long long *)flag_word, ~unit_bits);
+        }
+        return;
+    }
+    if (stamp) stamp[3] = __builtin_amdgcn_s_memtime();
+    // pull: kBlock / U lanes per request; cached reverse entries first
+    {
+        constexpr int L = kBlock / U;
+        bool ok = false;
+        uint32_t r = S.root[rj];
+        if (r != KETOGPU_NODE_NONE) {
+            uint32_t nrev = S.rev_n[rj];
+            for (uint32_t p = rl; p < nrev && !ok; p += L) {
+                uint32_t v = p < (uint32_t)kRevCache ? S.rev_c[rj][p] : g.rev_col[S.rev_b[rj] + p];
+                rev++;
+                if (v == r) {
+                    ok = true;
+                } else if (v < g.Ni) {
+                    int s = key_lookup(S.key, v);
+                    ok = s >= 0 && ((S.st[s] >> rj) & 1u);
+                }
+            }
+        }
+        if (ok) atomicOr(&S.res, 1u << rj);
+    }
+    wave_stats_add(rows, edges, rev, &S.cnt_rows, &S.cnt_edges, &S.cnt_rev);
+    __syncthreads();
+    if (stamp) {
+        stamp[4] = __builtin_amdgcn_s_memtime();
+        stamp[5] = n_levels;
+        stamp[6] = S.n_used;
+        stamp[7] = 1;
+    }
+    if (tid == 0) {
+        if (S.res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)S.res << shift);
+        atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
+        atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
+        atomicAdd(&stat_slot(stats)[2], S.cnt_rev);
     }
 }
 
@@ -889,9 +1205,9 @@ __global__ __launch_bounds__(kBlock) void wave_unit_kernel(DevGraph g, const uin
         for (int q = 0; q < U; q++)
             if ((bal >> (q * LPC)) & lm) res |= 1u << q;
         if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << shift);
-        atomicAdd(&stats[1], (unsigned long long)rows);
-        atomicAdd(&stats[2], (unsigned long long)edges);
-        atomicAdd(&stats[3], (unsigned long long)rev);
+        atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
+        atomicAdd(&stat_slot(stats)[1], (unsigned long long)edges);
+        atomicAdd(&stat_slot(stats)[2], (unsigned long long)rev);
     }
 }
 
@@ -1000,7 +1316,11 @@ struct ketogpu_engine {
     size_t ev_used = 0;
     bool use_units = true;
     int wave_u = 8;
+    bool use_v2 = true;
+    const FRec *frec = nullptr;  // v2 edge records (parallel to fint_col)
     unsigned long long *stamps = nullptr;  // KETOGPU_STAMPS=1 diagnostic build
+    std::vector<uint64_t> stat_host;
+    unsigned lds_pad = 0;  // KETOGPU_LDS_PAD: extra dynamic LDS per workgroup (occupancy experiments)
 
     void report_stamps() {
         std::vector<unsigned long long> h((size_t)65536 * 8);
@@ -1065,11 +1385,15 @@ struct ketogpu_engine {
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
-        // first LDS pass: "w4" / "w8" / "w16" = one wave per 4/8/16 requests, "b16" =
-        // one workgroup per 16 requests (then 4, then 1)
+        // first LDS pass: "v2" (default) = unit2_kernel, one workgroup per 16 requests with
+        // edge records; "b16" = unit_kernel; "w4" / "w8" / "w16" = one wave per 4/8/16
+        // requests.  Spills go on to 4-request and 1-request units, then the global path.
         const char *plan = getenv("KETOGPU_UNITS");
-        std::string p = plan ? plan : "w8";
+        std::string p = plan ? plan : "v2";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
+        use_v2 = p == "v2";
+        if (use_v2 && s.fint_col.size() >= (1ull << 32)) use_v2 = false;  // record begins are u32
+        if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
         if (getenv("KETOGPU_STAMPS")) {
             stamps = dalloc<unsigned long long>((size_t)65536 * 8);
             owned.push_back(stamps);
@@ -1093,6 +1417,14 @@ struct ketogpu_engine {
             for (uint32_t v = 0; v < s.Ni; v++)
                 if (s.fint_off[v + 1] > s.fint_off[v]) hk[v >> 5] |= 1u << (v & 31);
             has_kids = up(hk);
+        }
+        if (use_v2) {
+            std::vector<FRec> rec(s.fint_col.size());
+            for (size_t e = 0; e < rec.size(); e++) {
+                uint32_t u = s.fint_col[e];
+                rec[e] = FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u], 0};
+            }
+            frec = up(rec);
         }
 
         size_t free_b = 0, total_b = 0;
@@ -1122,7 +1454,7 @@ struct ketogpu_engine {
         for (void *p : {(void *)st.fe_key, (void *)st.fe_mask, (void *)st.fe_pre, (void *)st.touch}) owned.push_back(p);
         st.ctr = dalloc<unsigned long long>(8);
         st.overflow = dalloc<unsigned int>(4);
-        st.stats = dalloc<unsigned long long>(8);
+        st.stats = dalloc<unsigned long long>(8 + 4 * kStatSlots);
         spill_count = dalloc<unsigned int>(4);
         for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats, (void *)spill_count}) owned.push_back(p);
         HIP_CHECK(hipHostMalloc((void **)&h_ctr, 16 * sizeof(uint64_t), hipHostMallocDefault));
@@ -1142,6 +1474,17 @@ struct ketogpu_engine {
         spill_targets = dalloc<uint32_t>(spill_cap);
         spill_allowed = dalloc<uint64_t>(spill_cap / 64 + 1);
         spill_flags = dalloc<uint64_t>(spill_cap / 64 + 1);
+    }
+
+    // sum the spread unit-statistics slots (rows, edges, reverse entries)
+    void read_unit_stats(uint64_t out[3]) {
+        stat_host.resize(4 * kStatSlots);
+        HIP_CHECK(hipMemcpyAsync(stat_host.data(), st.stats + 8, 4 * kStatSlots * sizeof(uint64_t),
+                                 hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+        out[0] = out[1] = out[2] = 0;
+        for (int i = 0; i < kStatSlots; i++)
+            for (int k = 0; k < 3; k++) out[k] += stat_host[(size_t)i * 4 + k];
     }
 
     uint32_t read_spill_count() {
@@ -1198,6 +1541,36 @@ struct ketogpu_engine {
         uint64_t units = (q.n + 15) / 16;
         uint64_t left = 0;
         for (int pass = 0; pass < 3; pass++) {
+            if (use_v2) {
+                uint64_t grid = pass == 0 ? units : left * 4;
+                if (!grid) break;
+                uint32_t *in = pass == 0 ? nullptr : list[(pass - 1) & 1], *out = list[pass & 1];
+                HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
+                hipEvent_t a = ev(), b = ev();
+                HIP_CHECK(hipEventRecord(a, stream));
+                if (pass == 0)
+                    hipLaunchKernelGGL(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), lds_pad, stream, g, frec,
+                                       q.roots, q.targets, q.n, q.allowed, q.flags, nullptr, 1u, out, spill_count,
+                                       st.stats, stamps);
+                else if (pass == 1)
+                    hipLaunchKernelGGL(unit2_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
+                                       q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+                else
+                    hipLaunchKernelGGL(unit2_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
+                                       q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+                HIP_CHECK(hipEventRecord(b, stream));
+                unit_ev.push_back({a, b});
+                left = read_spill_count();
+                rs.spilled_units += left;
+                rs.push_launches++;
+                rs.unit_launches++;
+                if (pass == 0) {  // the dominant launch: keep its own byte count
+                    uint64_t t3[3];
+                    read_unit_stats(t3);
+                    rs.main_bytes = 16 * t3[0] + 16 * t3[1] + 4 * t3[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
+                }
+                continue;
+            }
             uint64_t grid = pass == 0 ? units : left * 4;
             if (!grid) return 0;
             uint32_t *in = pass == 0 ? nullptr : list[(pass - 1) & 1], *out = list[pass & 1];
@@ -1218,6 +1591,7 @@ struct ketogpu_engine {
             left = read_spill_count();
             rs.spilled_units += left;
             rs.push_launches++;
+            rs.unit_launches++;
         }
         // the last pass wrote single requests into list[0]
         return left;
@@ -1340,7 +1714,7 @@ struct ketogpu_engine {
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
         uint64_t words = (q.n + 63) / 64;
-        HIP_CHECK(hipMemsetAsync(st.stats, 0, 8 * sizeof(uint64_t), stream));
+        HIP_CHECK(hipMemsetAsync(st.stats, 0, (8 + 4 * kStatSlots) * sizeof(uint64_t), stream));
         HIP_CHECK(hipMemsetAsync(q.flags, 0, std::max<uint64_t>(words, 1) * 8, stream));
         HIP_CHECK(hipMemsetAsync(q.allowed, 0, std::max<uint64_t>(words, 1) * 8, stream));
         HIP_CHECK(hipEventRecord(t_begin, stream));
@@ -1367,15 +1741,19 @@ struct ketogpu_engine {
             run_global(q, rs, push_ev, pull_ev);
         }
         HIP_CHECK(hipEventRecord(t_end, stream));
-        HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-        HIP_CHECK(hipStreamSynchronize(stream));
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        uint64_t t3[3];
+        read_unit_stats(t3);  // synchronizes the stream
         uint64_t examined = h_ctr[8];
         // unit path: 16 B per row opened (offset pair), 4 B per interior edge, 4 B per
         // reverse entry, 4+4 B per request (root, target), 8 B per result word
-        rs.unit_rows = h_ctr[9];
-        rs.unit_edges = h_ctr[10];
-        rs.unit_rev = h_ctr[11];
-        rs.bytes_unit = 16 * rs.unit_rows + 4 * rs.unit_edges + 4 * rs.unit_rev + 8 * q.n + 8 * words;
+        rs.unit_rows = t3[0];
+        rs.unit_edges = t3[1];
+        rs.unit_rev = t3[2];
+        // v2 reads a 16 B edge record per edge and its row opens are the root/reverse
+        // offset pairs only; v1 reads 4 B column entries and opens every frontier row
+        rs.bytes_unit = 16 * rs.unit_rows + (use_v2 && !wave_u ? 16 : 4) * rs.unit_edges + 4 * rs.unit_rev +
+                        8 * q.n + 8 * words;
         rs.rev_edges = examined + rs.unit_rev;
         rs.interior_edges += rs.unit_edges;
         // global path pull bytes: 16 per request row open (rev_off), 4 per reverse entry,
@@ -1383,9 +1761,10 @@ struct ketogpu_engine {
         rs.bytes_pull = examined ? 16 * q.n + 4 * examined + 8 * examined + 8 * words : 0;
         rs.bytes_total = rs.bytes_unit + rs.bytes_push + rs.bytes_pull + 8 * 2 * rs.touched;
         float ms = 0;
-        for (auto &p : unit_ev) {
-            HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
+        for (size_t i = 0; i < unit_ev.size(); i++) {
+            HIP_CHECK(hipEventElapsedTime(&ms, unit_ev[i].first, unit_ev[i].second));
             rs.ms_unit += ms;
+            if (i == 0) rs.main_ms = ms;
         }
         for (auto &p : push_ev) {
             HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
