@@ -36,7 +36,7 @@ def parse():
     p.add_argument("--small", action="store_true", help="1/100-size graph for quick runs (not the metric)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU work of the baseline sample")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
     return p.parse_args()
 
@@ -134,10 +134,12 @@ def main():
     out = None
     if rank == 0:
         # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time
+        plan = os.environ.get("KETOGPU_UNITS", "bidi")
+        main = {"bidi": "bidi_kernel<16>", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
         fam = {
-            "unit2_kernel<16>": (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
-            "unit2_kernel<4>+<1> (spill passes)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
-                                                   max(st["unit_launches"] - 1, 0)),
+            main: (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
+            "spill passes (unit2_kernel cascade)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
+                                                    max(st["unit_launches"] - 1, 0)),
             "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - st["unit_launches"]),
             "pull_kernel": (st["bytes_pull"], st["ms_pull"], st["rounds"]),
         }

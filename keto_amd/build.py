@@ -15,7 +15,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
 
 SOURCES = ["snapshot.cpp", "host_engine.cpp", "device_engine.hip"]
-HEADERS = ["ketogpu_internal.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
+HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
 
 
 def _stale(out, deps):

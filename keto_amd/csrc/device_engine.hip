@@ -39,17 +39,17 @@
 #include <string>
 #include <vector>
 
+#include "device_util.hpp"
 #include "ketogpu_internal.hpp"
 
 using namespace ketogpu;
+using namespace kdev;
 
 namespace {
 
 constexpr int kBlock = 256;
 constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;
-constexpr int kCntShift = 36;  // packed append counter: count << 36 | prefix
-constexpr uint64_t kPreMask = (1ull << kCntShift) - 1;
 constexpr uint32_t kDynBase = 0x80000000u;
 
 struct DevGraph {
@@ -73,59 +73,6 @@ struct DevState {
 };
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bm, uint32_t i) { return (bm[i >> 5] >> (i & 31)) & 1u; }
-
-// 64-lane inclusive scan of a uint64 value
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint64_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
-// Append (key, row length) to a frontier list with one atomic per wave.  Every lane of
-// the wave must call this (inactive lanes pass want = false).
-__device__ __forceinline__ void wave_append(bool want, uint64_t key, uint64_t deg, int lane,
-                                            unsigned long long *ctr, uint64_t base, uint64_t cap,
-                                            uint64_t *out_key, uint64_t *out_pre, uint64_t *out_mask,
-                                            uint64_t mask, unsigned int *overflow) {
-    uint64_t val = want ? ((1ull << kCntShift) | deg) : 0ull;
-    uint64_t incl = wave_incl_scan(val, lane);
-    uint64_t total = __shfl(incl, 63, 64);
-    if (!total) return;
-    unsigned long long start = 0;
-    if (lane == 63) start = atomicAdd(ctr, (unsigned long long)total);
-    start = __shfl(start, 63, 64);
-    if (want) {
-        uint64_t pos = start + incl - val;
-        uint64_t idx = base + (pos >> kCntShift);
-        if (idx < cap) {
-            out_key[idx] = key;
-            out_pre[idx] = pos & kPreMask;
-            if (out_mask) out_mask[idx] = mask;
-        } else {
-            atomicOr(overflow, 1u);
-        }
-    }
-}
-
-__device__ __forceinline__ void wave_touch(bool want, uint64_t key, int lane, unsigned long long *ctr,
-                                           uint64_t *touch, uint64_t cap, unsigned int *overflow) {
-    uint64_t bal = __ballot(want);
-    if (!bal) return;
-    int leader = __ffsll((unsigned long long)bal) - 1;
-    unsigned long long start = 0;
-    if (lane == leader) start = atomicAdd(ctr, (unsigned long long)__popcll(bal));
-    start = __shfl(start, leader, 64);
-    if (want) {
-        uint64_t idx = start + __popcll(bal & ((1ull << lane) - 1));
-        if (idx < cap)
-            touch[idx] = key;
-        else
-            atomicOr(overflow, 1u);
-    }
-}
 
 // Push mask m of word w into interior node u: returns the bits u gains.
 __device__ __forceinline__ void push_one(const DevGraph &g, const DevState &s, uint32_t w, uint32_t u, uint64_t m,
@@ -214,25 +161,6 @@ __global__ __launch_bounds__(kBlock) void seed_dynamic_kernel(DevGraph g, DevSta
                 atomicOr(s.overflow, 1u);
         }
     }
-}
-
-// first index in a[0, n) with a[i] > key, computed by one full wave (64-ary search)
-__device__ uint64_t wave_upper_bound(const uint64_t *a, uint64_t n, uint64_t key, int lane) {
-    uint64_t lo = 0, hi = n;
-    while (hi - lo > 64) {
-        uint64_t step = (hi - lo + 63) / 64;
-        uint64_t idx = lo + (uint64_t)lane * step;
-        bool le = idx < hi && a[idx] <= key;
-        int cnt = __popcll(__ballot(le));
-        if (cnt == 0) return lo;  // a[lo] > key
-        uint64_t nlo = lo + (uint64_t)(cnt - 1) * step + 1;
-        uint64_t nhi = lo + (uint64_t)cnt * step;
-        lo = nlo;
-        hi = nhi < hi ? nhi : hi;
-    }
-    uint64_t idx = lo + lane;
-    bool le = idx < hi && a[idx] <= key;
-    return lo + __popcll(__ballot(le));
 }
 
 // ----------------------------------------------------------------- expand
@@ -955,6 +883,349 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
     }
 }
 
+// --------------------------------------------- bidirectional units (v3, default)
+// Reachability is symmetric under edge reversal: with B(t) = expandable nodes that reach
+// t through >= 1 edge, allowed(r, t) <=> r in B(t).  v3 grows BOTH sides of every request
+// of a 16-request unit in one LDS table whose 64-bit state word per node holds, per
+// direction d (0 forward, 1 backward), visited bits << 32d and pending bits << 32d + 16:
+//   * forward from r over the interior subgraph (FRec records, as v2),
+//   * backward from t over interior predecessors (BRec records parallel to rev_col: node
+//     ids put interior nodes first and reverse rows are sorted, so a node's interior
+//     predecessors are exactly the prefix of its reverse row).
+// Seed level: r is marked forward-visited, fint(r) is pushed forward and every entry of
+// rev(t) backward (a source entry can only meet r itself, so it is compared, not stored).
+// A request is allowed as soon as one node carries both of its bits.  Each later level,
+// every open request expands the side whose pending frontier has the smaller degree sum
+// (bidirectional BFS), so the work is bounded by the cheaper side and positives stop
+// where the searches meet.  A request whose pending frontier is empty on either side is
+// false: a path r -> v1 -> ... -> vk = t has v1 in fint(r) and v(k-1) in rev(t), both
+// marked by the seed, so a closed side would already have met the other (no depth
+// cutoff, R2).  Used when the snapshot has no ambiguous keys (R4 flags are raised by
+// forward rows) and record begins fit u32; dynamic roots and table/list overflow spill
+// to the v2 cascade.
+constexpr int kBFront = 384;
+
+template <int U>
+struct BidiShared {
+    uint32_t key[kHash];
+    unsigned long long st[kHash];
+    uint16_t p_sd[2][kBFront];  // pending lists (ping-pong): slot | dir << 15
+    uint32_t p_begin[2][kBFront], p_deg[2][kBFront];
+    uint16_t e_sd[kBFront], e_mask[kBFront];  // this level's expansion list
+    uint32_t e_begin[kBFront], e_deg[kBFront];
+    uint32_t c_pre[kBlock + 1];
+    uint32_t wave_sum[kBlock / 64];
+    uint32_t cost[2][U];
+    uint32_t root[U];
+    uint32_t sel[2];
+    uint32_t n_used, n_e, n_p[2], spill, found, active;
+    unsigned long long cnt_rows, cnt_edges, cnt_rev;
+};
+
+// exclusive block scan of one u32 per thread into S.c_pre; returns the total
+template <class SH>
+__device__ __forceinline__ uint32_t block_scan_sh(uint32_t v, SH &S) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+    }
+    if (lane == 63) S.wave_sum[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; i++) {
+        uint32_t s = S.wave_sum[i];
+        base += i < wv ? s : 0;
+        total += s;
+    }
+    S.c_pre[tid] = base + x - v;
+    if (tid == 0) S.c_pre[kBlock] = total;
+    __syncthreads();
+    return total;
+}
+
+// wave-aggregated append to an LDS list: index of this lane's entry (all lanes call)
+__device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
+    uint64_t bal = __ballot(want);
+    uint32_t base = 0;
+    if (bal) {
+        int leader = __ffsll((unsigned long long)bal) - 1;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (uint32_t)__popcll(bal));
+        base = __shfl(base, leader, 64);
+    }
+    return base + lanes_below(bal);
+}
+
+template <int U>
+__device__ __forceinline__ void bidi_push(BidiShared<U> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
+                                          uint32_t m, int d, int nxt) {
+    int h = -1;
+    bool inserted = false;
+    if (want) {
+        uint32_t hh = hslot(u);
+        for (int p = 0; p < kHash; p++, hh = (hh + 1) & (kHash - 1)) {
+            uint32_t kv = S.key[hh];
+            if (kv == kEmpty) {
+                uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
+                if (prev == kEmpty) {
+                    inserted = true;
+                    h = (int)hh;
+                    break;
+                }
+                kv = prev;
+            }
+            if (kv == u) {
+                h = (int)hh;
+                break;
+            }
+        }
+        if (h < 0) S.spill = 1;
+    }
+    const int lane = threadIdx.x & 63;
+    uint64_t bal = __ballot(inserted);
+    if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
+        uint32_t c = (uint32_t)__popcll(bal);
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)kHashMax) S.spill = 1;
+    }
+    bool app = false;
+    if (h >= 0) {
+        const int vs = 32 * d;
+        // one 64-bit atomic per push: the old word also carries the other direction's
+        // visited bits, so of two pushes that complete a meet the later one sees it
+        unsigned long long old = atomicOr(&S.st[h], (unsigned long long)m << vs);
+        uint32_t newly = m & ~(uint32_t)(old >> vs) & 0xFFFFu;
+        uint32_t meet = newly & (uint32_t)(old >> (32 - vs)) & 0xFFFFu;
+        if (meet) atomicOr(&S.found, meet);
+        newly &= ~meet;
+        if (newly && deg) {
+            unsigned long long o2 = atomicOr(&S.st[h], (unsigned long long)newly << (vs + 16));
+            app = !((uint32_t)(o2 >> (vs + 16)) & 0xFFFFu);
+        }
+    }
+    uint32_t idx = lds_append(app, &S.n_p[nxt]);
+    if (app) {
+        if (idx < (uint32_t)kBFront) {
+            S.p_sd[nxt][idx] = (uint16_t)(h | (d << 15));
+            S.p_begin[nxt][idx] = begin;
+            S.p_deg[nxt][idx] = deg;
+        } else {
+            S.spill = 1;
+        }
+    }
+}
+
+// expand expansion-list entries [base, base + k); block-uniform loop count
+template <int U>
+__device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
+                                            BidiShared<U> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
+    uint32_t dg = (uint32_t)threadIdx.x < k ? S.e_deg[base + threadIdx.x] : 0;
+    uint32_t total = block_scan_sh(dg, S);
+    for (uint32_t eb = 0; eb < total; eb += kBlock) {
+        uint32_t e = eb + threadIdx.x;
+        bool want = e < total;
+        uint32_t u = 0, deg = 0, bg = 0, m = 0;
+        int d = 0;
+        if (want) {
+            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (S.c_pre[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const uint32_t idx = base + lo;
+            d = S.e_sd[idx] >> 15;
+            m = S.e_mask[idx] & S.active & ~*(volatile uint32_t *)&S.found;
+            FRec rc = (d ? brec : frec)[(uint64_t)S.e_begin[idx] + (e - S.c_pre[lo])];
+            u = rc.node;
+            deg = rc.deg;
+            bg = rc.begin;
+            edges++;
+            if (d && u >= g.Ni) {  // a source predecessor of t: it meets only r itself
+                uint32_t hit = 0;
+                for (uint32_t b = m; b; b &= b - 1)
+                    if (S.root[__ffs(b) - 1] == u) hit |= b & (~b + 1);
+                if (hit) atomicOr(&S.found, hit);
+                m = 0;
+            }
+            want = m != 0;
+        }
+        bidi_push<U>(S, want, u, deg, bg, m, d, nxt);
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+                                                      const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                                                      uint64_t *allowed, uint32_t *spill_out,
+                                                      unsigned int *spill_count, unsigned long long *stats,
+                                                      unsigned long long *stamps) {
+    static_assert(U <= 16, "16 request bits per direction");
+    __shared__ BidiShared<U> S;
+    const int tid = threadIdx.x;
+    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
+    const uint64_t unit = blockIdx.x;
+    const uint64_t c0 = unit * U;
+    const int shift = (int)(c0 & 63);
+    for (int i = tid; i < kHash; i += kBlock) {
+        S.key[i] = kEmpty;
+        S.st[i] = 0;
+    }
+    if (tid == 0) {
+        S.n_used = S.n_e = S.n_p[0] = S.n_p[1] = S.spill = S.found = S.active = 0;
+        S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
+    }
+    if (tid < 2 * U) S.cost[tid / U][tid % U] = 0;
+    uint64_t rows = 0, edges = 0;
+    uint32_t n_levels = 0;
+    // seed list: entry j < U = forward row of r_j, entry U + j = reverse row of t_j
+    if (tid < U) {
+        uint64_t c = c0 + tid;
+        uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+        if (c < n) {
+            r = roots[c];
+            t = targets[c];
+        }
+        if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
+        uint64_t fb = 0, fe = 0, rb = 0, re = 0;
+        if (r != KETOGPU_NODE_NONE && r < kDynBase) {
+            fb = g.fint_off[r];
+            fe = g.fint_off[r + 1];
+            rb = g.rev_off[t];
+            re = g.rev_off[t + 1];
+            rows += 2;
+        }
+        S.root[tid] = r;
+        S.e_sd[tid] = 0;
+        S.e_mask[tid] = (uint16_t)(1u << tid);
+        S.e_begin[tid] = (uint32_t)fb;
+        S.e_deg[tid] = (uint32_t)(fe - fb);
+        S.e_sd[U + tid] = (uint16_t)(1u << 15);
+        S.e_mask[U + tid] = (uint16_t)(1u << tid);
+        S.e_begin[U + tid] = (uint32_t)rb;
+        S.e_deg[U + tid] = (uint32_t)(re - rb);
+    }
+    __syncthreads();
+    if (tid < U) {
+        uint32_t r = S.root[tid];
+        if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
+        if (r != KETOGPU_NODE_NONE && r < kDynBase) atomicOr(&S.active, 1u << tid);
+    }
+    __syncthreads();
+    if (S.spill) {
+        if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    // r is forward-visited at distance 0 (interior roots only: a source root can only be
+    // reached backward from rev(t), where it is compared directly)
+    if (tid < 64) {
+        bool v = tid < U && ((S.active >> tid) & 1u) && S.root[tid] < g.Ni;
+        bidi_push<U>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
+    }
+    __syncthreads();
+    if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
+    bidi_expand<U>(g, frec, brec, S, 0, 2 * U, 0, edges);
+    if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
+    int cur = 0;
+    for (;;) {
+        __syncthreads();
+        const uint32_t cnt = S.n_p[cur];
+        const uint32_t act = S.active & ~S.found;
+        if (S.spill || !cnt || !act) break;
+        n_levels++;
+        // per-request pending degree sums per direction
+        for (uint32_t base = 0; base < cnt; base += kBlock) {
+            uint32_t i = base + tid;
+            if (i < cnt) {
+                uint32_t sd = S.p_sd[cur][i], d = sd >> 15;
+                uint32_t pb = (uint32_t)(S.st[sd & 0x7FFFu] >> (32 * d + 16)) & act;
+                uint32_t dg = S.p_deg[cur][i];
+                for (; pb; pb &= pb - 1) atomicAdd(&S.cost[d][__ffs(pb) - 1], dg);
+            }
+        }
+        __syncthreads();
+        const int nxt = cur ^ 1;
+        if (tid < 64) {
+            bool a = tid < U && ((act >> tid) & 1u);
+            uint32_t cf = a ? S.cost[0][tid] : 0, cb = a ? S.cost[1][tid] : 0;
+            uint64_t closed = __ballot(a && (cf == 0 || cb == 0));
+            uint64_t fwd = __ballot(a && cf && cb && cf <= cb);
+            uint64_t bwd = __ballot(a && cf && cb && cf > cb);
+            if (tid < U) S.cost[0][tid] = S.cost[1][tid] = 0;
+            if (tid == 0) {
+                S.active = act & ~(uint32_t)closed;
+                S.sel[0] = (uint32_t)fwd;
+                S.sel[1] = (uint32_t)bwd;
+                S.n_e = 0;
+                S.n_p[nxt] = 0;
+            }
+        }
+        __syncthreads();
+        // split: the chosen direction's bits go to this level's expansion list, open
+        // requests' other bits stay pending (carried to the next list)
+        const uint32_t act2 = S.active;
+        for (uint32_t base = 0; base < cnt; base += kBlock) {
+            uint32_t i = base + tid;
+            uint32_t take = 0, rest = 0, sd = 0;
+            if (i < cnt) {
+                sd = S.p_sd[cur][i];
+                const uint32_t d = sd >> 15, s = sd & 0x7FFFu;
+                uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
+                take = pb & S.sel[d];
+                rest = pb & act2 & ~take;
+                uint32_t clr = pb & ~rest;
+                if (clr) atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
+            }
+            uint32_t ei = lds_append(take != 0, &S.n_e);
+            uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
+            if (take) {  // ei < cnt <= kBFront
+                S.e_sd[ei] = (uint16_t)sd;
+                S.e_mask[ei] = (uint16_t)take;
+                S.e_begin[ei] = S.p_begin[cur][i];
+                S.e_deg[ei] = S.p_deg[cur][i];
+            }
+            if (rest) {  // pi < cnt <= kBFront
+                S.p_sd[nxt][pi] = (uint16_t)sd;
+                S.p_begin[nxt][pi] = S.p_begin[cur][i];
+                S.p_deg[nxt][pi] = S.p_deg[cur][i];
+            }
+        }
+        __syncthreads();
+        const uint32_t ne = S.n_e;
+        for (uint32_t base = 0; base < ne; base += kBlock) {
+            uint32_t k = ne - base < (uint32_t)kBlock ? ne - base : (uint32_t)kBlock;
+            bidi_expand<U>(g, frec, brec, S, base, k, nxt, edges);
+            __syncthreads();
+        }
+        cur = nxt;
+    }
+    __syncthreads();
+    if (S.spill) {
+        if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    if (stamp) stamp[3] = __builtin_amdgcn_s_memtime();
+    wave_stats_add(rows, edges, 0, &S.cnt_rows, &S.cnt_edges, &S.cnt_rev);
+    __syncthreads();
+    if (stamp) {
+        stamp[4] = stamp[3];
+        stamp[5] = n_levels;
+        stamp[6] = S.n_used;
+        stamp[7] = 1;
+    }
+    if (tid == 0) {
+        uint32_t res = S.found & ((1u << U) - 1);
+        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << shift);
+        atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
+        atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
+    }
+}
+
 // ------------------------------------------------- wave-synchronous units
 // Same algorithm as unit_kernel with ONE WAVE per unit: the four waves of a workgroup
 // own four independent LDS partitions, so a BFS level needs no workgroup barrier, only
@@ -1317,7 +1588,9 @@ struct ketogpu_engine {
     bool use_units = true;
     int wave_u = 8;
     bool use_v2 = true;
+    bool use_bidi = true;
     const FRec *frec = nullptr;  // v2 edge records (parallel to fint_col)
+    const FRec *brec = nullptr;  // v3 reverse records (parallel to rev_col)
     unsigned long long *stamps = nullptr;  // KETOGPU_STAMPS=1 diagnostic build
     std::vector<uint64_t> stat_host;
     unsigned lds_pad = 0;  // KETOGPU_LDS_PAD: extra dynamic LDS per workgroup (occupancy experiments)
@@ -1385,14 +1658,18 @@ struct ketogpu_engine {
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
-        // first LDS pass: "v2" (default) = unit2_kernel, one workgroup per 16 requests with
-        // edge records; "b16" = unit_kernel; "w4" / "w8" / "w16" = one wave per 4/8/16
-        // requests.  Spills go on to 4-request and 1-request units, then the global path.
+        // first LDS pass: "bidi" (default) = bidi_kernel, bidirectional search per request,
+        // spills continue on the v2 cascade; "v2" = unit2_kernel, one workgroup per 16
+        // requests with edge records; "b16" = unit_kernel; "w4" / "w8" / "w16" = one wave
+        // per 4/8/16 requests.  Spills go on to 4-request and 1-request units, then the
+        // global path.
         const char *plan = getenv("KETOGPU_UNITS");
-        std::string p = plan ? plan : "v2";
+        std::string p = plan ? plan : "bidi";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        use_v2 = p == "v2";
+        use_v2 = p == "v2" || p == "bidi";
         if (use_v2 && s.fint_col.size() >= (1ull << 32)) use_v2 = false;  // record begins are u32
+        // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
+        use_bidi = p == "bidi" && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
         if (getenv("KETOGPU_STAMPS")) {
             stamps = dalloc<unsigned long long>((size_t)65536 * 8);
@@ -1425,6 +1702,20 @@ struct ketogpu_engine {
                 rec[e] = FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u], 0};
             }
             frec = up(rec);
+        }
+        if (use_bidi) {
+            // interior predecessors of v = the prefix of rev(v) below Ni (sorted rows)
+            std::vector<uint32_t> ideg(s.Ni);
+            for (uint32_t v = 0; v < s.Ni; v++) {
+                const uint32_t *b = s.rev_col.data() + s.rev_off[v], *e = s.rev_col.data() + s.rev_off[v + 1];
+                ideg[v] = (uint32_t)(std::lower_bound(b, e, s.Ni) - b);
+            }
+            std::vector<FRec> rec(s.rev_col.size());
+            for (size_t e = 0; e < rec.size(); e++) {
+                uint32_t v = s.rev_col[e];
+                rec[e] = v < s.Ni ? FRec{v, ideg[v], (uint32_t)s.rev_off[v], 0} : FRec{v, 0, 0, 0};
+            }
+            brec = up(rec);
         }
 
         size_t free_b = 0, total_b = 0;
@@ -1540,37 +1831,62 @@ struct ketogpu_engine {
         }
         uint64_t units = (q.n + 15) / 16;
         uint64_t left = 0;
-        for (int pass = 0; pass < 3; pass++) {
-            if (use_v2) {
-                uint64_t grid = pass == 0 ? units : left * 4;
-                if (!grid) break;
-                uint32_t *in = pass == 0 ? nullptr : list[(pass - 1) & 1], *out = list[pass & 1];
+        if (use_v2) {
+            // stage 0 covers every 16-request unit; each later stage re-runs the previous
+            // stage's spilled units split `fan` ways: bidi<16> -> unit2<16> -> unit2<4> -> unit2<1>
+            struct Stage {
+                int kind, u;
+                uint32_t fan;
+            };
+            std::vector<Stage> stages;
+            if (use_bidi) stages.push_back({0, 16, 1});
+            stages.push_back({1, 16, 1});
+            stages.push_back({1, 4, 4});
+            stages.push_back({1, 1, 4});
+            for (size_t si = 0; si < stages.size(); si++) {
+                const Stage &sg = stages[si];
+                uint64_t grid = si == 0 ? units : left * sg.fan;
+                if (!grid) return 0;
+                uint32_t *in = si == 0 ? nullptr : list[(si - 1) & 1], *out = list[si & 1];
+                unsigned long long *stp = si == 0 ? stamps : nullptr;
+                unsigned pad = si == 0 ? lds_pad : 0;
                 HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
                 hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
-                if (pass == 0)
-                    hipLaunchKernelGGL(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), lds_pad, stream, g, frec,
-                                       q.roots, q.targets, q.n, q.allowed, q.flags, nullptr, 1u, out, spill_count,
-                                       st.stats, stamps);
-                else if (pass == 1)
+                if (sg.kind == 0)
+                    hipLaunchKernelGGL(bidi_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec, brec,
+                                       q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
+                else if (sg.u == 16)
+                    hipLaunchKernelGGL(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec,
+                                       q.roots, q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count,
+                                       st.stats, stp);
+                else if (sg.u == 4)
                     hipLaunchKernelGGL(unit2_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+                                       q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count, st.stats,
+                                       nullptr);
                 else
                     hipLaunchKernelGGL(unit2_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
+                                       q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count, st.stats,
+                                       nullptr);
                 HIP_CHECK(hipEventRecord(b, stream));
                 unit_ev.push_back({a, b});
                 left = read_spill_count();
                 rs.spilled_units += left;
                 rs.push_launches++;
                 rs.unit_launches++;
-                if (pass == 0) {  // the dominant launch: keep its own byte count
+                if (si == 0) {  // the dominant launch: keep its own byte count
                     uint64_t t3[3];
                     read_unit_stats(t3);
                     rs.main_bytes = 16 * t3[0] + 16 * t3[1] + 4 * t3[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
                 }
-                continue;
             }
+            // the global path reads the last stage's single requests from list[0]
+            uint32_t *last = list[(stages.size() - 1) & 1];
+            if (left && last != list[0])
+                HIP_CHECK(hipMemcpyAsync(list[0], last, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+            return left;
+        }
+        for (int pass = 0; pass < 3; pass++) {
             uint64_t grid = pass == 0 ? units : left * 4;
             if (!grid) return 0;
             uint32_t *in = pass == 0 ? nullptr : list[(pass - 1) & 1], *out = list[pass & 1];

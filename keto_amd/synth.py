@@ -82,8 +82,8 @@ class Workload:
         self.counts = {"parent": v.n_parent, "member": v.n_member, "grant": v.n_grant, "tuples": n}
 
     def __del__(self):
-        if getattr(self, "h", None):
-            slib().ks_rbac_free(self.h)
+        if getattr(self, "h", None) and _slib is not None:
+            _slib.ks_rbac_free(self.h)
             self.h = None
 
     def request_batch(self):

@@ -1,0 +1,118 @@
+"""Summarise the rocprofv3 output of tools/profile.sh into profiles/<tag>/.
+
+    python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles/<tag> [--workload config2_rbac]
+
+Reads the kernel-trace stats (trace/**/*kernel_stats.csv, *kernel_trace.csv) and one
+--pmc directory per counter pass (pmc_*/**/*counter_collection.csv) and writes
+  kernel_stats.csv   the rocprofv3 --stats summary, copied as is
+  traffic.json       per kernel family: average duration (kernel trace), resources of the
+                     dispatch, per-dispatch average of every counter, and HBM bytes per
+                     launch from FETCH_SIZE/WRITE_SIZE (KB in rocprofv3) — raw, and with
+                     FETCH_SIZE doubled as MI355X_MICROARCH.md "HBM" prescribes for gfx950
+                     (128-B read requests tallied at 64 B).  bench.py reads
+                     kernels[<family>].hbm_bytes_per_launch for roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+FAMILIES = [
+    ("bidi_kernel<16>", r"bidi_kernel<16"),
+    ("unit2_kernel<16>", r"unit2_kernel<16>"),
+    ("unit2_kernel<4>+<1> (spill passes)", r"unit2_kernel<(4|1)>"),
+    ("unit_kernel", r"[^2]unit_kernel<"),
+    ("expand_kernel", r"\bexpand_kernel"),
+    ("pull_kernel", r"\bpull_kernel"),
+    ("reset_kernel", r"\breset_kernel"),
+    ("gather_kernel", r"\bgather_kernel"),
+    ("seed_kernel", r"\bseed_kernel"),
+    ("part_expand_kernel", r"part_expand_kernel"),
+    ("part_apply_kernel", r"part_apply_kernel"),
+]
+
+
+def family(name):
+    for fam, rx in FAMILIES:
+        if re.search(rx, name):
+            return fam
+    return None
+
+
+def read_csv(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def summarise(src, workload):
+    out = {"workload": workload, "source": src, "kernels": {}}
+    dur = defaultdict(list)
+    res = {}
+    for tr in glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        for r in read_csv(tr):
+            fam = family(r.get("Kernel_Name", ""))
+            if not fam:
+                continue
+            dur[fam].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            res[fam] = {k: r[k] for k in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size",
+                                          "Workgroup_Size", "Grid_Size") if k in r}
+    per = defaultdict(lambda: defaultdict(list))
+    for cc in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+        by_dispatch = defaultdict(lambda: defaultdict(float))
+        names = {}
+        for r in read_csv(cc):
+            fam = family(r.get("Kernel_Name", ""))
+            if not fam:
+                continue
+            d = (cc, r.get("Dispatch_Id"), r.get("Agent_Id"))
+            by_dispatch[d][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[d] = fam
+        for d, ctrs in by_dispatch.items():
+            for c, v in ctrs.items():
+                per[names[d]][c].append(v)
+    for fam in sorted(set(per) | set(dur)):
+        k = {"dispatches_timed": len(dur.get(fam, []))}
+        if dur.get(fam):
+            k["avg_duration_ms"] = sum(dur[fam]) / len(dur[fam]) / 1e6
+        k["resources"] = res.get(fam)
+        c = {n: sum(v) / len(v) for n, v in sorted(per[fam].items())}
+        k["counters"] = c
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            k["hbm_bytes_per_launch_raw"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            k["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            if k.get("avg_duration_ms"):
+                k["hbm_GBps"] = k["hbm_bytes_per_launch"] / (k["avg_duration_ms"] * 1e-3) / 1e9
+        if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+            k["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        if c.get("SQ_WAVE_CYCLES", 0) > 0:
+            for part in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if part in c:
+                    k[part.lower() + "_frac"] = c[part] / c["SQ_WAVE_CYCLES"]
+        out["kernels"][fam] = k
+    out["note"] = ("FETCH_SIZE/WRITE_SIZE are KB per dispatch; hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
+                   "(gfx950 read correction, MI355X_MICROARCH.md 'HBM'); *_raw without the doubling.  The counters "
+                   "sit at the L2's memory side, so Infinity-Cache hits are included.")
+    return out
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    workload = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "config2_rbac"
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    out = summarise(src, workload)
+    with open(os.path.join(dst, "traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({fam: {kk: v.get(kk) for kk in ("avg_duration_ms", "hbm_bytes_per_launch", "hbm_GBps",
+                                                      "l2_hit_rate")}
+                      for fam, v in out["kernels"].items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
