@@ -252,6 +252,59 @@ typedef struct {
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 
+/* ------------------------------------------------------- partitioned mode */
+/* Hash-partitioned traversal for graphs that do not fit one GPU (BASELINE config #5,
+ * SURVEY.md 8(e)); replaces the same SubjectIsAllowed recursion as ketogpu_check_ids
+ * (internal/check/engine.go:33-95), spread over ranks.  Node v is owned by rank
+ * ketogpu_part_owner(v, world) = mix64(v) % world; a rank holds the forward interior rows
+ * and traversal state of its expandable nodes and the reverse rows of its nodes.  These
+ * calls are one rank's device steps of a round; the caller moves the records between
+ * ranks (keto_amd/partition.py: torch.distributed all_to_all over RCCL):
+ *   begin -> { emit -> [all-to-all] -> apply -> [all-reduce frontier; stop at 0] -> expand }
+ *         -> pull_emit -> [all-to-all] -> pull_answer -> end   (answer = OR of end() bits)
+ * Buffers named *_dev are device memory on the rank's GPU.  A step that returns
+ * KETOGPU_ENOMEM (buffers too small for this round) leaves the round to ketogpu_part_abort;
+ * every rank must then abort and retry with fewer requests per round.  Snapshots with
+ * ambiguous Subject.String() keys are refused (KETOGPU_EINVAL). */
+typedef struct ketogpu_part ketogpu_part;
+typedef struct {
+    uint32_t a; /* BFS: 64-request word of the round; pull: request index of the round */
+    uint32_t b; /* node id (global) — its owner receives the record                     */
+    uint64_t m; /* BFS: request bits of word a; pull: 0                                  */
+} ketogpu_record;
+typedef struct {
+    int32_t device;
+    int32_t rank, world;          /* world <= 64                                       */
+    uint64_t record_capacity;     /* outgoing records per step; 0 = auto               */
+    uint32_t max_words_per_round; /* 0 = auto (state budget)                           */
+    uint64_t state_budget_bytes;  /* 0 = auto                                          */
+} ketogpu_part_opts;
+typedef struct {
+    uint64_t owned_interior, owned_expandable, owned_forward_edges, owned_reverse_edges;
+    uint64_t rounds, levels, frontier_entries, forward_edges;
+    uint64_t records_sent, records_received, queries_answered;
+} ketogpu_part_stats;
+uint32_t ketogpu_part_owner(uint32_t node, int32_t world);
+int ketogpu_part_new(const ketogpu_snapshot *s, const ketogpu_part_opts *opts, ketogpu_part **out);
+void ketogpu_part_free(ketogpu_part *p);
+/* 64-request words one round holds */
+uint64_t ketogpu_part_round_words(const ketogpu_part *p);
+/* same (roots, targets) host arrays on every rank, n <= 64 * round_words */
+int ketogpu_part_begin(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n);
+/* this step's outgoing records grouped by destination rank into send_dev; counts[world] */
+int ketogpu_part_emit(ketogpu_part *p, ketogpu_record *send_dev, uint64_t capacity, uint64_t *counts);
+/* OR received records into the owned state; *frontier = owned entries of the next level */
+int ketogpu_part_apply(ketogpu_part *p, const ketogpu_record *recv_dev, uint64_t n, uint64_t *frontier);
+/* the owned frontier's rows -> the next emit's records */
+int ketogpu_part_expand(ketogpu_part *p);
+/* after the last level: direct hits of owned targets + queries (request, interior node) */
+int ketogpu_part_pull_emit(ketogpu_part *p, ketogpu_record *send_dev, uint64_t capacity, uint64_t *counts);
+int ketogpu_part_pull_answer(ketogpu_part *p, const ketogpu_record *recv_dev, uint64_t n);
+/* this rank's hit bits of the round (ceil(n/64) host words) and state reset */
+int ketogpu_part_end(ketogpu_part *p, uint64_t *allowed_bits);
+int ketogpu_part_abort(ketogpu_part *p);
+int ketogpu_part_stats_get(const ketogpu_part *p, ketogpu_part_stats *out);
+
 /* ------------------------------------------------------------------ expand */
 /* BuildTree(subject, rest_depth).  *out = NULL is the nil tree (JSON null).
  * KETOGPU_ENOTFOUND when a fetched page references an unknown namespace. */

@@ -102,6 +102,24 @@ class TreeNode(C.Structure):
     _fields_ = [("type", C.c_int32), ("num_children", C.c_uint32), ("subject", Subject)]
 
 
+class Record(C.Structure):
+    _fields_ = [("a", C.c_uint32), ("b", C.c_uint32), ("m", C.c_uint64)]
+
+
+class PartOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("record_capacity", C.c_uint64),
+                ("max_words_per_round", C.c_uint32), ("state_budget_bytes", C.c_uint64)]
+
+
+class PartStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "owned_interior", "owned_expandable", "owned_forward_edges", "owned_reverse_edges", "rounds", "levels",
+        "frontier_entries", "forward_edges", "records_sent", "records_received", "queries_answered")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 # every symbol declared in include/ketogpu.h, with its ctypes signature
 vp, i32, u32, sz = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
 SIGNATURES = {
@@ -131,6 +149,19 @@ SIGNATURES = {
     "ketogpu_abi_version": (C.c_int, []),
     "ketogpu_free": (None, [vp]),
     "ketogpu_device_count": (C.c_int, []),
+    "ketogpu_part_owner": (C.c_uint32, [u32, i32]),
+    "ketogpu_part_new": (C.c_int, [vp, C.POINTER(PartOpts), C.POINTER(vp)]),
+    "ketogpu_part_free": (None, [vp]),
+    "ketogpu_part_round_words": (C.c_uint64, [vp]),
+    "ketogpu_part_begin": (C.c_int, [vp, vp, vp, sz]),
+    "ketogpu_part_emit": (C.c_int, [vp, vp, C.c_uint64, vp]),
+    "ketogpu_part_apply": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "ketogpu_part_expand": (C.c_int, [vp]),
+    "ketogpu_part_pull_emit": (C.c_int, [vp, vp, C.c_uint64, vp]),
+    "ketogpu_part_pull_answer": (C.c_int, [vp, vp, C.c_uint64]),
+    "ketogpu_part_end": (C.c_int, [vp, vp]),
+    "ketogpu_part_abort": (C.c_int, [vp]),
+    "ketogpu_part_stats_get": (C.c_int, [vp, C.POINTER(PartStats)]),
 }
 
 _lib = None

@@ -1,0 +1,722 @@
+// partition.hip — hash-partitioned traversal for graphs that do not fit one GPU
+// (BASELINE.json config #5).
+//
+// Node v is owned by rank owner(v) = mix64(v) mod world.  A rank holds, for the nodes
+// it owns: the forward interior rows and the 64-request traversal state of its
+// expandable nodes, and the reverse rows of its nodes.  One round checks up to 64*W
+// requests (W words of the multi-source bitmask BFS of SURVEY.md 8(a)):
+//   begin      owned roots r seed (word, u, bit) for u in fint(r)
+//   emit       outgoing records grouped by owner(u) into the caller's send buffer
+//   [exchange] all-to-all of counts, then records (keto_amd/partition.py: RCCL)
+//   apply      received masks OR'd into vis[word][u]; bits new to u enter the frontier
+//   [all-reduce of the frontier size: stop at 0 — no depth cutoff, R2]
+//   expand     the owned frontier's rows -> next outgoing records
+//   pull_emit  for owned targets t: r in rev(t) is a direct hit, every interior v in
+//              rev(t) becomes a query (request, v) for owner(v)
+//   pull_answer  a query is a hit when vis[word][v] has the request's bit
+//   end        this rank's hit bits; the answer is their OR over ranks
+// The check formula is the one the single-GPU engines use: allowed(r, t)
+// <=> r in rev(t) or rev(t) ∩ X(r) != {} with X(r) the interior closure of r.
+// Snapshots with ambiguous Subject.String() keys (R4) are refused: their exact
+// re-evaluation needs the whole graph on one host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "device_util.hpp"
+#include "ketogpu_internal.hpp"
+
+using namespace ketogpu;
+using namespace kdev;
+
+namespace {
+
+constexpr int kPB = 256;
+constexpr int kPItems = 4;
+constexpr int kPTile = kPB * kPItems;
+constexpr uint32_t kMaxWorld = 64;
+
+__host__ __device__ __forceinline__ uint32_t part_owner(uint32_t v, uint32_t world) {
+    uint64_t x = v;
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return (uint32_t)(x % world);
+}
+
+struct PartDev {
+    uint32_t world, Ni, Nx, N, Nil;
+    const uint32_t *lx;      // [Nx] local id of an owned expandable node (interior first) or NONE
+    const uint64_t *lf_off;  // [Nxl + 1] forward interior rows of owned expandable nodes
+    const uint32_t *lf_col;  //           (global node ids)
+    const uint32_t *lt;      // [N] local reverse row of an owned node or NONE
+    const uint64_t *lr_off;  // [Ntl + 1] reverse rows of owned nodes (global ids, sorted)
+    const uint32_t *lr_col;
+    uint64_t *vis, *nxt;     // [W][Nil]
+    uint64_t *fe_key, *fe_pre, *fe_mask;
+    uint64_t fe_cap;
+    uint64_t *touch;
+    uint64_t touch_cap;
+    ketogpu_record *obuf;    // outgoing records of the current step (unordered)
+    uint64_t ocap;
+    unsigned long long *ctr;  // [0..1] frontier counters (ping-pong), [2] touch, [3] obuf
+    unsigned int *overflow;   // bit 0 list/buffer overflow, bit 1 misrouted record
+    uint64_t *allowed;        // this rank's hit bits of the round
+    const uint32_t *roots, *targets;
+    uint64_t n;
+};
+
+// append a record to obuf with one atomic per wave (all lanes call)
+__device__ __forceinline__ void emit_rec(bool want, uint32_t a, uint32_t b, uint64_t m, const PartDev &P) {
+    uint64_t bal = __ballot(want);
+    if (!bal) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(&P.ctr[3], (unsigned long long)__popcll(bal));
+    base = __shfl(base, leader, 64);
+    if (want) {
+        uint64_t idx = base + __popcll(bal & ((1ull << lane) - 1));
+        if (idx < P.ocap)
+            P.obuf[idx] = ketogpu_record{a, b, m};
+        else
+            atomicOr(P.overflow, 1u);
+    }
+}
+
+// owned roots: (word, u, bit) for every interior successor u
+__global__ __launch_bounds__(kPB) void part_seed_kernel(PartDev P) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    uint64_t b = 0, e = 0, m = 0;
+    uint32_t w = 0;
+    if (i < P.n) {
+        uint32_t r = P.roots[i], t = P.targets[i];
+        if (r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE && r < P.Nx) {
+            uint32_t l = P.lx[r];
+            if (l != KETOGPU_NODE_NONE) {
+                b = P.lf_off[l];
+                e = P.lf_off[l + 1];
+                w = (uint32_t)(i >> 6);
+                m = 1ull << (i & 63);
+            }
+        }
+    }
+    for (uint64_t k = b;; k++) {
+        bool want = k < e;
+        if (!__ballot(want)) break;
+        emit_rec(want, w, want ? P.lf_col[k] : 0, m, P);
+    }
+}
+
+// load-balanced expansion of frontier entries [ent_begin, ent_begin + ent_count)
+// (row-length prefix in fe_pre) into outgoing records
+__global__ __launch_bounds__(kPB) void part_expand_kernel(PartDev P, uint64_t ent_begin, uint64_t ent_count,
+                                                          uint64_t total_edges) {
+    __shared__ uint64_t s_pre[kPTile + 1];
+    __shared__ uint64_t s_first, s_count;
+    const int lane = threadIdx.x & 63;
+    const uint64_t *pre = P.fe_pre + ent_begin;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kPTile; t0 < total_edges; t0 += (uint64_t)gridDim.x * kPTile) {
+        const uint64_t t1 = t0 + kPTile < total_edges ? t0 + kPTile : total_edges;
+        if (threadIdx.x < 64) {
+            uint64_t i0 = wave_upper_bound(pre, ent_count, t0, lane) - 1;
+            uint64_t i1 = wave_upper_bound(pre, ent_count, t1 - 1, lane) - 1;
+            if (lane == 0) {
+                s_first = i0;
+                s_count = i1 - i0 + 1;
+            }
+        }
+        __syncthreads();
+        const uint64_t first = s_first, count = s_count;
+        for (uint64_t j = threadIdx.x; j <= count; j += kPB)
+            s_pre[j] = (first + j < ent_count) ? pre[first + j] : total_edges;
+        __syncthreads();
+#pragma unroll 1
+        for (int it = 0; it < kPItems; it++) {
+            const uint64_t e = t0 + (uint64_t)it * kPB + threadIdx.x;
+            bool want = e < t1;
+            uint32_t w = 0, u = 0;
+            uint64_t m = 0;
+            if (want) {
+                uint64_t lo = 0, hi = count;  // entry j: s_pre[j] <= e < s_pre[j+1]
+                while (hi - lo > 1) {
+                    uint64_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= e)
+                        lo = mid;
+                    else
+                        hi = mid;
+                }
+                const uint64_t ent = ent_begin + first + lo;
+                const uint64_t k = P.fe_key[ent];
+                w = (uint32_t)(k >> 32);
+                const uint32_t l = (uint32_t)k;
+                m = P.fe_mask[ent];
+                u = P.lf_col[P.lf_off[l] + (e - s_pre[lo])];
+            }
+            emit_rec(want, w, u, m, P);
+        }
+        __syncthreads();
+    }
+}
+
+// per-destination record counts (LDS histogram, one global atomic per rank per block)
+__global__ __launch_bounds__(kPB) void part_count_kernel(const ketogpu_record *rec, uint64_t n, uint32_t world,
+                                                         unsigned long long *counts) {
+    __shared__ uint32_t h[kMaxWorld];
+    if (threadIdx.x < kMaxWorld) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kPB)
+        atomicAdd(&h[part_owner(rec[i].b, world)], 1u);
+    __syncthreads();
+    if (threadIdx.x < world && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+// records -> out grouped by destination (cursor[g] starts at the group's offset); each
+// block reserves its share of every group once per 256-record tile
+__global__ __launch_bounds__(kPB) void part_scatter_kernel(const ketogpu_record *rec, uint64_t n, uint32_t world,
+                                                           unsigned long long *cursor, ketogpu_record *out) {
+    __shared__ uint32_t h[kMaxWorld];
+    __shared__ unsigned long long base[kMaxWorld];
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kPB; t0 < n; t0 += (uint64_t)gridDim.x * kPB) {
+        if (threadIdx.x < kMaxWorld) h[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t i = t0 + threadIdx.x;
+        const bool have = i < n;
+        ketogpu_record r{0, 0, 0};
+        uint32_t o = 0, pos = 0;
+        if (have) {
+            r = rec[i];
+            o = part_owner(r.b, world);
+            pos = atomicAdd(&h[o], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < world && h[threadIdx.x])
+            base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+        __syncthreads();
+        if (have) out[base[o] + pos] = r;
+        __syncthreads();
+    }
+}
+
+// received (word, u, mask): OR into the owned state, new bits enter the next frontier
+__global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogpu_record *rec, uint64_t n,
+                                                         uint64_t out_base, unsigned long long *out_ctr) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    bool app = false, touched = false;
+    uint64_t key = 0, deg = 0;
+    if (i < n) {
+        const ketogpu_record r = rec[i];
+        const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
+        if (l < P.Nil) {
+            const size_t slot = (size_t)r.a * P.Nil + l;
+            const uint64_t nw = r.m & ~P.vis[slot];
+            if (nw) {
+                const uint64_t old = atomicOr((unsigned long long *)&P.vis[slot], (unsigned long long)nw);
+                const uint64_t newly = nw & ~old;
+                if (newly) {
+                    key = ((uint64_t)r.a << 32) | l;
+                    const uint64_t d = P.lf_off[l + 1] - P.lf_off[l];
+                    if (d) {
+                        const uint64_t o2 = atomicOr((unsigned long long *)&P.nxt[slot], (unsigned long long)newly);
+                        if (!o2) {
+                            app = true;
+                            deg = d;
+                        }
+                    } else if (!old) {
+                        touched = true;  // vis-only entry: recorded once for the reset
+                    }
+                }
+            }
+        } else {
+            atomicOr(P.overflow, 2u);  // not an interior node of this rank
+        }
+    }
+    wave_append(app, key, deg, lane, out_ctr, out_base, P.fe_cap, P.fe_key, P.fe_pre, nullptr, 0, P.overflow);
+    wave_touch(touched, key, lane, &P.ctr[2], P.touch, P.touch_cap, P.overflow);
+}
+
+// next level's masks: nxt -> entry list, nxt cleared
+__global__ __launch_bounds__(kPB) void part_gather_kernel(PartDev P, uint64_t b, uint64_t e) {
+    const uint64_t i = b + (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    if (i >= e) return;
+    const uint64_t k = P.fe_key[i];
+    const size_t slot = (size_t)(k >> 32) * P.Nil + (uint32_t)k;
+    P.fe_mask[i] = P.nxt[slot];
+    P.nxt[slot] = 0;
+}
+
+// owned targets: direct hits (r in rev(t)) and queries (request, interior v in rev(t))
+__global__ __launch_bounds__(kPB) void part_pull_emit_kernel(PartDev P) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    uint64_t b = 0, e = 0;
+    uint32_t r = KETOGPU_NODE_NONE;
+    if (i < P.n) {
+        const uint32_t t = P.targets[i];
+        r = P.roots[i];
+        if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
+            const uint32_t lt = P.lt[t];
+            if (lt != KETOGPU_NODE_NONE) {
+                b = P.lr_off[lt];
+                e = P.lr_off[lt + 1];
+            }
+        }
+    }
+    bool hit = false;
+    for (uint64_t k = b;; k++) {
+        const bool more = k < e && !hit;
+        if (!__ballot(more)) break;
+        bool q = false;
+        uint32_t v = 0;
+        if (more) {
+            v = P.lr_col[k];
+            if (v == r)
+                hit = true;
+            else
+                q = v < P.Ni;
+        }
+        emit_rec(q, (uint32_t)i, v, 0, P);
+    }
+    if (hit) atomicOr((unsigned long long *)&P.allowed[i >> 6], 1ull << (i & 63));
+}
+
+__global__ __launch_bounds__(kPB) void part_pull_answer_kernel(PartDev P, const ketogpu_record *rec, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    if (i >= n) return;
+    const ketogpu_record r = rec[i];
+    const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
+    if (l >= P.Nil || r.a >= P.n) {
+        atomicOr(P.overflow, 2u);
+        return;
+    }
+    if ((P.vis[(size_t)(r.a >> 6) * P.Nil + l] >> (r.a & 63)) & 1ull)
+        atomicOr((unsigned long long *)&P.allowed[r.a >> 6], 1ull << (r.a & 63));
+}
+
+__global__ __launch_bounds__(kPB) void part_reset_kernel(uint64_t *vis, uint32_t Nil, const uint64_t *keys, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    vis[(size_t)(k >> 32) * Nil + (uint32_t)k] = 0;
+}
+
+inline unsigned pblocks(uint64_t n) { return (unsigned)std::max<uint64_t>(1, (n + kPB - 1) / kPB); }
+
+#define PHIP(x)                                                                                        \
+    do {                                                                                               \
+        hipError_t _e = (x);                                                                           \
+        if (_e != hipSuccess) throw Error(KETOGPU_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+template <class T>
+T *palloc(size_t n) {
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) throw Error(KETOGPU_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return (T *)p;
+}
+
+}  // namespace
+
+struct ketogpu_part {
+    int device = 0;
+    uint32_t rank = 0, world = 1;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    PartDev P{};
+    std::vector<void *> owned;
+    uint64_t W = 1;                  // words per round
+    uint32_t *d_roots = nullptr, *d_targets = nullptr;
+    unsigned long long *d_counts = nullptr, *d_cursor = nullptr;
+    unsigned long long *h = nullptr;  // pinned: counters and counts
+    // frontier bookkeeping of the round
+    uint64_t lb = 0, cnt = 0, edges = 0;
+    int cur = 0;
+    bool dirty = false;  // state may hold bits a sparse reset does not know about
+    ketogpu_part_stats stats{};
+
+    ~ketogpu_part() {
+        if (stream) {
+            (void)hipSetDevice(device);
+            (void)hipStreamSynchronize(stream);
+        }
+        for (void *p : owned) (void)hipFree(p);
+        if (h) (void)hipHostFree(h);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    template <class T>
+    T *own(T *p) {
+        owned.push_back((void *)p);
+        return p;
+    }
+    template <class T>
+    T *upload(const std::vector<T> &v) {
+        T *p = own(palloc<T>(v.size()));
+        if (!v.empty()) PHIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        return p;
+    }
+
+    void init(const Snapshot &s, const ketogpu_part_opts &o) {
+        if (o.world < 1 || (uint32_t)o.world > kMaxWorld || o.rank < 0 || o.rank >= o.world)
+            throw Error(KETOGPU_EINVAL, "partition: need 0 <= rank < world <= 64");
+        if (s.has_ambiguous)
+            throw Error(KETOGPU_EINVAL, "partition: snapshots with ambiguous Subject.String() keys (R4) are not supported");
+        device = o.device;
+        rank = (uint32_t)o.rank;
+        world = (uint32_t)o.world;
+        int ndev = 0;
+        PHIP(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) throw Error(KETOGPU_EDEVICE, "no such HIP device");
+        PHIP(hipSetDevice(device));
+        PHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        // local numbering: owned interior nodes [0, Nil), then owned sources
+        std::vector<uint32_t> lx(s.Nx, NONE);
+        std::vector<uint32_t> order;
+        for (uint32_t v = 0; v < s.Ni; v++)
+            if (part_owner(v, world) == rank) lx[v] = (uint32_t)order.size(), order.push_back(v);
+        const uint32_t Nil = (uint32_t)order.size();
+        for (uint32_t v = s.Ni; v < s.Nx; v++)
+            if (part_owner(v, world) == rank) lx[v] = (uint32_t)order.size(), order.push_back(v);
+        std::vector<uint64_t> lf_off{0};
+        std::vector<uint32_t> lf_col;
+        for (uint32_t v : order) {
+            lf_col.insert(lf_col.end(), s.fint_col.begin() + s.fint_off[v], s.fint_col.begin() + s.fint_off[v + 1]);
+            lf_off.push_back(lf_col.size());
+        }
+        std::vector<uint32_t> lt(s.N, NONE);
+        std::vector<uint64_t> lr_off{0};
+        std::vector<uint32_t> lr_col;
+        for (uint32_t t = 0; t < s.N; t++) {
+            if (part_owner(t, world) != rank || s.rev_off[t + 1] == s.rev_off[t]) continue;
+            lt[t] = (uint32_t)(lr_off.size() - 1);
+            lr_col.insert(lr_col.end(), s.rev_col.begin() + s.rev_off[t], s.rev_col.begin() + s.rev_off[t + 1]);
+            lr_off.push_back(lr_col.size());
+        }
+        P.world = world;
+        P.Ni = s.Ni;
+        P.Nx = s.Nx;
+        P.N = s.N;
+        P.Nil = Nil;
+        P.lx = upload(lx);
+        P.lf_off = upload(lf_off);
+        P.lf_col = upload(lf_col);
+        P.lt = upload(lt);
+        P.lr_off = upload(lr_off);
+        P.lr_col = upload(lr_col);
+        stats.owned_interior = Nil;
+        stats.owned_expandable = order.size();
+        stats.owned_forward_edges = lf_col.size();
+        stats.owned_reverse_edges = lr_col.size();
+
+        size_t free_b = 0, total_b = 0;
+        PHIP(hipMemGetInfo(&free_b, &total_b));
+        uint64_t budget = o.state_budget_bytes ? o.state_budget_bytes : std::min<uint64_t>(free_b / 4, 32ull << 30);
+        budget = std::min<uint64_t>(budget, (uint64_t)free_b / 2);
+        uint64_t lists = budget / 4;
+        P.fe_cap = std::max<uint64_t>(lists / 32, 1 << 16);
+        P.touch_cap = P.fe_cap;
+        P.ocap = o.record_capacity ? o.record_capacity : std::max<uint64_t>(lists / 16, 1 << 16);
+        W = std::max<uint64_t>(1, (budget - std::min(budget, lists + P.ocap * 16)) / (16ull * std::max<uint32_t>(Nil, 1)));
+        if (o.max_words_per_round) W = std::min<uint64_t>(W, o.max_words_per_round);
+        W = std::min<uint64_t>(W, 1u << 16);
+        const size_t state = (size_t)W * std::max<uint32_t>(Nil, 1);
+        P.vis = own(palloc<uint64_t>(state));
+        P.nxt = own(palloc<uint64_t>(state));
+        PHIP(hipMemsetAsync(P.vis, 0, state * 8, stream));
+        PHIP(hipMemsetAsync(P.nxt, 0, state * 8, stream));
+        P.fe_key = own(palloc<uint64_t>(P.fe_cap));
+        P.fe_pre = own(palloc<uint64_t>(P.fe_cap));
+        P.fe_mask = own(palloc<uint64_t>(P.fe_cap));
+        P.touch = own(palloc<uint64_t>(P.touch_cap));
+        P.obuf = own(palloc<ketogpu_record>(P.ocap));
+        P.ctr = own(palloc<unsigned long long>(8));
+        P.overflow = own(palloc<unsigned int>(4));
+        P.allowed = own(palloc<uint64_t>(W));
+        d_roots = own(palloc<uint32_t>(W * 64));
+        d_targets = own(palloc<uint32_t>(W * 64));
+        d_counts = own(palloc<unsigned long long>(kMaxWorld));
+        d_cursor = own(palloc<unsigned long long>(kMaxWorld));
+        PHIP(hipHostMalloc((void **)&h, (16 + 2 * kMaxWorld) * sizeof(unsigned long long), hipHostMallocDefault));
+        P.roots = d_roots;
+        P.targets = d_targets;
+        PHIP(hipStreamSynchronize(stream));
+    }
+
+    void read_ctr() {
+        PHIP(hipMemcpyAsync(h, P.ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+        PHIP(hipMemcpyAsync(h + 4, P.overflow, sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+        PHIP(hipStreamSynchronize(stream));
+    }
+    uint32_t overflow_bits() const { return (uint32_t)h[4]; }
+
+    void begin(const uint32_t *roots, const uint32_t *targets, uint64_t n) {
+        if (dirty) reset(true);
+        if (n > W * 64) throw Error(KETOGPU_EINVAL, "partition: more requests than one round holds");
+        for (uint64_t i = 0; i < n; i++)
+            if ((roots[i] != NONE && roots[i] >= P.Nx) || (targets[i] != NONE && targets[i] >= P.N))
+                throw Error(KETOGPU_EINVAL, "request " + std::to_string(i) + " has a node id outside the snapshot");
+        P.n = n;
+        dirty = true;
+        if (n) {
+            PHIP(hipMemcpyAsync(d_roots, roots, n * 4, hipMemcpyHostToDevice, stream));
+            PHIP(hipMemcpyAsync(d_targets, targets, n * 4, hipMemcpyHostToDevice, stream));
+        }
+        PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
+        PHIP(hipMemsetAsync(P.overflow, 0, 4 * sizeof(unsigned int), stream));
+        PHIP(hipMemsetAsync(P.allowed, 0, W * 8, stream));
+        lb = cnt = edges = 0;
+        cur = 0;
+        hipLaunchKernelGGL(part_seed_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P);
+        PHIP(hipGetLastError());
+        stats.rounds++;
+    }
+
+    // bucket obuf by destination into send; returns KETOGPU_ENOMEM on overflow
+    int pack(ketogpu_record *send, uint64_t capacity, uint64_t *counts) {
+        read_ctr();
+        const uint64_t n = h[3];
+        if (overflow_bits() || n > capacity) {
+            for (uint32_t g = 0; g < world; g++) counts[g] = 0;
+            return KETOGPU_ENOMEM;
+        }
+        PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
+        if (n) {
+            unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
+            hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
+            PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+            PHIP(hipStreamSynchronize(stream));
+            unsigned long long off = 0;
+            for (uint32_t g = 0; g < world; g++) {
+                counts[g] = h[16 + g];
+                h[16 + kMaxWorld + g] = off;
+                off += h[16 + g];
+            }
+            PHIP(hipMemcpyAsync(d_cursor, h + 16 + kMaxWorld, world * sizeof(unsigned long long),
+                                hipMemcpyHostToDevice, stream));
+            hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_cursor, send);
+            PHIP(hipGetLastError());
+        } else {
+            for (uint32_t g = 0; g < world; g++) counts[g] = 0;
+        }
+        PHIP(hipMemsetAsync(&P.ctr[3], 0, sizeof(unsigned long long), stream));
+        PHIP(hipStreamSynchronize(stream));
+        stats.records_sent += n;
+        return KETOGPU_OK;
+    }
+
+    int apply(const ketogpu_record *recv, uint64_t n, uint64_t *frontier) {
+        const int nxt = cur ^ 1;
+        PHIP(hipMemsetAsync(&P.ctr[nxt], 0, sizeof(unsigned long long), stream));
+        const uint64_t base = lb + cnt;
+        if (n)
+            hipLaunchKernelGGL(part_apply_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n, base,
+                               &P.ctr[nxt]);
+        read_ctr();
+        stats.records_received += n;
+        if (overflow_bits()) {
+            *frontier = 0;
+            return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_ENOMEM;
+        }
+        const uint64_t ncnt = h[nxt] >> kCntShift, nedges = h[nxt] & kPreMask;
+        if (ncnt)
+            hipLaunchKernelGGL(part_gather_kernel, dim3(pblocks(ncnt)), dim3(kPB), 0, stream, P, base, base + ncnt);
+        lb = base;
+        cnt = ncnt;
+        edges = nedges;
+        cur = nxt;
+        *frontier = ncnt;
+        stats.levels++;
+        stats.frontier_entries += ncnt;
+        PHIP(hipStreamSynchronize(stream));
+        return KETOGPU_OK;
+    }
+
+    void expand() {
+        if (cnt && edges) {
+            uint64_t tiles = (edges + kPTile - 1) / kPTile;
+            unsigned grid = (unsigned)std::min<uint64_t>(tiles, 256ull * 16);
+            hipLaunchKernelGGL(part_expand_kernel, dim3(grid), dim3(kPB), 0, stream, P, lb, cnt, edges);
+            PHIP(hipGetLastError());
+            stats.forward_edges += edges;
+        }
+        PHIP(hipStreamSynchronize(stream));
+    }
+
+    void pull_emit() {
+        hipLaunchKernelGGL(part_pull_emit_kernel, dim3(pblocks(P.n)), dim3(kPB), 0, stream, P);
+        PHIP(hipGetLastError());
+    }
+
+    int pull_answer(const ketogpu_record *recv, uint64_t n) {
+        if (n) hipLaunchKernelGGL(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n);
+        read_ctr();
+        stats.queries_answered += n;
+        return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_OK;
+    }
+
+    // clear the round's state: sparse (recorded entries) unless bits may be unrecorded
+    void reset(bool dense) {
+        read_ctr();
+        if (dense || overflow_bits()) {
+            const size_t state = (size_t)W * std::max<uint32_t>(P.Nil, 1);
+            PHIP(hipMemsetAsync(P.vis, 0, state * 8, stream));
+            PHIP(hipMemsetAsync(P.nxt, 0, state * 8, stream));
+        } else {
+            const uint64_t ents = lb + cnt, ntouch = h[2];
+            if (ents)
+                hipLaunchKernelGGL(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key,
+                                   ents);
+            if (ntouch)
+                hipLaunchKernelGGL(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
+                                   ntouch);
+        }
+        PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
+        PHIP(hipMemsetAsync(P.overflow, 0, 4 * sizeof(unsigned int), stream));
+        PHIP(hipStreamSynchronize(stream));
+        lb = cnt = edges = 0;
+        dirty = false;
+    }
+
+    void end(uint64_t *bits) {
+        const uint64_t words = (P.n + 63) / 64;
+        if (words && bits) PHIP(hipMemcpyAsync(bits, P.allowed, words * 8, hipMemcpyDeviceToHost, stream));
+        PHIP(hipStreamSynchronize(stream));
+        reset(false);
+    }
+};
+
+// ------------------------------------------------------------------- C ABI
+#define PAPI_BEGIN try {
+#define PAPI_END                                                                                       \
+    }                                                                                                  \
+    catch (const Error &e) {                                                                           \
+        set_last_error(e.what());                                                                      \
+        return e.code;                                                                                 \
+    }                                                                                                  \
+    catch (const std::bad_alloc &) {                                                                   \
+        set_last_error("out of host memory");                                                          \
+        return KETOGPU_ENOMEM;                                                                         \
+    }                                                                                                  \
+    return KETOGPU_OK;
+
+extern "C" {
+
+uint32_t ketogpu_part_owner(uint32_t node, int32_t world) { return world > 0 ? part_owner(node, (uint32_t)world) : 0; }
+
+int ketogpu_part_new(const ketogpu_snapshot *s, const ketogpu_part_opts *opts, ketogpu_part **out) {
+    PAPI_BEGIN
+    if (!s || !opts || !out) throw Error(KETOGPU_EINVAL, "null argument");
+    *out = nullptr;
+    auto p = std::make_unique<ketogpu_part>();
+    p->init(*reinterpret_cast<const Snapshot *>(s), *opts);
+    *out = p.release();
+    PAPI_END
+}
+
+void ketogpu_part_free(ketogpu_part *p) { delete p; }
+
+uint64_t ketogpu_part_round_words(const ketogpu_part *p) { return p ? p->W : 0; }
+
+int ketogpu_part_begin(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n) {
+    PAPI_BEGIN
+    if (!p || (n && (!roots || !targets))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->begin(roots, targets, n);
+    PAPI_END
+}
+
+int ketogpu_part_emit(ketogpu_part *p, ketogpu_record *send, uint64_t capacity, uint64_t *counts) {
+    PAPI_BEGIN
+    if (!p || !counts || (capacity && !send)) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    int rc = p->pack(send, capacity, counts);
+    if (rc) {
+        set_last_error("partition: outgoing records exceed the buffers; retry with fewer words per round");
+        return rc;
+    }
+    PAPI_END
+}
+
+int ketogpu_part_apply(ketogpu_part *p, const ketogpu_record *recv, uint64_t n, uint64_t *frontier) {
+    PAPI_BEGIN
+    if (!p || !frontier || (n && !recv)) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    int rc = p->apply(recv, n, frontier);
+    if (rc) {
+        set_last_error(rc == KETOGPU_EINVAL ? "partition: received a record for a node this rank does not own"
+                                            : "partition: frontier lists overflow; retry with fewer words per round");
+        return rc;
+    }
+    PAPI_END
+}
+
+int ketogpu_part_expand(ketogpu_part *p) {
+    PAPI_BEGIN
+    if (!p) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->expand();
+    PAPI_END
+}
+
+int ketogpu_part_pull_emit(ketogpu_part *p, ketogpu_record *send, uint64_t capacity, uint64_t *counts) {
+    PAPI_BEGIN
+    if (!p || !counts || (capacity && !send)) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->pull_emit();
+    int rc = p->pack(send, capacity, counts);
+    if (rc) {
+        set_last_error("partition: pull queries exceed the buffers; retry with fewer words per round");
+        return rc;
+    }
+    PAPI_END
+}
+
+int ketogpu_part_pull_answer(ketogpu_part *p, const ketogpu_record *recv, uint64_t n) {
+    PAPI_BEGIN
+    if (!p || (n && !recv)) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    if (p->pull_answer(recv, n)) throw Error(KETOGPU_EINVAL, "partition: query for a node this rank does not own");
+    PAPI_END
+}
+
+int ketogpu_part_end(ketogpu_part *p, uint64_t *allowed_bits) {
+    PAPI_BEGIN
+    if (!p) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->end(allowed_bits);
+    PAPI_END
+}
+
+int ketogpu_part_abort(ketogpu_part *p) {
+    PAPI_BEGIN
+    if (!p) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->reset(true);
+    PAPI_END
+}
+
+int ketogpu_part_stats_get(const ketogpu_part *p, ketogpu_part_stats *out) {
+    if (!p || !out) {
+        set_last_error("null argument");
+        return KETOGPU_EINVAL;
+    }
+    *out = p->stats;
+    return KETOGPU_OK;
+}
+
+}  // extern "C"
