@@ -903,16 +903,17 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // cutoff, R2).  Used when the snapshot has no ambiguous keys (R4 flags are raised by
 // forward rows) and record begins fit u32; dynamic roots and table/list overflow spill
 // to the v2 cascade.
-constexpr int kBFront = 384;
-
-template <int U>
+// HLOG: log2 of the LDS table slots; F: pending/expansion list capacity
+template <int U, int HLOG, int F>
 struct BidiShared {
-    uint32_t key[kHash];
-    unsigned long long st[kHash];
-    uint16_t p_sd[2][kBFront];  // pending lists (ping-pong): slot | dir << 15
-    uint32_t p_begin[2][kBFront], p_deg[2][kBFront];
-    uint16_t e_sd[kBFront], e_mask[kBFront];  // this level's expansion list
-    uint32_t e_begin[kBFront], e_deg[kBFront];
+    static constexpr int H = 1 << HLOG;
+    static constexpr int HMAX = H * 3 / 4;
+    uint32_t key[H];
+    unsigned long long st[H];
+    uint16_t p_sd[2][F];  // pending lists (ping-pong): slot | dir << 15
+    uint32_t p_begin[2][F], p_deg[2][F];
+    uint16_t e_sd[F], e_mask[F];  // this level's expansion list
+    uint32_t e_begin[F], e_deg[F];
     uint32_t c_pre[kBlock + 1];
     uint32_t wave_sum[kBlock / 64];
     uint32_t cost[2][U];
@@ -959,14 +960,15 @@ __device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
     return base + lanes_below(bal);
 }
 
-template <int U>
-__device__ __forceinline__ void bidi_push(BidiShared<U> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
+template <int U, int HLOG, int F>
+__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
                                           uint32_t m, int d, int nxt) {
     int h = -1;
     bool inserted = false;
     if (want) {
-        uint32_t hh = hslot(u);
-        for (int p = 0; p < kHash; p++, hh = (hh + 1) & (kHash - 1)) {
+        constexpr int H = BidiShared<U, HLOG, F>::H;
+        uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
+        for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
             uint32_t kv = S.key[hh];
             if (kv == kEmpty) {
                 uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
@@ -988,7 +990,7 @@ __device__ __forceinline__ void bidi_push(BidiShared<U> &S, bool want, uint32_t 
     uint64_t bal = __ballot(inserted);
     if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
         uint32_t c = (uint32_t)__popcll(bal);
-        if (atomicAdd(&S.n_used, c) + c > (uint32_t)kHashMax) S.spill = 1;
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)BidiShared<U, HLOG, F>::HMAX) S.spill = 1;
     }
     bool app = false;
     if (h >= 0) {
@@ -1007,7 +1009,7 @@ __device__ __forceinline__ void bidi_push(BidiShared<U> &S, bool want, uint32_t 
     }
     uint32_t idx = lds_append(app, &S.n_p[nxt]);
     if (app) {
-        if (idx < (uint32_t)kBFront) {
+        if (idx < (uint32_t)F) {
             S.p_sd[nxt][idx] = (uint16_t)(h | (d << 15));
             S.p_begin[nxt][idx] = begin;
             S.p_deg[nxt][idx] = deg;
@@ -1018,9 +1020,9 @@ __device__ __forceinline__ void bidi_push(BidiShared<U> &S, bool want, uint32_t 
 }
 
 // expand expansion-list entries [base, base + k); block-uniform loop count
-template <int U>
+template <int U, int HLOG, int F>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
-                                            BidiShared<U> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
+                                            BidiShared<U, HLOG, F> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
     uint32_t dg = (uint32_t)threadIdx.x < k ? S.e_deg[base + threadIdx.x] : 0;
     uint32_t total = block_scan_sh(dg, S);
     for (uint32_t eb = 0; eb < total; eb += kBlock) {
@@ -1054,25 +1056,25 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
             }
             want = m != 0;
         }
-        bidi_push<U>(S, want, u, deg, bg, m, d, nxt);
+        bidi_push<U, HLOG, F>(S, want, u, deg, bg, m, d, nxt);
     }
 }
 
-template <int U>
+template <int U, int HLOG, int F>
 __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                       const uint32_t *roots, const uint32_t *targets, uint64_t n,
                                                       uint64_t *allowed, uint32_t *spill_out,
                                                       unsigned int *spill_count, unsigned long long *stats,
                                                       unsigned long long *stamps) {
     static_assert(U <= 16, "16 request bits per direction");
-    __shared__ BidiShared<U> S;
+    __shared__ BidiShared<U, HLOG, F> S;
     const int tid = threadIdx.x;
     unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t unit = blockIdx.x;
     const uint64_t c0 = unit * U;
     const int shift = (int)(c0 & 63);
-    for (int i = tid; i < kHash; i += kBlock) {
+    for (int i = tid; i < BidiShared<U, HLOG, F>::H; i += kBlock) {
         S.key[i] = kEmpty;
         S.st[i] = 0;
     }
@@ -1125,11 +1127,11 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
     // reached backward from rev(t), where it is compared directly)
     if (tid < 64) {
         bool v = tid < U && ((S.active >> tid) & 1u) && S.root[tid] < g.Ni;
-        bidi_push<U>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
+        bidi_push<U, HLOG, F>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
     }
     __syncthreads();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
-    bidi_expand<U>(g, frec, brec, S, 0, 2 * U, 0, edges);
+    bidi_expand<U, HLOG, F>(g, frec, brec, S, 0, 2 * U, 0, edges);
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
     for (;;) {
@@ -1183,13 +1185,13 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
             }
             uint32_t ei = lds_append(take != 0, &S.n_e);
             uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
-            if (take) {  // ei < cnt <= kBFront
+            if (take) {  // ei < cnt <= F
                 S.e_sd[ei] = (uint16_t)sd;
                 S.e_mask[ei] = (uint16_t)take;
                 S.e_begin[ei] = S.p_begin[cur][i];
                 S.e_deg[ei] = S.p_deg[cur][i];
             }
-            if (rest) {  // pi < cnt <= kBFront
+            if (rest) {  // pi < cnt <= F
                 S.p_sd[nxt][pi] = (uint16_t)sd;
                 S.p_begin[nxt][pi] = S.p_begin[cur][i];
                 S.p_deg[nxt][pi] = S.p_deg[cur][i];
@@ -1199,7 +1201,7 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
         const uint32_t ne = S.n_e;
         for (uint32_t base = 0; base < ne; base += kBlock) {
             uint32_t k = ne - base < (uint32_t)kBlock ? ne - base : (uint32_t)kBlock;
-            bidi_expand<U>(g, frec, brec, S, base, k, nxt, edges);
+            bidi_expand<U, HLOG, F>(g, frec, brec, S, base, k, nxt, edges);
             __syncthreads();
         }
         cur = nxt;
@@ -1589,6 +1591,7 @@ struct ketogpu_engine {
     int wave_u = 8;
     bool use_v2 = true;
     bool use_bidi = true;
+    int bidi_hlog = 10;  // KETOGPU_BIDI_HLOG: LDS table of the bidi pass (9, 10 or 11)
     const FRec *frec = nullptr;  // v2 edge records (parallel to fint_col)
     const FRec *brec = nullptr;  // v3 reverse records (parallel to rev_col)
     unsigned long long *stamps = nullptr;  // KETOGPU_STAMPS=1 diagnostic build
@@ -1671,6 +1674,7 @@ struct ketogpu_engine {
         // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_bidi = p == "bidi" && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
+        if (const char *hl = getenv("KETOGPU_BIDI_HLOG")) bidi_hlog = atoi(hl);
         if (getenv("KETOGPU_STAMPS")) {
             stamps = dalloc<unsigned long long>((size_t)65536 * 8);
             owned.push_back(stamps);
@@ -1853,9 +1857,15 @@ struct ketogpu_engine {
                 HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
                 hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
-                if (sg.kind == 0)
-                    hipLaunchKernelGGL(bidi_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec, brec,
-                                       q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
+                if (sg.kind == 0 && bidi_hlog == 11)
+                    hipLaunchKernelGGL((bidi_kernel<16, 11, 384>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
+                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
+                else if (sg.kind == 0 && bidi_hlog == 9)
+                    hipLaunchKernelGGL((bidi_kernel<16, 9, 192>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
+                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
+                else if (sg.kind == 0)
+                    hipLaunchKernelGGL((bidi_kernel<16, 10, 256>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
+                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
                 else if (sg.u == 16)
                     hipLaunchKernelGGL(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec,
                                        q.roots, q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count,

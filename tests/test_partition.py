@@ -108,7 +108,7 @@ def test_partition_device_single_rank(seed):
     st = eng.local.stats()
     assert st["rounds"] >= 6 and st["levels"] > 0 and st["records_sent"] > 0
     # tiny buffers: rounds overflow and are retried with fewer words, same answers
-    small = PartitionedEngine(snap, device=0, record_capacity=512, max_words_per_round=8)
+    small = PartitionedEngine(snap, device=0, record_capacity=2048, max_words_per_round=8)
     np.testing.assert_array_equal(small.check_ids(roots, targets), want)
     assert small.retries > 0
 

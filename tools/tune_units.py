@@ -1,5 +1,5 @@
 """A/B the LDS unit plans on config #2 in ONE process (same graph, same requests):
-KETOGPU_UNITS = w4 | w8 | w16 | b16, plus the global path.  Prints ms per 1M-request
+KETOGPU_UNITS = bidi[:hlog] | v2 | w4 | w8 | w16 | b16, plus the global path.  Prints ms per 1M-request
 run (median of interleaved rounds) and checks every plan returns identical bits."""
 import os
 import sys
@@ -23,9 +23,11 @@ engines, queries = {}, {}
 for p in plans:
     if p == "global":
         os.environ["KETOGPU_PATH"] = "global"
-    else:
+    else:  # plan[:hlog], e.g. bidi:10
         os.environ.pop("KETOGPU_PATH", None)
-        os.environ["KETOGPU_UNITS"] = p
+        os.environ["KETOGPU_UNITS"] = p.split(":")[0]
+        if ":" in p:
+            os.environ["KETOGPU_BIDI_HLOG"] = p.split(":")[1]
     engines[p] = check.Engine(snap, state_budget_bytes=16 << 30)
     queries[p] = engines[p].upload(roots, targets)
 ref = None
