@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU work of the baseline sample")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
+    p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
+                   help="replicated: graph on every GPU, request batches sharded (the metric's line); "
+                        "partitioned: hash-partitioned graph, per-level all-to-all (config #5 path)")
     return p.parse_args()
 
 
@@ -90,6 +93,8 @@ def cpu_model():
 def main():
     a = parse()
     rank, world, local = dist_init(a.gpus)
+    if a.mode == "partitioned":
+        return main_partitioned(a, rank, world, local)
     from keto_amd import check, synth
     from keto_amd.snapshot import Snapshot
 
@@ -180,6 +185,54 @@ def main():
             "pcie_inclusive_checks_per_s": round(n / t_host, 1),
             "snapshot": {k: v for k, v in snap.stats().items() if k.startswith("num_")},
         }
+        print(json.dumps(out), flush=True)
+    barrier(world)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def main_partitioned(a, rank, world, local):
+    """Config #5's path on config #2's graph: the snapshot is hash-partitioned over the
+    ranks (keto_amd/partition.py, partition.hip) and every level exchanges records with
+    all_to_all over RCCL.  Every rank holds the same global batch of 1M * world requests
+    (weak scaling); value = that batch / the slowest rank's time."""
+    from keto_amd import check, synth
+    from keto_amd.partition import PartitionedEngine
+    from keto_amd.snapshot import Snapshot
+    scale = 100 if a.small else 1
+    n_req = (1_000_000 // (10 if a.small else 1)) * world
+    sizes = dict(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
+                 tuples=50_000_000 // scale, checks=n_req)
+    w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    roots, targets = w.resolve(snap)
+    eng = PartitionedEngine(snap, device=local, record_capacity=1 << 26)
+    for _ in range(a.warmup):
+        got = eng.check_ids(roots, targets)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        got = eng.check_ids(roots, targets)
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    st = eng.local.stats()
+    out = None
+    if rank == 0:
+        # parity: the single-GPU engine on this rank's GPU holds the whole graph here
+        ref = check.Engine(snap, device=local).check_ids(roots, targets)
+        out = {"metric": METRIC, "value": round(n_req * a.steps / dt, 1), "unit": "checks/s", "n_gpus": world,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "u32 ids / u64 bitmasks (integer)",
+               "data": "synthetic: config #2 RBAC generator, seed 0x4B45544F; graph hash-partitioned",
+               "config": {"workload": "config2_rbac_partitioned" + ("_small" if a.small else ""), **sizes,
+                          "mode": "hash-partitioned graph, per-level all-to-all", "parallelism": f"partition x{world}"},
+               "roofline": None, "cpu_baseline": None,
+               "parity": {"sample": int(n_req), "mismatches": int((got != ref).sum()),
+                          "against": "single-GPU engine"},
+               "partition": {k: int(v) for k, v in st.items()},
+               "exchange": {"records": int(eng.records), "levels": int(eng.levels), "retries": int(eng.retries)}}
         print(json.dumps(out), flush=True)
     barrier(world)
     if world > 1:

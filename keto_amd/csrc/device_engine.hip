@@ -409,6 +409,8 @@ __device__ __forceinline__ int unit_lookup(const UnitShared &S, uint32_t v) {
 // tens of thousands of workgroups adding to ONE address serialize at the memory side
 // (~12 ns per atomic) and that alone cost ~2 ms per 1M requests.
 constexpr int kStatSlots = 1024;
+// statistics buffer: [8 misc][2 regions x 4 * kStatSlots][8 reduced][spill counters]
+constexpr int kStatsLen = 8 + 8 * kStatSlots + 8 + 4;
 __device__ __forceinline__ unsigned long long *stat_slot(unsigned long long *stats) {
     return stats + 8 + (size_t)(blockIdx.x & (kStatSlots - 1)) * 4;
 }
@@ -903,19 +905,21 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // cutoff, R2).  Used when the snapshot has no ambiguous keys (R4 flags are raised by
 // forward rows) and record begins fit u32; dynamic roots and table/list overflow spill
 // to the v2 cascade.
-// HLOG: log2 of the LDS table slots; F: pending/expansion list capacity
-template <int U, int HLOG, int F>
+// HLOG: log2 of the LDS table slots; F: pending/expansion list capacity; BT: threads per
+// unit (256 = four waves, 64 = one wave: more units per CU, barriers of one wave); LF:
+// maximum table load in eighths (a unit spills beyond it)
+template <int U, int HLOG, int F, int BT, int LF = 6>
 struct BidiShared {
     static constexpr int H = 1 << HLOG;
-    static constexpr int HMAX = H * 3 / 4;
+    static constexpr int HMAX = H * LF / 8;
     uint32_t key[H];
     unsigned long long st[H];
     uint16_t p_sd[2][F];  // pending lists (ping-pong): slot | dir << 15
     uint32_t p_begin[2][F], p_deg[2][F];
     uint16_t e_sd[F], e_mask[F];  // this level's expansion list
     uint32_t e_begin[F], e_deg[F];
-    uint32_t c_pre[kBlock + 1];
-    uint32_t wave_sum[kBlock / 64];
+    uint32_t c_pre[BT + 1];
+    uint32_t wave_sum[BT / 64];
     uint32_t cost[2][U];
     uint32_t root[U];
     uint32_t sel[2];
@@ -923,8 +927,8 @@ struct BidiShared {
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
 };
 
-// exclusive block scan of one u32 per thread into S.c_pre; returns the total
-template <class SH>
+// exclusive block scan of one u32 per thread (BT threads) into S.c_pre; returns the total
+template <int BT, class SH>
 __device__ __forceinline__ uint32_t block_scan_sh(uint32_t v, SH &S) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     uint32_t x = v;
@@ -937,13 +941,13 @@ __device__ __forceinline__ uint32_t block_scan_sh(uint32_t v, SH &S) {
     __syncthreads();
     uint32_t base = 0, total = 0;
 #pragma unroll
-    for (int i = 0; i < kBlock / 64; i++) {
+    for (int i = 0; i < BT / 64; i++) {
         uint32_t s = S.wave_sum[i];
         base += i < wv ? s : 0;
         total += s;
     }
     S.c_pre[tid] = base + x - v;
-    if (tid == 0) S.c_pre[kBlock] = total;
+    if (tid == 0) S.c_pre[BT] = total;
     __syncthreads();
     return total;
 }
@@ -960,13 +964,13 @@ __device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
     return base + lanes_below(bal);
 }
 
-template <int U, int HLOG, int F>
-__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
+template <int U, int HLOG, int F, int BT, int LF>
+__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
                                           uint32_t m, int d, int nxt) {
     int h = -1;
     bool inserted = false;
     if (want) {
-        constexpr int H = BidiShared<U, HLOG, F>::H;
+        constexpr int H = BidiShared<U, HLOG, F, BT, LF>::H;
         uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
         for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
             uint32_t kv = S.key[hh];
@@ -990,7 +994,7 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F> &S, bool want, 
     uint64_t bal = __ballot(inserted);
     if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
         uint32_t c = (uint32_t)__popcll(bal);
-        if (atomicAdd(&S.n_used, c) + c > (uint32_t)BidiShared<U, HLOG, F>::HMAX) S.spill = 1;
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)BidiShared<U, HLOG, F, BT, LF>::HMAX) S.spill = 1;
     }
     bool app = false;
     if (h >= 0) {
@@ -1020,12 +1024,12 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F> &S, bool want, 
 }
 
 // expand expansion-list entries [base, base + k); block-uniform loop count
-template <int U, int HLOG, int F>
+template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
-                                            BidiShared<U, HLOG, F> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
+                                            BidiShared<U, HLOG, F, BT, LF> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
     uint32_t dg = (uint32_t)threadIdx.x < k ? S.e_deg[base + threadIdx.x] : 0;
-    uint32_t total = block_scan_sh(dg, S);
-    for (uint32_t eb = 0; eb < total; eb += kBlock) {
+    uint32_t total = block_scan_sh<BT>(dg, S);
+    for (uint32_t eb = 0; eb < total; eb += BT) {
         uint32_t e = eb + threadIdx.x;
         bool want = e < total;
         uint32_t u = 0, deg = 0, bg = 0, m = 0;
@@ -1056,25 +1060,23 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
             }
             want = m != 0;
         }
-        bidi_push<U, HLOG, F>(S, want, u, deg, bg, m, d, nxt);
+        bidi_push<U, HLOG, F, BT, LF>(S, want, u, deg, bg, m, d, nxt);
     }
 }
 
-template <int U, int HLOG, int F>
-__global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
-                                                      const uint32_t *roots, const uint32_t *targets, uint64_t n,
-                                                      uint64_t *allowed, uint32_t *spill_out,
-                                                      unsigned int *spill_count, unsigned long long *stats,
-                                                      unsigned long long *stamps) {
+// one unit (requests [U*unit, U*unit + U)) by the whole workgroup
+template <int U, int HLOG, int F, int BT, int LF>
+__device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, const DevGraph &g, const FRec *frec,
+                                          const FRec *brec, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                                          uint64_t *allowed, const uint64_t unit, uint32_t *spill_out,
+                                          unsigned int *spill_count, unsigned long long *stats,
+                                          unsigned long long *stamp) {
     static_assert(U <= 16, "16 request bits per direction");
-    __shared__ BidiShared<U, HLOG, F> S;
     const int tid = threadIdx.x;
-    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
-    const uint64_t unit = blockIdx.x;
     const uint64_t c0 = unit * U;
     const int shift = (int)(c0 & 63);
-    for (int i = tid; i < BidiShared<U, HLOG, F>::H; i += kBlock) {
+    for (int i = tid; i < BidiShared<U, HLOG, F, BT, LF>::H; i += BT) {
         S.key[i] = kEmpty;
         S.st[i] = 0;
     }
@@ -1127,11 +1129,11 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
     // reached backward from rev(t), where it is compared directly)
     if (tid < 64) {
         bool v = tid < U && ((S.active >> tid) & 1u) && S.root[tid] < g.Ni;
-        bidi_push<U, HLOG, F>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
+        bidi_push<U, HLOG, F, BT, LF>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
     }
     __syncthreads();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
-    bidi_expand<U, HLOG, F>(g, frec, brec, S, 0, 2 * U, 0, edges);
+    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, 0, 2 * U, 0, edges);
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
     for (;;) {
@@ -1141,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
         if (S.spill || !cnt || !act) break;
         n_levels++;
         // per-request pending degree sums per direction
-        for (uint32_t base = 0; base < cnt; base += kBlock) {
+        for (uint32_t base = 0; base < cnt; base += BT) {
             uint32_t i = base + tid;
             if (i < cnt) {
                 uint32_t sd = S.p_sd[cur][i], d = sd >> 15;
@@ -1171,7 +1173,7 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
         // split: the chosen direction's bits go to this level's expansion list, open
         // requests' other bits stay pending (carried to the next list)
         const uint32_t act2 = S.active;
-        for (uint32_t base = 0; base < cnt; base += kBlock) {
+        for (uint32_t base = 0; base < cnt; base += BT) {
             uint32_t i = base + tid;
             uint32_t take = 0, rest = 0, sd = 0;
             if (i < cnt) {
@@ -1199,9 +1201,9 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
         }
         __syncthreads();
         const uint32_t ne = S.n_e;
-        for (uint32_t base = 0; base < ne; base += kBlock) {
-            uint32_t k = ne - base < (uint32_t)kBlock ? ne - base : (uint32_t)kBlock;
-            bidi_expand<U, HLOG, F>(g, frec, brec, S, base, k, nxt, edges);
+        for (uint32_t base = 0; base < ne; base += BT) {
+            uint32_t k = ne - base < (uint32_t)BT ? ne - base : (uint32_t)BT;
+            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, base, k, nxt, edges);
             __syncthreads();
         }
         cur = nxt;
@@ -1225,6 +1227,69 @@ __global__ __launch_bounds__(kBlock) void bidi_kernel(DevGraph g, const FRec *fr
         if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << shift);
         atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
         atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
+    }
+}
+
+// Stage kernel.  in_count == nullptr: workgroup b runs unit parents ? parents[b] : b.
+// Otherwise persistent: the workgroups stride over the *in_count units listed in
+// parents (the previous stage's spills), so the stage is launched without the host
+// reading that count first.
+template <int U, int HLOG, int F, int BT, int LF>
+__global__ __launch_bounds__(BT) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+                                                  const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                                                  uint64_t *allowed, const uint32_t *parents,
+                                                  const unsigned int *in_count, uint32_t *spill_out,
+                                                  unsigned int *spill_count, unsigned long long *stats,
+                                                  unsigned long long *stamps) {
+    __shared__ BidiShared<U, HLOG, F, BT, LF> S;
+    if (!in_count) {
+        unsigned long long *stamp =
+            (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed,
+                                      parents ? parents[blockIdx.x] : blockIdx.x, spill_out, spill_count, stats, stamp);
+        return;
+    }
+    const unsigned cnt = *in_count;
+    for (unsigned b = blockIdx.x; b < cnt; b += gridDim.x) {
+        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed, parents[b], spill_out, spill_count,
+                                      stats, nullptr);
+        __syncthreads();
+    }
+}
+
+// zero the per-run outputs and counters in one launch
+__global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t *a, uint64_t na, uint64_t *b, uint64_t nb,
+                                                       unsigned long long *c, uint64_t nc) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < na + nb + nc; i += (uint64_t)gridDim.x * kBlock) {
+        if (i < na)
+            a[i] = 0;
+        else if (i < na + nb)
+            b[i - na] = 0;
+        else
+            c[i - na - nb] = 0;
+    }
+}
+
+// sum the spread statistics slots of `regions` regions into out[3 * region + k]
+__global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned long long *slots, int regions,
+                                                              unsigned long long *out) {
+    __shared__ unsigned long long part[kBlock / 64][3];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int r = 0; r < regions; r++) {
+        unsigned long long v[3] = {0, 0, 0};
+        for (int i = threadIdx.x; i < kStatSlots; i += kBlock)
+            for (int k = 0; k < 3; k++) v[k] += slots[(size_t)r * 4 * kStatSlots + (size_t)i * 4 + k];
+        for (int k = 0; k < 3; k++) {
+            for (int d = 32; d; d >>= 1) v[k] += __shfl_down(v[k], d, 64);
+            if (lane == 0) part[wv][k] = v[k];
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            unsigned long long t = 0;
+            for (int w = 0; w < kBlock / 64; w++) t += part[w][threadIdx.x];
+            out[3 * r + threadIdx.x] = t;
+        }
+        __syncthreads();
     }
 }
 
@@ -1514,6 +1579,13 @@ inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kB
             throw Error(KETOGPU_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e));              \
     } while (0)
 
+// every launch is checked: a failed launch must fail its call, not a later one
+#define KLAUNCH(...)                                 \
+    do {                                             \
+        hipLaunchKernelGGL(__VA_ARGS__);             \
+        HIP_CHECK(hipGetLastError());                \
+    } while (0)
+
 template <class T>
 T *dalloc(size_t n) {
     void *p = nullptr;
@@ -1591,7 +1663,34 @@ struct ketogpu_engine {
     int wave_u = 8;
     bool use_v2 = true;
     bool use_bidi = true;
-    int bidi_hlog = 10;  // KETOGPU_BIDI_HLOG: LDS table of the bidi pass (9, 10 or 11)
+    // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
+    // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run with kBidiWide
+    struct BidiCfg {
+        int hlog, bt, f, lf;
+        bool operator==(const BidiCfg &o) const { return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf; }
+    };
+    static constexpr BidiCfg kBidiWide{11, 256, 384, 6};
+    BidiCfg bidi_cfg{9, 64, 128, 7};
+
+    void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
+                     const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
+                     unsigned long long *stp) {
+#define KETO_BIDI(HL, F, BT, LF)                                                                                  \
+    if (c == BidiCfg{HL, BT, F, LF}) {                                                                           \
+        KLAUNCH((bidi_kernel<16, HL, F, BT, LF>), dim3(grid), dim3(BT), pad, stream, g, frec, brec,   \
+                           q.roots, q.targets, q.n, q.allowed, parents, in_count, out, out_count, stats, stp);   \
+        return;                                                                                                  \
+    }
+        KETO_BIDI(11, 384, 256, 6)
+        KETO_BIDI(10, 256, 256, 6)
+        KETO_BIDI(10, 256, 64, 6)
+        KETO_BIDI(9, 192, 64, 6)
+        KETO_BIDI(9, 128, 64, 6)
+        KETO_BIDI(9, 192, 64, 7)
+        KETO_BIDI(9, 128, 64, 7)
+#undef KETO_BIDI
+        throw Error(KETOGPU_EINVAL, "KETOGPU_BIDI: unsupported configuration");
+    }
     const FRec *frec = nullptr;  // v2 edge records (parallel to fint_col)
     const FRec *brec = nullptr;  // v3 reverse records (parallel to rev_col)
     unsigned long long *stamps = nullptr;  // KETOGPU_STAMPS=1 diagnostic build
@@ -1674,7 +1773,10 @@ struct ketogpu_engine {
         // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_bidi = p == "bidi" && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
-        if (const char *hl = getenv("KETOGPU_BIDI_HLOG")) bidi_hlog = atoi(hl);
+        if (const char *bc = getenv("KETOGPU_BIDI")) {  // "hlog,threads,lists,load", e.g. "9,64,192,6"
+            BidiCfg c = bidi_cfg;
+            if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_cfg = c;
+        }
         if (getenv("KETOGPU_STAMPS")) {
             stamps = dalloc<unsigned long long>((size_t)65536 * 8);
             owned.push_back(stamps);
@@ -1749,10 +1851,10 @@ struct ketogpu_engine {
         for (void *p : {(void *)st.fe_key, (void *)st.fe_mask, (void *)st.fe_pre, (void *)st.touch}) owned.push_back(p);
         st.ctr = dalloc<unsigned long long>(8);
         st.overflow = dalloc<unsigned int>(4);
-        st.stats = dalloc<unsigned long long>(8 + 4 * kStatSlots);
-        spill_count = dalloc<unsigned int>(4);
-        for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats, (void *)spill_count}) owned.push_back(p);
-        HIP_CHECK(hipHostMalloc((void **)&h_ctr, 16 * sizeof(uint64_t), hipHostMallocDefault));
+        st.stats = dalloc<unsigned long long>(kStatsLen);
+        spill_count = (unsigned int *)(st.stats + 8 + 8 * kStatSlots + 8);
+        for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats}) owned.push_back(p);  // spill_count lives in st.stats
+        HIP_CHECK(hipHostMalloc((void **)&h_ctr, 64 * sizeof(uint64_t), hipHostMallocDefault));
         HIP_CHECK(hipStreamSynchronize(stream));
     }
 
@@ -1772,14 +1874,14 @@ struct ketogpu_engine {
     }
 
     // sum the spread unit-statistics slots (rows, edges, reverse entries)
+    unsigned long long *stat_out() { return st.stats + 8 + 8 * kStatSlots; }
+
+    // sum the spread unit-statistics slots of both regions (rows, edges, reverse entries)
     void read_unit_stats(uint64_t out[3]) {
-        stat_host.resize(4 * kStatSlots);
-        HIP_CHECK(hipMemcpyAsync(stat_host.data(), st.stats + 8, 4 * kStatSlots * sizeof(uint64_t),
-                                 hipMemcpyDeviceToHost, stream));
+        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 32, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
-        out[0] = out[1] = out[2] = 0;
-        for (int i = 0; i < kStatSlots; i++)
-            for (int k = 0; k < 3; k++) out[k] += stat_host[(size_t)i * 4 + k];
+        for (int k = 0; k < 3; k++) out[k] = h_ctr[32 + k] + h_ctr[35 + k];
     }
 
     uint32_t read_spill_count() {
@@ -1803,13 +1905,13 @@ struct ketogpu_engine {
             hipEvent_t a = ev(), b = ev();
             HIP_CHECK(hipEventRecord(a, stream));
             if (wave_u == 4)
-                hipLaunchKernelGGL((wave_unit_kernel<4, 9>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                KLAUNCH((wave_unit_kernel<4, 9>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
                                    q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
             else if (wave_u == 8)
-                hipLaunchKernelGGL((wave_unit_kernel<8, 10>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
+                KLAUNCH((wave_unit_kernel<8, 10>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
                                    q.roots, q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
             else
-                hipLaunchKernelGGL((wave_unit_kernel<16, 11>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
+                KLAUNCH((wave_unit_kernel<16, 11>), dim3(grid), dim3(kBlock), 0, stream, g, has_kids,
                                    q.roots, q.targets, q.n, q.allowed, q.flags, list[0], spill_count, st.stats);
             HIP_CHECK(hipEventRecord(b, stream));
             unit_ev.push_back({a, b});
@@ -1821,7 +1923,7 @@ struct ketogpu_engine {
             a = ev();
             b = ev();
             HIP_CHECK(hipEventRecord(a, stream));
-            hipLaunchKernelGGL(unit_kernel<1>, dim3((unsigned)(left * wave_u)), dim3(kBlock), 0, stream, g, has_kids,
+            KLAUNCH(unit_kernel<1>, dim3((unsigned)(left * wave_u)), dim3(kBlock), 0, stream, g, has_kids,
                                q.roots, q.targets, q.n, q.allowed, q.flags, list[0], (uint32_t)wave_u, list[1],
                                spill_count, st.stats, nullptr);
             HIP_CHECK(hipEventRecord(b, stream));
@@ -1836,64 +1938,92 @@ struct ketogpu_engine {
         uint64_t units = (q.n + 15) / 16;
         uint64_t left = 0;
         if (use_v2) {
-            // stage 0 covers every 16-request unit; each later stage re-runs the previous
-            // stage's spilled units split `fan` ways: bidi<16> -> unit2<16> -> unit2<4> -> unit2<1>
+            // Stage list.  With bidi: bidi (configured shape) over every unit, then bidi with
+            // the wide table PERSISTENT over stage 0's spills (their count is read on the
+            // device), statistics of the two stages in separate regions, and one host
+            // synchronization for counts and statistics.  Whatever still spills (rare) runs
+            // the host-driven unit2 cascade: unit2<16> -> unit2<4> -> unit2<1> -> global path.
+            uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
+            if (use_bidi) {
+                const bool wide = !(bidi_cfg == kBidiWide);
+                hipEvent_t a = ev(), b = ev(), c = ev();
+                HIP_CHECK(hipEventRecord(a, stream));
+                launch_bidi(bidi_cfg, (unsigned)units, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
+                            st.stats, stamps);
+                HIP_CHECK(hipEventRecord(b, stream));
+                if (wide)
+                    launch_bidi(kBidiWide, (unsigned)std::min<uint64_t>(units, 1024), 0, q, list[0], &spill_count[0],
+                                list[1], &spill_count[1], st.stats + 4 * kStatSlots, nullptr);
+                HIP_CHECK(hipEventRecord(c, stream));
+                KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2,
+                                   stat_out());
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                                         stream));
+                HIP_CHECK(hipStreamSynchronize(stream));
+                unit_ev.push_back({a, b});
+                if (wide) unit_ev.push_back({b, c});
+                const uint64_t *t = (const uint64_t *)h_ctr + 16;
+                rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
+                const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
+                rs.spilled_units += cnt[0] + (wide ? cnt[1] : 0);
+                rs.push_launches += wide ? 2 : 1;
+                rs.unit_launches += wide ? 2 : 1;
+                left = wide ? cnt[1] : cnt[0];
+                from = wide ? list[1] : list[0];
+                if (!left) return 0;
+            }
             struct Stage {
-                int kind, u;
+                int u;
                 uint32_t fan;
             };
-            std::vector<Stage> stages;
-            if (use_bidi) stages.push_back({0, 16, 1});
-            stages.push_back({1, 16, 1});
-            stages.push_back({1, 4, 4});
-            stages.push_back({1, 1, 4});
-            for (size_t si = 0; si < stages.size(); si++) {
+            const Stage stages[3] = {{16, 1}, {4, 4}, {1, 4}};
+            uint32_t *in = from;
+            uint32_t *bufs[2] = {from == list[0] ? list[1] : list[0], from == list[0] ? list[0] : list[1]};
+            if (!from) bufs[0] = list[0], bufs[1] = list[1];
+            for (int si = 0; si < 3; si++) {
                 const Stage &sg = stages[si];
-                uint64_t grid = si == 0 ? units : left * sg.fan;
+                const bool first = !from && si == 0;  // unit2<16> over every unit (plan "v2")
+                uint64_t grid = first ? units : left * sg.fan;
                 if (!grid) return 0;
-                uint32_t *in = si == 0 ? nullptr : list[(si - 1) & 1], *out = list[si & 1];
-                unsigned long long *stp = si == 0 ? stamps : nullptr;
-                unsigned pad = si == 0 ? lds_pad : 0;
-                HIP_CHECK(hipMemsetAsync(spill_count, 0, sizeof(unsigned int), stream));
+                uint32_t *out = bufs[si & 1];
+                unsigned long long *stp = first ? stamps : nullptr;
+                unsigned pad = first ? lds_pad : 0;
+                HIP_CHECK(hipMemsetAsync(spill_count + 2, 0, sizeof(unsigned int), stream));
                 hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
-                if (sg.kind == 0 && bidi_hlog == 11)
-                    hipLaunchKernelGGL((bidi_kernel<16, 11, 384>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
-                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
-                else if (sg.kind == 0 && bidi_hlog == 9)
-                    hipLaunchKernelGGL((bidi_kernel<16, 9, 192>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
-                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
-                else if (sg.kind == 0)
-                    hipLaunchKernelGGL((bidi_kernel<16, 10, 256>), dim3((unsigned)grid), dim3(kBlock), pad, stream, g,
-                                       frec, brec, q.roots, q.targets, q.n, q.allowed, out, spill_count, st.stats, stp);
-                else if (sg.u == 16)
-                    hipLaunchKernelGGL(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec,
-                                       q.roots, q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count,
+                const uint32_t *par = first ? nullptr : in;
+                if (sg.u == 16)
+                    KLAUNCH(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec,
+                                       q.roots, q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
                                        st.stats, stp);
                 else if (sg.u == 4)
-                    hipLaunchKernelGGL(unit2_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count, st.stats,
-                                       nullptr);
+                    KLAUNCH(unit2_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
+                                       q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
+                                       st.stats, nullptr);
                 else
-                    hipLaunchKernelGGL(unit2_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, in, sg.fan, out, spill_count, st.stats,
-                                       nullptr);
+                    KLAUNCH(unit2_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
+                                       q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
+                                       st.stats, nullptr);
                 HIP_CHECK(hipEventRecord(b, stream));
                 unit_ev.push_back({a, b});
-                left = read_spill_count();
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 12, spill_count + 2, sizeof(unsigned int), hipMemcpyDeviceToHost,
+                                         stream));
+                HIP_CHECK(hipStreamSynchronize(stream));
+                left = (uint32_t)h_ctr[12];
                 rs.spilled_units += left;
                 rs.push_launches++;
                 rs.unit_launches++;
-                if (si == 0) {  // the dominant launch: keep its own byte count
+                if (first) {  // the dominant launch: keep its own byte count
                     uint64_t t3[3];
                     read_unit_stats(t3);
                     rs.main_bytes = 16 * t3[0] + 16 * t3[1] + 4 * t3[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
                 }
+                in = out;
             }
             // the global path reads the last stage's single requests from list[0]
-            uint32_t *last = list[(stages.size() - 1) & 1];
-            if (left && last != list[0])
-                HIP_CHECK(hipMemcpyAsync(list[0], last, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+            if (left && in != list[0])
+                HIP_CHECK(hipMemcpyAsync(list[0], in, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
             return left;
         }
         for (int pass = 0; pass < 3; pass++) {
@@ -1904,13 +2034,13 @@ struct ketogpu_engine {
             hipEvent_t a = ev(), b = ev();
             HIP_CHECK(hipEventRecord(a, stream));
             if (pass == 0)
-                hipLaunchKernelGGL(unit_kernel<16>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                KLAUNCH(unit_kernel<16>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
                                    q.targets, q.n, q.allowed, q.flags, nullptr, 1u, out, spill_count, st.stats, stamps);
             else if (pass == 1)
-                hipLaunchKernelGGL(unit_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                KLAUNCH(unit_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
                                    q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
             else
-                hipLaunchKernelGGL(unit_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
+                KLAUNCH(unit_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, has_kids, q.roots,
                                    q.targets, q.n, q.allowed, q.flags, in, 4u, out, spill_count, st.stats, nullptr);
             HIP_CHECK(hipEventRecord(b, stream));
             unit_ev.push_back({a, b});
@@ -1941,7 +2071,7 @@ struct ketogpu_engine {
         HIP_CHECK(hipMemsetAsync(st.ctr, 0, 3 * sizeof(uint64_t), stream));
         HIP_CHECK(hipMemsetAsync(st.overflow, 0, sizeof(unsigned int), stream));
         *(uint64_t *)&h_ctr[3] = 0;
-        hipLaunchKernelGGL(seed_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
+        KLAUNCH(seed_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
                            q.flags);
         read_counters();
         uint64_t cnt = h_ctr[0] >> kCntShift, edges = h_ctr[0] & kPreMask;
@@ -1949,13 +2079,13 @@ struct ketogpu_engine {
         uint64_t lb = 0;
         int cur = 0;  // ctr index of the current level
         if (q.has_dyn) {
-            hipLaunchKernelGGL(seed_dynamic_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots,
+            KLAUNCH(seed_dynamic_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots,
                                q.targets, c0, n, q.dyn_int_off, q.dyn_int, q.dyn_amb, q.flags, lb + cnt, &st.ctr[1]);
         }
         bool overflow = (uint32_t)h_ctr[3] != 0;
         for (uint64_t level = 0; !overflow; level++) {
             if (level > 0 && cnt)
-                hipLaunchKernelGGL(gather_kernel, dim3(blocks_for(cnt)), dim3(kBlock), 0, stream, g, st, lb, lb + cnt);
+                KLAUNCH(gather_kernel, dim3(blocks_for(cnt)), dim3(kBlock), 0, stream, g, st, lb, lb + cnt);
             bool dyn_pending = level == 0 && q.has_dyn;
             if (!cnt && !dyn_pending) break;
             int nxt = cur ^ 1;
@@ -1965,7 +2095,7 @@ struct ketogpu_engine {
                 unsigned grid = (unsigned)std::min<uint64_t>(tiles, 256ull * 16);
                 hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
-                hipLaunchKernelGGL(expand_kernel, dim3(grid), dim3(kBlock), 0, stream, g, st, lb, cnt, edges, lb + cnt,
+                KLAUNCH(expand_kernel, dim3(grid), dim3(kBlock), 0, stream, g, st, lb, cnt, edges, lb + cnt,
                                    &st.ctr[nxt], q.flags, wg0);
                 HIP_CHECK(hipEventRecord(b, stream));
                 push_ev.push_back({a, b});
@@ -1996,18 +2126,18 @@ struct ketogpu_engine {
         }
         hipEvent_t a = ev(), b = ev();
         HIP_CHECK(hipEventRecord(a, stream));
-        hipLaunchKernelGGL(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
+        KLAUNCH(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
                            q.dyn_full_off, q.dyn_full, q.allowed);
         HIP_CHECK(hipEventRecord(b, stream));
         pull_ev.push_back({a, b});
         // reset every visited entry recorded in this round (levels >= 1 and touch list)
         uint64_t first = level_begin.size() > 1 ? level_begin[1] : lb;
         if (lb > first)
-            hipLaunchKernelGGL(reset_kernel, dim3(blocks_for(lb - first)), dim3(kBlock), 0, stream, st.vis, g.Ni,
+            KLAUNCH(reset_kernel, dim3(blocks_for(lb - first)), dim3(kBlock), 0, stream, st.vis, g.Ni,
                                st.fe_key + first, lb - first);
         uint64_t ntouch = h_ctr[2];
         if (ntouch)
-            hipLaunchKernelGGL(reset_kernel, dim3(blocks_for(ntouch)), dim3(kBlock), 0, stream, st.vis, g.Ni, st.touch,
+            KLAUNCH(reset_kernel, dim3(blocks_for(ntouch)), dim3(kBlock), 0, stream, st.vis, g.Ni, st.touch,
                                ntouch);
         rs.touched += (lb - first) + ntouch;
         rs.rounds++;
@@ -2040,16 +2170,16 @@ struct ketogpu_engine {
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
         uint64_t words = (q.n + 63) / 64;
-        HIP_CHECK(hipMemsetAsync(st.stats, 0, (8 + 4 * kStatSlots) * sizeof(uint64_t), stream));
-        HIP_CHECK(hipMemsetAsync(q.flags, 0, std::max<uint64_t>(words, 1) * 8, stream));
-        HIP_CHECK(hipMemsetAsync(q.allowed, 0, std::max<uint64_t>(words, 1) * 8, stream));
+        // one launch zeroes results, flags, statistics and spill counters
+        KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
+                           q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen);
         HIP_CHECK(hipEventRecord(t_begin, stream));
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
             uint64_t ns = run_units(q, rs, unit_ev);
             rs.spilled_requests = ns;
             if (ns) {  // single requests whose closure exceeds an LDS table: global path
-                hipLaunchKernelGGL(spill_gather_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
+                KLAUNCH(spill_gather_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
                                    q.roots, q.targets, q.n, spill_roots, spill_targets);
                 Batch sb = q;
                 sb.roots = spill_roots;
@@ -2060,7 +2190,7 @@ struct ketogpu_engine {
                 HIP_CHECK(hipMemsetAsync(spill_flags, 0, (ns / 64 + 1) * 8, stream));
                 HIP_CHECK(hipMemsetAsync(spill_allowed, 0, (ns / 64 + 1) * 8, stream));
                 run_global(sb, rs, push_ev, pull_ev);
-                hipLaunchKernelGGL(spill_scatter_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
+                KLAUNCH(spill_scatter_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
                                    spill_allowed, spill_flags, q.allowed, q.flags);
             }
         } else {
@@ -2069,7 +2199,7 @@ struct ketogpu_engine {
         HIP_CHECK(hipEventRecord(t_end, stream));
         HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         uint64_t t3[3];
-        read_unit_stats(t3);  // synchronizes the stream
+        read_unit_stats(t3);  // both statistics regions; synchronizes the stream
         uint64_t examined = h_ctr[8];
         // unit path: 16 B per row opened (offset pair), 4 B per interior edge, 4 B per
         // reverse entry, 4+4 B per request (root, target), 8 B per result word

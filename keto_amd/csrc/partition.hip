@@ -314,6 +314,12 @@ inline unsigned pblocks(uint64_t n) { return (unsigned)std::max<uint64_t>(1, (n 
         if (_e != hipSuccess) throw Error(KETOGPU_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+#define KLAUNCH(...)                                 \
+    do {                                             \
+        hipLaunchKernelGGL(__VA_ARGS__);             \
+        PHIP(hipGetLastError());                     \
+    } while (0)
+
 template <class T>
 T *palloc(size_t n) {
     void *p = nullptr;
@@ -473,7 +479,7 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(P.allowed, 0, W * 8, stream));
         lb = cnt = edges = 0;
         cur = 0;
-        hipLaunchKernelGGL(part_seed_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P);
+        KLAUNCH(part_seed_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P);
         PHIP(hipGetLastError());
         stats.rounds++;
     }
@@ -489,7 +495,7 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
         if (n) {
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
-            hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
+            KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
             PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             PHIP(hipStreamSynchronize(stream));
             unsigned long long off = 0;
@@ -500,7 +506,7 @@ struct ketogpu_part {
             }
             PHIP(hipMemcpyAsync(d_cursor, h + 16 + kMaxWorld, world * sizeof(unsigned long long),
                                 hipMemcpyHostToDevice, stream));
-            hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_cursor, send);
+            KLAUNCH(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_cursor, send);
             PHIP(hipGetLastError());
         } else {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
@@ -516,7 +522,7 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(&P.ctr[nxt], 0, sizeof(unsigned long long), stream));
         const uint64_t base = lb + cnt;
         if (n)
-            hipLaunchKernelGGL(part_apply_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n, base,
+            KLAUNCH(part_apply_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n, base,
                                &P.ctr[nxt]);
         read_ctr();
         stats.records_received += n;
@@ -526,7 +532,7 @@ struct ketogpu_part {
         }
         const uint64_t ncnt = h[nxt] >> kCntShift, nedges = h[nxt] & kPreMask;
         if (ncnt)
-            hipLaunchKernelGGL(part_gather_kernel, dim3(pblocks(ncnt)), dim3(kPB), 0, stream, P, base, base + ncnt);
+            KLAUNCH(part_gather_kernel, dim3(pblocks(ncnt)), dim3(kPB), 0, stream, P, base, base + ncnt);
         lb = base;
         cnt = ncnt;
         edges = nedges;
@@ -542,7 +548,7 @@ struct ketogpu_part {
         if (cnt && edges) {
             uint64_t tiles = (edges + kPTile - 1) / kPTile;
             unsigned grid = (unsigned)std::min<uint64_t>(tiles, 256ull * 16);
-            hipLaunchKernelGGL(part_expand_kernel, dim3(grid), dim3(kPB), 0, stream, P, lb, cnt, edges);
+            KLAUNCH(part_expand_kernel, dim3(grid), dim3(kPB), 0, stream, P, lb, cnt, edges);
             PHIP(hipGetLastError());
             stats.forward_edges += edges;
         }
@@ -550,12 +556,12 @@ struct ketogpu_part {
     }
 
     void pull_emit() {
-        hipLaunchKernelGGL(part_pull_emit_kernel, dim3(pblocks(P.n)), dim3(kPB), 0, stream, P);
+        KLAUNCH(part_pull_emit_kernel, dim3(pblocks(P.n)), dim3(kPB), 0, stream, P);
         PHIP(hipGetLastError());
     }
 
     int pull_answer(const ketogpu_record *recv, uint64_t n) {
-        if (n) hipLaunchKernelGGL(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n);
+        if (n) KLAUNCH(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n);
         read_ctr();
         stats.queries_answered += n;
         return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_OK;
@@ -571,10 +577,10 @@ struct ketogpu_part {
         } else {
             const uint64_t ents = lb + cnt, ntouch = h[2];
             if (ents)
-                hipLaunchKernelGGL(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key,
+                KLAUNCH(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key,
                                    ents);
             if (ntouch)
-                hipLaunchKernelGGL(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
+                KLAUNCH(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
                                    ntouch);
         }
         PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));

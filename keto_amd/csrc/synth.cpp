@@ -283,6 +283,261 @@ ks_rbac *ks_rbac_generate(const ks_rbac_params *p) {
     return w;
 }
 
+// ---------------------------------------------------------------------------------
+// Config #3 (BASELINE.json configs[2]): drive-like folder hierarchy.  Folders in `depth`
+// levels (level k+1 twice the size of level k), every non-root folder's viewers include
+// its parent's: folders:f#viewer@(folders:parent(f)#viewer).  Flat groups with Poisson
+// memberships; the remaining tuples are grants folders:f#viewer@(groups:g#member)
+// (group_frac) or folders:f#viewer@u.  Checks folders:f#viewer@u, half constructed
+// positives (a grant on f or one of its ancestors).  Namespaces: groups 1, folders 2.
+typedef struct {
+    uint64_t users, groups, folders, tuples, checks, seed;
+    double member_mean, group_frac;
+    uint64_t depth, check_seed;
+} ks_folders_params;
+
+ks_rbac *ks_folders_generate(const ks_folders_params *p) {
+    auto *w = new ks_rbac();
+    Rng rng(p->seed);
+    const uint64_t U = p->users, G = std::max<uint64_t>(p->groups, 1), F = std::max<uint64_t>(p->folders, 1);
+    const uint64_t D = std::max<uint64_t>(1, std::min<uint64_t>(p->depth, 30));
+    // level sizes: L_k proportional to 2^k
+    std::vector<uint64_t> lbase(D + 1, 0);
+    {
+        double tot = (double)((1ull << D) - 1);
+        uint64_t acc = 0;
+        for (uint64_t k = 0; k < D; k++) {
+            uint64_t sz = k + 1 == D ? F - acc : std::max<uint64_t>(1, (uint64_t)((double)F * (double)(1ull << k) / tot));
+            if (acc + sz > F) sz = F - acc;
+            lbase[k] = acc;
+            acc += sz;
+        }
+        lbase[D] = F;
+    }
+    std::vector<uint32_t> parent(F, UINT32_MAX);
+    for (uint64_t k = 1; k < D; k++) {
+        uint64_t prev = lbase[k] - lbase[k - 1];
+        for (uint64_t f = lbase[k]; f < lbase[k + 1]; f++)
+            if (prev) parent[f] = (uint32_t)(lbase[k - 1] + rng.below(prev));
+    }
+    std::vector<std::vector<uint32_t>> members(G);
+    std::poisson_distribution<int> pois(p->member_mean);
+    std::mt19937_64 mt(p->seed ^ 0x5bd1e995);
+    for (uint64_t u = 0; u < U; u++) {
+        int k = pois(mt);
+        for (int j = 0; j < k; j++) members[rng.below(G)].push_back((uint32_t)u), w->n_member++;
+    }
+    for (uint64_t f = 0; f < F; f++) w->n_parent += parent[f] != UINT32_MAX;
+    uint64_t used = w->n_parent + w->n_member;
+    uint64_t n_grant = p->tuples > used ? p->tuples - used : F;
+    std::vector<std::vector<uint32_t>> fgroups(F), fusers(F);
+    for (uint64_t i = 0; i < n_grant; i++) {
+        uint64_t f = rng.below(F);
+        if (rng.unit() < p->group_frac)
+            fgroups[f].push_back((uint32_t)rng.below(G));
+        else
+            fusers[f].push_back((uint32_t)rng.below(U));
+    }
+    w->n_grant = n_grant;
+    std::vector<uint32_t> urank(U), grank(G), frank(F);
+    {
+        auto o = lex_order(U);
+        for (uint64_t i = 0; i < U; i++) urank[o[i]] = (uint32_t)i;
+        auto og = lex_order(G);
+        for (uint64_t i = 0; i < G; i++) grank[og[i]] = (uint32_t)i;
+        auto of = lex_order(F);
+        for (uint64_t i = 0; i < F; i++) frank[of[i]] = (uint32_t)i;
+    }
+    auto row_set = [&](int32_t ns, char op, uint64_t o, const char *rel, char sp, uint64_t so, int32_t sns,
+                       const char *srel) {
+        w->ns.push_back(ns);
+        w->kind.push_back(1);
+        w->ss_ns.push_back(sns);
+        w->obj.put_num(op, o);
+        w->rel.put(rel, strlen(rel));
+        w->sid.empty();
+        w->ss_obj.put_num(sp, so);
+        w->ss_rel.put(srel, strlen(srel));
+    };
+    auto row_id = [&](int32_t ns, char op, uint64_t o, const char *rel, uint64_t u) {
+        w->ns.push_back(ns);
+        w->kind.push_back(0);
+        w->ss_ns.push_back(0);
+        w->obj.put_num(op, o);
+        w->rel.put(rel, strlen(rel));
+        w->sid.put_num('u', u);
+        w->ss_obj.empty();
+        w->ss_rel.empty();
+    };
+    auto by_u = [&](uint32_t a, uint32_t b) { return urank[a] < urank[b]; };
+    auto by_g = [&](uint32_t a, uint32_t b) { return grank[a] < grank[b]; };
+    for (uint32_t g : lex_order(G)) {  // namespace 1: groups
+        auto &m = members[g];
+        std::sort(m.begin(), m.end(), by_u);
+        for (uint32_t u : m) row_id(1, 'g', g, "member", u);
+    }
+    for (uint32_t f : lex_order(F)) {  // namespace 2: folders; subject sets by (ns id, object)
+        auto &fg = fgroups[f];
+        std::sort(fg.begin(), fg.end(), by_g);
+        for (uint32_t g : fg) row_set(2, 'f', f, "viewer", 'g', g, 1, "member");
+        if (parent[f] != UINT32_MAX) row_set(2, 'f', f, "viewer", 'f', parent[f], 2, "viewer");
+        auto &fu = fusers[f];
+        std::sort(fu.begin(), fu.end(), by_u);
+        for (uint32_t u : fu) row_id(2, 'f', f, "viewer", u);
+    }
+    (void)frank;
+    if (p->check_seed) rng = Rng(p->check_seed);
+    const uint64_t C = p->checks;
+    w->chk_doc.resize(C);
+    w->chk_user.resize(C);
+    w->chk_pos.resize(C);
+    for (uint64_t i = 0; i < C; i++) {
+        uint64_t f = rng.below(F), u = rng.below(U);
+        bool pos = false;
+        if (rng.unit() < 0.5) {
+            for (int tries = 0; tries < 64 && !pos; tries++) {
+                uint64_t f0 = rng.below(F), a = f0;
+                uint64_t up = rng.below(D);
+                for (uint64_t s = 0; s < up && parent[a] != UINT32_MAX; s++) a = parent[a];
+                uint64_t ng = fgroups[a].size(), nu = fusers[a].size();
+                if (!ng && !nu) continue;
+                uint64_t k = rng.below(ng + nu);
+                if (k >= ng) {
+                    f = f0, u = fusers[a][k - ng], pos = true;
+                } else {
+                    auto &m = members[fgroups[a][k]];
+                    if (m.empty()) continue;
+                    f = f0, u = m[rng.below(m.size())], pos = true;
+                }
+            }
+        }
+        w->chk_doc[i] = (uint32_t)f;
+        w->chk_user[i] = (uint32_t)u;
+        w->chk_pos[i] = pos;
+        w->rq_ns.put("folders", 7);
+        w->rq_obj.put_num('f', f);
+        w->rq_rel.put("viewer", 6);
+        w->rq_sid.put_num('u', u);
+    }
+    return w;
+}
+
+// ---------------------------------------------------------------------------------
+// Config #4 (BASELINE.json configs[3]): power-law social/group graph.  Users join
+// Poisson(member_mean) groups chosen by Zipf(s) popularity; groups nest into groups
+// (groups:gP#member@(groups:gC#member)) with Zipf popularity on BOTH ends, acyclic (the
+// parent precedes the child in a random order), `nest_per_group` edges per group on
+// average.  Checks groups:g#member@u, g half Zipf-popular half uniform, half constructed
+// positives (a walk down from g).  Namespace: groups 1.
+typedef struct {
+    uint64_t users, groups, tuples, checks, seed;
+    double zipf_s, member_mean, nest_per_group;
+    uint64_t check_seed;
+} ks_social_params;
+
+ks_rbac *ks_social_generate(const ks_social_params *p) {
+    auto *w = new ks_rbac();
+    Rng rng(p->seed);
+    const uint64_t U = p->users, G = std::max<uint64_t>(p->groups, 2);
+    std::vector<double> cdf(G);
+    {
+        double acc = 0;
+        for (uint64_t k = 0; k < G; k++) acc += 1.0 / std::pow((double)(k + 1), p->zipf_s), cdf[k] = acc;
+        for (auto &x : cdf) x /= acc;
+    }
+    auto zipf = [&]() {
+        uint64_t r = std::lower_bound(cdf.begin(), cdf.end(), rng.unit()) - cdf.begin();
+        return r >= G ? G - 1 : r;
+    };
+    // popularity rank -> group (member side), topological position of each group
+    std::vector<uint32_t> pop(G), topo(G), at(G);
+    std::iota(pop.begin(), pop.end(), 0u);
+    for (uint64_t i = G; i > 1; i--) std::swap(pop[i - 1], pop[rng.below(i)]);
+    std::iota(at.begin(), at.end(), 0u);
+    for (uint64_t i = G; i > 1; i--) std::swap(at[i - 1], at[rng.below(i)]);
+    for (uint64_t i = 0; i < G; i++) topo[at[i]] = (uint32_t)i;  // topo[g] = position
+    std::vector<std::vector<uint32_t>> children(G), members(G);
+    const uint64_t n_nest = (uint64_t)(p->nest_per_group * (double)G);
+    for (uint64_t i = 0; i < n_nest; i++) {
+        uint32_t a = pop[zipf()], b = pop[zipf()];
+        if (a == b) continue;
+        if (topo[a] > topo[b]) std::swap(a, b);  // parent precedes child: acyclic
+        children[a].push_back(b);
+        w->n_parent++;
+    }
+    uint64_t budget = p->tuples > w->n_parent ? p->tuples - w->n_parent : U;
+    std::poisson_distribution<int> pois(p->member_mean);
+    std::mt19937_64 mt(p->seed ^ 0x5bd1e995);
+    for (uint64_t u = 0; u < U && w->n_member < budget; u++) {
+        int k = pois(mt);
+        for (int j = 0; j < k; j++) members[pop[zipf()]].push_back((uint32_t)u), w->n_member++;
+    }
+    std::vector<uint32_t> urank(U), grank(G);
+    {
+        auto o = lex_order(U);
+        for (uint64_t i = 0; i < U; i++) urank[o[i]] = (uint32_t)i;
+        auto og = lex_order(G);
+        for (uint64_t i = 0; i < G; i++) grank[og[i]] = (uint32_t)i;
+    }
+    auto by_u = [&](uint32_t a, uint32_t b) { return urank[a] < urank[b]; };
+    auto by_g = [&](uint32_t a, uint32_t b) { return grank[a] < grank[b]; };
+    for (uint32_t g : lex_order(G)) {
+        auto &ch = children[g];
+        std::sort(ch.begin(), ch.end(), by_g);
+        for (uint32_t c : ch) {
+            w->ns.push_back(1);
+            w->kind.push_back(1);
+            w->ss_ns.push_back(1);
+            w->obj.put_num('g', g);
+            w->rel.put("member", 6);
+            w->sid.empty();
+            w->ss_obj.put_num('g', c);
+            w->ss_rel.put("member", 6);
+        }
+        auto &m = members[g];
+        std::sort(m.begin(), m.end(), by_u);
+        for (uint32_t u : m) {
+            w->ns.push_back(1);
+            w->kind.push_back(0);
+            w->ss_ns.push_back(0);
+            w->obj.put_num('g', g);
+            w->rel.put("member", 6);
+            w->sid.put_num('u', u);
+            w->ss_obj.empty();
+            w->ss_rel.empty();
+        }
+    }
+    if (p->check_seed) rng = Rng(p->check_seed);
+    const uint64_t C = p->checks;
+    w->chk_doc.resize(C);
+    w->chk_user.resize(C);
+    w->chk_pos.resize(C);
+    for (uint64_t i = 0; i < C; i++) {
+        uint64_t g = rng.unit() < 0.5 ? pop[zipf()] : rng.below(G), u = rng.below(U);
+        bool pos = false;
+        if (rng.unit() < 0.5) {
+            uint64_t c = g;
+            for (int hop = 0; hop < 16 && !pos; hop++) {  // walk down to a member
+                uint64_t nc = children[c].size(), nm = members[c].size();
+                if (!nc && !nm) break;
+                uint64_t k = rng.below(nc + nm);
+                if (k >= nc)
+                    u = members[c][k - nc], pos = true;
+                else
+                    c = children[c][k];
+            }
+        }
+        w->chk_doc[i] = (uint32_t)g;
+        w->chk_user[i] = (uint32_t)u;
+        w->chk_pos[i] = pos;
+        w->rq_ns.put("groups", 6);
+        w->rq_obj.put_num('g', g);
+        w->rq_rel.put("member", 6);
+        w->rq_sid.put_num('u', u);
+    }
+    return w;
+}
+
 void ks_rbac_view_get(const ks_rbac *w, ks_rbac_view *v) {
     v->n = w->ns.size();
     v->namespace_id = w->ns.data();

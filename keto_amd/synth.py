@@ -2,6 +2,9 @@
 
 Config #2 — synthetic RBAC: 10M users, 100k nested groups,
 50M tuples, 1M checks docs:d#viewer@u (half constructed positives), seed 0x4B45544F.
+Config #3 — drive-like folders (parent#viewer subject sets, depth 10, 500M tuples).
+Config #4 — power-law social/group graph (1B tuples).  Full sizes are the defaults of
+rbac() / folders() / social(); tests and quick runs pass smaller sizes.
 Rows come out in the reference's ORDER BY order (SQLite semantics), i.e. exactly what
 the snapshot loader would read from the database.
 """
@@ -22,6 +25,17 @@ class Params(C.Structure):
         ("zipf_s", C.c_double), ("member_mean", C.c_double), ("check_seed", C.c_uint64)]
 
 
+class FolderParams(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("users", "groups", "folders", "tuples", "checks", "seed")] + [
+        ("member_mean", C.c_double), ("group_frac", C.c_double), ("depth", C.c_uint64), ("check_seed", C.c_uint64)]
+
+
+class SocialParams(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("users", "groups", "tuples", "checks", "seed")] + [
+        ("zipf_s", C.c_double), ("member_mean", C.c_double), ("nest_per_group", C.c_double),
+        ("check_seed", C.c_uint64)]
+
+
 class View(C.Structure):
     _fields_ = [("n", C.c_uint64)] + [(n, C.c_void_p) for n in (
         "namespace_id", "object_data", "object_off", "relation_data", "relation_off", "subject_kind",
@@ -40,6 +54,10 @@ def slib():
         _slib = C.CDLL(path)
         _slib.ks_rbac_generate.restype = C.c_void_p
         _slib.ks_rbac_generate.argtypes = [C.POINTER(Params)]
+        _slib.ks_folders_generate.restype = C.c_void_p
+        _slib.ks_folders_generate.argtypes = [C.POINTER(FolderParams)]
+        _slib.ks_social_generate.restype = C.c_void_p
+        _slib.ks_social_generate.argtypes = [C.POINTER(SocialParams)]
         _slib.ks_rbac_view_get.argtypes = [C.c_void_p, C.POINTER(View)]
         _slib.ks_rbac_free.argtypes = [C.c_void_p]
     return _slib
@@ -53,13 +71,18 @@ def _arr(ptr, n, dtype):
 
 
 class Workload:
-    """rows (columnar, ORDER BY order) + check requests; arrays view C++ memory"""
+    """rows (columnar, ORDER BY order) + check requests; arrays view C++ memory.
+    A request i is (ns, f"{prefix}{chk_doc[i]}", relation) @ u{chk_user[i]}."""
 
-    namespaces = [("groups", 1), ("docs", 2)]
-
-    def __init__(self, params: Params):
+    def __init__(self, params, kind="rbac"):
         self.params = params
-        self.h = slib().ks_rbac_generate(C.byref(params))
+        self.kind = kind
+        gen, self.namespaces, self.request_shape = {
+            "rbac": (slib().ks_rbac_generate, [("groups", 1), ("docs", 2)], ("docs", "d", "viewer")),
+            "folders": (slib().ks_folders_generate, [("groups", 1), ("folders", 2)], ("folders", "f", "viewer")),
+            "social": (slib().ks_social_generate, [("groups", 1)], ("groups", "g", "member")),
+        }[kind]
+        self.h = gen(C.byref(params))
         v = View()
         slib().ks_rbac_view_get(self.h, C.byref(v))
         self.v = v
@@ -105,7 +128,8 @@ class Workload:
 
     def requests(self, idx):
         """(ns, obj, rel, subject dict) for the oracle"""
-        return [("docs", f"d{int(self.chk_doc[i])}", "viewer", {"subject_id": f"u{int(self.chk_user[i])}"})
+        ns, prefix, rel = self.request_shape
+        return [(ns, f"{prefix}{int(self.chk_doc[i])}", rel, {"subject_id": f"u{int(self.chk_user[i])}"})
                 for i in idx]
 
 
@@ -113,3 +137,17 @@ def rbac(users=10_000_000, groups=100_000, docs=2_000_000, tuples=50_000_000, ch
          zipf_s=1.1, member_mean=3.0, check_seed=0):
     """check_seed = 0: checks drawn from the graph's own random stream"""
     return Workload(Params(users, groups, docs, tuples, checks, seed, zipf_s, member_mean, check_seed))
+
+
+def folders(users=10_000_000, groups=100_000, folders=20_000_000, tuples=500_000_000, checks=1_000_000, seed=SEED,
+            member_mean=3.0, group_frac=0.1, depth=10, check_seed=0):
+    """config #3: drive-like folder hierarchy (parent#viewer subject sets, depth 10)"""
+    return Workload(FolderParams(users, groups, folders, tuples, checks, seed, member_mean, group_frac, depth,
+                                 check_seed), "folders")
+
+
+def social(users=100_000_000, groups=10_000_000, tuples=1_000_000_000, checks=1_000_000, seed=SEED, zipf_s=1.0,
+           member_mean=8.0, nest_per_group=1.0, check_seed=0):
+    """config #4: power-law social/group graph (Zipf popularity, acyclic nesting)"""
+    return Workload(SocialParams(users, groups, tuples, checks, seed, zipf_s, member_mean, nest_per_group,
+                                 check_seed), "social")

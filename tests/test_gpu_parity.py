@@ -45,10 +45,21 @@ def test_nil_subject_is_bad_request():
         eng.SubjectIsAllowed(rt.InternalRelationTuple("n", "o", "r", None))
 
 
+@pytest.fixture(params=["bidi", "bidi-wide", "v2"])
+def unit_plan(request, monkeypatch):
+    """first LDS pass of engines created while active: the default bidirectional units
+    (one-wave, 512-slot tables), bidi with the wide 2048-slot table, or forward-only unit2"""
+    if request.param == "v2":
+        monkeypatch.setenv("KETOGPU_UNITS", "v2")
+    elif request.param == "bidi-wide":
+        monkeypatch.setenv("KETOGPU_BIDI", "11,256,384,6")
+    return request.param
+
+
 @pytest.mark.parametrize("seed,page_size,poison,collide,empty_ns,words", [
     (31, 100, False, False, False, 0), (32, 3, True, False, True, 0), (33, 2, True, True, False, 0),
     (34, 1, False, True, True, 0), (35, 100, False, False, False, 1), (36, 5, True, True, True, 2)])
-def test_random_tables_match_oracle(seed, page_size, poison, collide, empty_ns, words):
+def test_random_tables_match_oracle(seed, page_size, poison, collide, empty_ns, words, unit_plan):
     namespaces, rows = randgraph.make_graph(seed, n_rows=600, n_obj=30, n_users=40, poison=poison, collide=collide,
                                             empty_ns=empty_ns)
     snap = Snapshot.from_rows(namespaces, rows, page_size=page_size, sort=True)
@@ -136,9 +147,14 @@ def test_deep_chain_has_no_depth_cutoff():
     assert eng.check_many(reqs) == [True, True, True, True, False, False, True]
 
 
-def test_rbac_sample_matches_oracle():
+@pytest.mark.parametrize("kind", ["rbac", "folders", "social"])
+def test_synthetic_configs_match_oracle(kind, unit_plan):
+    """BASELINE configs #2 (RBAC), #3 (folders, depth 10) and #4 (power-law groups) at
+    small scale, every request against the oracle"""
     from keto_amd import synth
-    w = synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=20000, seed=7)
+    w = {"rbac": lambda: synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=20000, seed=7),
+         "folders": lambda: synth.folders(users=8000, groups=300, folders=12000, tuples=150000, checks=20000, seed=7),
+         "social": lambda: synth.social(users=20000, groups=6000, tuples=150000, checks=20000, seed=7)}[kind]()
     snap = Snapshot.from_columns(w.namespaces, w.columns)
     orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
     roots, targets = w.resolve(snap)

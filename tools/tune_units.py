@@ -23,11 +23,11 @@ engines, queries = {}, {}
 for p in plans:
     if p == "global":
         os.environ["KETOGPU_PATH"] = "global"
-    else:  # plan[:hlog], e.g. bidi:10
+    else:  # plan[:hlog,threads], e.g. bidi:9,64
         os.environ.pop("KETOGPU_PATH", None)
         os.environ["KETOGPU_UNITS"] = p.split(":")[0]
         if ":" in p:
-            os.environ["KETOGPU_BIDI_HLOG"] = p.split(":")[1]
+            os.environ["KETOGPU_BIDI"] = p.split(":")[1]
     engines[p] = check.Engine(snap, state_budget_bytes=16 << 30)
     queries[p] = engines[p].upload(roots, targets)
 ref = None
