@@ -17,7 +17,7 @@ KRX="bidi_kernel|unit2_kernel|expand_kernel|pull_kernel"
 echo "[profile] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B \
   > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
-tail -1 "$OUT/trace.log" > "$OUT/bench_line.json"
+grep '^{"metric"' "$OUT/trace.log" > "$OUT/bench_line.json"
 for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
          "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD"; do
   tag=$(echo "$C" | cut -d' ' -f1)
