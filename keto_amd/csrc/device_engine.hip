@@ -471,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void unit_kernel(DevGraph g, const uint32_t
     __shared__ UnitShared S;
     const int tid = threadIdx.x;
     // diagnostic build only (stamps != nullptr): s_memtime at phase boundaries
-    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
     uint32_t n_levels = 0;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
                                                        unsigned long long *stats, unsigned long long *stamps) {
     __shared__ Unit2Shared<U> S;
     const int tid = threadIdx.x;
-    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
     uint32_t n_levels = 0;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
@@ -888,41 +888,51 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // --------------------------------------------- bidirectional units (v3, default)
 // Reachability is symmetric under edge reversal: with B(t) = expandable nodes that reach
 // t through >= 1 edge, allowed(r, t) <=> r in B(t).  v3 grows BOTH sides of every request
-// of a 16-request unit in one LDS table whose 64-bit state word per node holds, per
-// direction d (0 forward, 1 backward), visited bits << 32d and pending bits << 32d + 16:
+// of a unit in one LDS table whose 64-bit state word per node holds, per direction d
+// (0 forward, 1 backward), visited bits << 32d and pending bits << 32d + 16:
 //   * forward from r over the interior subgraph (FRec records, as v2),
 //   * backward from t over interior predecessors (BRec records parallel to rev_col: node
 //     ids put interior nodes first and reverse rows are sorted, so a node's interior
 //     predecessors are exactly the prefix of its reverse row).
-// Seed level: r is marked forward-visited, fint(r) is pushed forward and every entry of
-// rev(t) backward (a source entry can only meet r itself, so it is compared, not stored).
-// A request is allowed as soon as one node carries both of its bits.  Each later level,
-// every open request expands the side whose pending frontier has the smaller degree sum
-// (bidirectional BFS), so the work is bounded by the cheaper side and positives stop
-// where the searches meet.  A request whose pending frontier is empty on either side is
-// false: a path r -> v1 -> ... -> vk = t has v1 in fint(r) and v(k-1) in rev(t), both
-// marked by the seed, so a closed side would already have met the other (no depth
-// cutoff, R2).  Used when the snapshot has no ambiguous keys (R4 flags are raised by
-// forward rows) and record begins fit u32; dynamic roots and table/list overflow spill
-// to the v2 cascade.
-// HLOG: log2 of the LDS table slots; F: pending/expansion list capacity; BT: threads per
-// unit (256 = four waves, 64 = one wave: more units per CU, barriers of one wave); LF:
+// Seeds: r is forward-visited at distance 0, t backward-visited at distance 0 (unless
+// t = r: a meet needs >= 1 edge).  When both seed rows are short (fint(r) and rev(t) <=
+// kSeedBothMax) both are pushed at once; otherwise r and t become pending and the first
+// level reads only the cheaper row, so a long rev(t) (a user with many direct grants)
+// never floods the table.  A request is allowed as soon as one node carries both of its
+// bits (a source entry of rev(t) can only meet r itself, so it is compared, not stored).
+// Each level, every open request expands both sides while both pending degree sums are
+// small, else the cheaper side (bidirectional BFS): work is bounded by the cheaper side
+// and positives stop where the searches meet.  Closure: a request whose pending frontier
+// is empty on one side is decided once the OTHER side's seed row has been read — every
+// path r -> v1 -> ... -> v(k-1) -> t has v1 in fint(r) and v(k-1) in rev(t); if that
+// seed is still pending it is expanded in lookup-only mode (checked against the closed
+// side, nothing inserted).  No depth cutoff (R2).  Used when the snapshot has no
+// ambiguous keys (R4 flags are raised by forward rows) and record begins fit u32;
+// dynamic roots and table/list overflow spill to the next stage.
+constexpr uint32_t kBothMax = 12;      // both sides expand while both pending sums are <= this
+constexpr uint32_t kSeedBothMax = 32;  // seeds pushed eagerly when both seed rows are <= this
+
+// HLOG: log2 of the LDS table slots; F: pending list capacity; BT: threads per unit
+// (256 = four waves, 64 = one wave: more units per CU, barriers of one wave); LF:
 // maximum table load in eighths (a unit spills beyond it)
 template <int U, int HLOG, int F, int BT, int LF = 6>
 struct BidiShared {
     static constexpr int H = 1 << HLOG;
     static constexpr int HMAX = H * LF / 8;
+    static constexpr int EM = BT > 2 * U ? BT : 2 * U;
     uint32_t key[H];
     unsigned long long st[H];
     uint16_t p_sd[2][F];  // pending lists (ping-pong): slot | dir << 15
     uint32_t p_begin[2][F], p_deg[2][F];
-    uint16_t e_sd[F], e_mask[F];  // this level's expansion list
-    uint32_t e_begin[F], e_deg[F];
+    uint16_t e_sd[2 * U];  // eager seed rows: forward of r_j, backward of t_j
+    uint32_t e_begin[2 * U], e_deg[2 * U];
+    uint16_t e_mask[EM];   // request bits of the entries being expanded
     uint32_t c_pre[BT + 1];
     uint32_t wave_sum[BT / 64];
-    uint32_t cost[2][U];
+    uint32_t cost[2][U];          // pending degree sums per direction and request
     uint32_t root[U];
-    uint32_t sel[2];
+    uint16_t rslot[U], tslot[U];  // table slots of the seeds r_j, t_j
+    uint32_t sel[2], lookup[2];   // per direction: bits expanded this level / lookup-only bits
     uint32_t n_used, n_e, n_p[2], spill, found, active;
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
 };
@@ -964,31 +974,40 @@ __device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
     return base + lanes_below(bal);
 }
 
+// find (insert == false) or find-or-insert u; -1 when absent (or the table is full)
+template <int HLOG>
+__device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
+    constexpr int H = 1 << HLOG;
+    uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
+    for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
+        uint32_t kv = key[hh];
+        if (kv == kEmpty) {
+            if (!insert) return -1;
+            uint32_t prev = atomicCAS(&key[hh], kEmpty, u);
+            if (prev == kEmpty) {
+                inserted = true;
+                return (int)hh;
+            }
+            kv = prev;
+        }
+        if (kv == u) return (int)hh;
+    }
+    return -1;
+}
+
+// Push mask m into node u in direction d.  Bits in S.lookup[d] belong to requests whose
+// other side is closed: for them u is only looked up (a meet or nothing), never inserted
+// nor made pending.  New pending bits add deg to their requests' pending sums.
 template <int U, int HLOG, int F, int BT, int LF>
-__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, bool want, uint32_t u, uint32_t deg, uint32_t begin,
-                                          uint32_t m, int d, int nxt) {
+__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, bool want, uint32_t u, uint32_t deg,
+                                          uint32_t begin, uint32_t m, int d, int nxt) {
+    const uint32_t lk = m & S.lookup[d];
     int h = -1;
     bool inserted = false;
     if (want) {
-        constexpr int H = BidiShared<U, HLOG, F, BT, LF>::H;
-        uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
-        for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
-            uint32_t kv = S.key[hh];
-            if (kv == kEmpty) {
-                uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
-                if (prev == kEmpty) {
-                    inserted = true;
-                    h = (int)hh;
-                    break;
-                }
-                kv = prev;
-            }
-            if (kv == u) {
-                h = (int)hh;
-                break;
-            }
-        }
-        if (h < 0) S.spill = 1;
+        const bool ins = (m & ~lk) != 0;
+        h = bidi_slot<HLOG>(S.key, u, ins, inserted);
+        if (h < 0 && ins) S.spill = 1;
     }
     const int lane = threadIdx.x & 63;
     uint64_t bal = __ballot(inserted);
@@ -1005,10 +1024,11 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, boo
         uint32_t newly = m & ~(uint32_t)(old >> vs) & 0xFFFFu;
         uint32_t meet = newly & (uint32_t)(old >> (32 - vs)) & 0xFFFFu;
         if (meet) atomicOr(&S.found, meet);
-        newly &= ~meet;
+        newly &= ~(meet | lk);
         if (newly && deg) {
             unsigned long long o2 = atomicOr(&S.st[h], (unsigned long long)newly << (vs + 16));
             app = !((uint32_t)(o2 >> (vs + 16)) & 0xFFFFu);
+            for (uint32_t b = newly; b; b &= b - 1) atomicAdd(&S.cost[d][__ffs(b) - 1], deg);
         }
     }
     uint32_t idx = lds_append(app, &S.n_p[nxt]);
@@ -1023,12 +1043,13 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, boo
     }
 }
 
-// expand expansion-list entries [base, base + k); block-uniform loop count
+// Expand k entries (entry j: sd[j], begin[j], S.e_mask[j]); `my_deg` is the degree this
+// thread contributes for entry threadIdx.x (0 when it has none).  Block-uniform loop.
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
-                                            BidiShared<U, HLOG, F, BT, LF> &S, uint32_t base, uint32_t k, int nxt, uint64_t &edges) {
-    uint32_t dg = (uint32_t)threadIdx.x < k ? S.e_deg[base + threadIdx.x] : 0;
-    uint32_t total = block_scan_sh<BT>(dg, S);
+                                            BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, uint32_t k,
+                                            const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
+    const uint32_t total = block_scan_sh<BT>(my_deg, S);
     for (uint32_t eb = 0; eb < total; eb += BT) {
         uint32_t e = eb + threadIdx.x;
         bool want = e < total;
@@ -1043,10 +1064,9 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
                 else
                     hi = mid;
             }
-            const uint32_t idx = base + lo;
-            d = S.e_sd[idx] >> 15;
-            m = S.e_mask[idx] & S.active & ~*(volatile uint32_t *)&S.found;
-            FRec rc = (d ? brec : frec)[(uint64_t)S.e_begin[idx] + (e - S.c_pre[lo])];
+            d = sd[lo] >> 15;
+            m = S.e_mask[lo] & S.active & ~*(volatile uint32_t *)&S.found;
+            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
             u = rc.node;
             deg = rc.deg;
             bg = rc.begin;
@@ -1072,11 +1092,12 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                                           unsigned int *spill_count, unsigned long long *stats,
                                           unsigned long long *stamp) {
     static_assert(U <= 16, "16 request bits per direction");
+    using SH = BidiShared<U, HLOG, F, BT, LF>;
     const int tid = threadIdx.x;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t c0 = unit * U;
     const int shift = (int)(c0 & 63);
-    for (int i = tid; i < BidiShared<U, HLOG, F, BT, LF>::H; i += BT) {
+    for (int i = tid; i < SH::H; i += BT) {
         S.key[i] = kEmpty;
         S.st[i] = 0;
     }
@@ -1085,55 +1106,81 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
     }
     if (tid < 2 * U) S.cost[tid / U][tid % U] = 0;
+    if (tid < 2) S.lookup[tid] = 0;
+    __syncthreads();
     uint64_t rows = 0, edges = 0;
     uint32_t n_levels = 0;
-    // seed list: entry j < U = forward row of r_j, entry U + j = reverse row of t_j
+    uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+    uint64_t fb = 0, fe = 0, rb = 0, re = 0;
     if (tid < U) {
         uint64_t c = c0 + tid;
-        uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
         if (c < n) {
             r = roots[c];
             t = targets[c];
         }
         if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
-        uint64_t fb = 0, fe = 0, rb = 0, re = 0;
         if (r != KETOGPU_NODE_NONE && r < kDynBase) {
             fb = g.fint_off[r];
             fe = g.fint_off[r + 1];
             rb = g.rev_off[t];
             re = g.rev_off[t + 1];
             rows += 2;
+            if (re > rb) atomicOr(&S.active, 1u << tid);  // nothing reaches a t without predecessors
         }
-        S.root[tid] = r;
-        S.e_sd[tid] = 0;
-        S.e_mask[tid] = (uint16_t)(1u << tid);
-        S.e_begin[tid] = (uint32_t)fb;
-        S.e_deg[tid] = (uint32_t)(fe - fb);
-        S.e_sd[U + tid] = (uint16_t)(1u << 15);
-        S.e_mask[U + tid] = (uint16_t)(1u << tid);
-        S.e_begin[U + tid] = (uint32_t)rb;
-        S.e_deg[U + tid] = (uint32_t)(re - rb);
-    }
-    __syncthreads();
-    if (tid < U) {
-        uint32_t r = S.root[tid];
         if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
-        if (r != KETOGPU_NODE_NONE && r < kDynBase) atomicOr(&S.active, 1u << tid);
+        S.root[tid] = r;
     }
     __syncthreads();
     if (S.spill) {
         if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
         return;
     }
-    // r is forward-visited at distance 0 (interior roots only: a source root can only be
-    // reached backward from rev(t), where it is compared directly)
-    if (tid < 64) {
-        bool v = tid < U && ((S.active >> tid) & 1u) && S.root[tid] < g.Ni;
-        bidi_push<U, HLOG, F, BT, LF>(S, v, v ? S.root[tid] : 0, 0, 0, 1u << (tid & 15), 0, 0);
+    if (tid < 64) {  // wave 0: lane j < U seeds request j
+        const bool v = tid < U && ((S.active >> tid) & 1u);
+        const uint32_t bit = 1u << (tid & 15);
+        const uint32_t rdeg = (uint32_t)(fe - fb), tdeg = (uint32_t)(re - rb);
+        const bool eager = rdeg <= kSeedBothMax && tdeg <= kSeedBothMax;
+        for (int side = 0; side < 2; side++) {
+            const uint32_t u = side ? t : r, deg = side ? tdeg : rdeg;
+            bool inserted = false;
+            const int h = v ? bidi_slot<HLOG>(S.key, u, true, inserted) : -1;
+            uint64_t bal = __ballot(inserted);
+            if (tid == 0) S.n_used += (uint32_t)__popcll(bal);  // <= 2U slots, far below HMAX
+            bool app = false;
+            if (h >= 0) {
+                if (side == 0)
+                    S.rslot[tid] = (uint16_t)h;
+                else
+                    S.tslot[tid] = (uint16_t)h;
+                const bool pend = !eager && deg;
+                unsigned long long bits = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
+                if (pend) bits |= (unsigned long long)bit << (32 * side + 16);
+                unsigned long long old = atomicOr(&S.st[h], bits);
+                app = pend && !((uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
+                if (pend) atomicAdd(&S.cost[side][tid], deg);
+            }
+            uint32_t idx = lds_append(app, &S.n_p[0]);
+            if (app) {  // idx < 2U <= F
+                S.p_sd[0][idx] = (uint16_t)(h | (side << 15));
+                S.p_begin[0][idx] = (uint32_t)(side ? rb : fb);
+                S.p_deg[0][idx] = deg;
+            }
+        }
+        if (tid < U) {  // eager rows (zero degree when not eager or not active)
+            const bool e = v && eager;
+            S.e_sd[tid] = 0;
+            S.e_begin[tid] = (uint32_t)fb;
+            S.e_deg[tid] = e ? rdeg : 0;
+            S.e_sd[U + tid] = (uint16_t)(1u << 15);
+            S.e_begin[U + tid] = (uint32_t)rb;
+            S.e_deg[U + tid] = e ? tdeg : 0;
+        }
+        if (tid < 2 * U) S.e_mask[tid] = (uint16_t)(1u << (tid % U));
     }
     __syncthreads();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
-    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, 0, 2 * U, 0, edges);
+    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, (uint32_t)tid < 2 * U ? S.e_deg[tid] : 0, 2 * U, S.e_sd,
+                                    S.e_begin, 0, edges);
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
     for (;;) {
@@ -1142,69 +1189,78 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         const uint32_t act = S.active & ~S.found;
         if (S.spill || !cnt || !act) break;
         n_levels++;
-        // per-request pending degree sums per direction
-        for (uint32_t base = 0; base < cnt; base += BT) {
-            uint32_t i = base + tid;
-            if (i < cnt) {
-                uint32_t sd = S.p_sd[cur][i], d = sd >> 15;
-                uint32_t pb = (uint32_t)(S.st[sd & 0x7FFFu] >> (32 * d + 16)) & act;
-                uint32_t dg = S.p_deg[cur][i];
-                for (; pb; pb &= pb - 1) atomicAdd(&S.cost[d][__ffs(pb) - 1], dg);
-            }
-        }
-        __syncthreads();
+        unsigned long long tp0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
         const int nxt = cur ^ 1;
         if (tid < 64) {
-            bool a = tid < U && ((act >> tid) & 1u);
-            uint32_t cf = a ? S.cost[0][tid] : 0, cb = a ? S.cost[1][tid] : 0;
-            uint64_t closed = __ballot(a && (cf == 0 || cb == 0));
-            uint64_t fwd = __ballot(a && cf && cb && cf <= cb);
-            uint64_t bwd = __ballot(a && cf && cb && cf > cb);
-            if (tid < U) S.cost[0][tid] = S.cost[1][tid] = 0;
+            // per request: expand both sides while both are cheap, else the cheaper one;
+            // a closed side decides the request once the other seed row has been read,
+            // else that seed is read in lookup-only mode
+            const bool a = tid < U && ((act >> tid) & 1u);
+            const uint32_t cf = a ? S.cost[0][tid] : 0, cb = a ? S.cost[1][tid] : 0;
+            const int j = tid & 15;
+            const bool rp = a && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);  // fint(r) unread
+            const bool tp = a && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);  // rev(t) unread
+            const bool fc = a && !cf, bc = a && !cb;
+            const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
+            const bool open = a && !closed;
+            const bool lkb = open && fc, lkf = open && bc;
+            const bool both = open && !fc && !bc && cf <= kBothMax && cb <= kBothMax;
+            const bool fwd = lkf || both || (open && !fc && !bc && cf <= cb);
+            const bool bwd = lkb || both || (open && !fc && !bc && cf > cb);
+            const uint64_t bcl = __ballot(closed), bf = __ballot(fwd), bb = __ballot(bwd);
+            const uint64_t lf = __ballot(lkf), lb = __ballot(lkb);
             if (tid == 0) {
-                S.active = act & ~(uint32_t)closed;
-                S.sel[0] = (uint32_t)fwd;
-                S.sel[1] = (uint32_t)bwd;
-                S.n_e = 0;
+                S.active = act & ~(uint32_t)bcl;
+                S.sel[0] = (uint32_t)bf;
+                S.sel[1] = (uint32_t)bb;
+                S.lookup[0] = (uint32_t)lf;
+                S.lookup[1] = (uint32_t)lb;
                 S.n_p[nxt] = 0;
             }
         }
         __syncthreads();
-        // split: the chosen direction's bits go to this level's expansion list, open
-        // requests' other bits stay pending (carried to the next list)
+        unsigned long long tp1 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+        // chunks of BT pending entries: the chosen direction's bits are taken (their
+        // pending sums drop) and expanded right away, open requests' other bits stay
+        // pending (the entry is carried to the next list)
         const uint32_t act2 = S.active;
-        for (uint32_t base = 0; base < cnt; base += BT) {
-            uint32_t i = base + tid;
-            uint32_t take = 0, rest = 0, sd = 0;
-            if (i < cnt) {
+        for (uint32_t base = 0; base < cnt && !S.spill; base += BT) {  // S.spill: read after a barrier
+            const uint32_t k = cnt - base < (uint32_t)BT ? cnt - base : (uint32_t)BT;
+            const uint32_t i = base + tid;
+            uint32_t take = 0, rest = 0, sd = 0, dg = 0, bg = 0;
+            if ((uint32_t)tid < k) {
                 sd = S.p_sd[cur][i];
+                dg = S.p_deg[cur][i];
+                bg = S.p_begin[cur][i];
                 const uint32_t d = sd >> 15, s = sd & 0x7FFFu;
-                uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
+                const uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
                 take = pb & S.sel[d];
                 rest = pb & act2 & ~take;
-                uint32_t clr = pb & ~rest;
-                if (clr) atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
+                const uint32_t clr = pb & ~rest;
+                if (clr) {
+                    atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
+                    for (uint32_t b = clr; b; b &= b - 1) atomicSub(&S.cost[d][__ffs(b) - 1], dg);
+                }
+                S.e_mask[tid] = (uint16_t)take;
             }
-            uint32_t ei = lds_append(take != 0, &S.n_e);
-            uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
-            if (take) {  // ei < cnt <= F
-                S.e_sd[ei] = (uint16_t)sd;
-                S.e_mask[ei] = (uint16_t)take;
-                S.e_begin[ei] = S.p_begin[cur][i];
-                S.e_deg[ei] = S.p_deg[cur][i];
+            const uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
+            if (rest) {
+                if (pi < (uint32_t)F) {
+                    S.p_sd[nxt][pi] = (uint16_t)sd;
+                    S.p_begin[nxt][pi] = bg;
+                    S.p_deg[nxt][pi] = dg;
+                } else {
+                    S.spill = 1;
+                }
             }
-            if (rest) {  // pi < cnt <= F
-                S.p_sd[nxt][pi] = (uint16_t)sd;
-                S.p_begin[nxt][pi] = S.p_begin[cur][i];
-                S.p_deg[nxt][pi] = S.p_deg[cur][i];
-            }
-        }
-        __syncthreads();
-        const uint32_t ne = S.n_e;
-        for (uint32_t base = 0; base < ne; base += BT) {
-            uint32_t k = ne - base < (uint32_t)BT ? ne - base : (uint32_t)BT;
-            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, base, k, nxt, edges);
+            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, take ? dg : 0, k, S.p_sd[cur] + base,
+                                            S.p_begin[cur] + base, nxt, edges);
             __syncthreads();
+        }
+        if (stamp) {
+            unsigned long long tp2 = __builtin_amdgcn_s_memtime();
+            stamp[8] += tp1 - tp0;
+            stamp[11] += tp2 - tp1;
         }
         cur = nxt;
     }
@@ -1238,21 +1294,23 @@ template <int U, int HLOG, int F, int BT, int LF>
 __global__ __launch_bounds__(BT) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                   const uint32_t *roots, const uint32_t *targets, uint64_t n,
                                                   uint64_t *allowed, const uint32_t *parents,
-                                                  const unsigned int *in_count, uint32_t *spill_out,
+                                                  const unsigned int *in_count, uint32_t fan, uint32_t *spill_out,
                                                   unsigned int *spill_count, unsigned long long *stats,
                                                   unsigned long long *stamps) {
     __shared__ BidiShared<U, HLOG, F, BT, LF> S;
     if (!in_count) {
         unsigned long long *stamp =
-            (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 8 : nullptr;
+            (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
         bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed,
                                       parents ? parents[blockIdx.x] : blockIdx.x, spill_out, spill_count, stats, stamp);
         return;
     }
-    const unsigned cnt = *in_count;
-    for (unsigned b = blockIdx.x; b < cnt; b += gridDim.x) {
-        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed, parents[b], spill_out, spill_count,
-                                      stats, nullptr);
+    // persistent: every listed unit of the previous stage splits into `fan` units of U
+    const uint64_t cnt = (uint64_t)*in_count * fan;
+    for (uint64_t b = blockIdx.x; b < cnt; b += gridDim.x) {
+        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed,
+                                      (uint64_t)parents[b / fan] * fan + b % fan, spill_out, spill_count, stats,
+                                      nullptr);
         __syncthreads();
     }
 }
@@ -1664,12 +1722,12 @@ struct ketogpu_engine {
     bool use_v2 = true;
     bool use_bidi = true;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
-    // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run with kBidiWide
+    // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run with bidi_wide
     struct BidiCfg {
         int hlog, bt, f, lf;
         bool operator==(const BidiCfg &o) const { return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf; }
     };
-    static constexpr BidiCfg kBidiWide{11, 256, 384, 6};
+    BidiCfg bidi_wide{11, 256, 384, 6};  // KETOGPU_BIDI_WIDE: the spill stage
     BidiCfg bidi_cfg{9, 64, 128, 7};
 
     void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
@@ -1678,12 +1736,13 @@ struct ketogpu_engine {
 #define KETO_BIDI(HL, F, BT, LF)                                                                                  \
     if (c == BidiCfg{HL, BT, F, LF}) {                                                                           \
         KLAUNCH((bidi_kernel<16, HL, F, BT, LF>), dim3(grid), dim3(BT), pad, stream, g, frec, brec,   \
-                           q.roots, q.targets, q.n, q.allowed, parents, in_count, out, out_count, stats, stp);   \
+                           q.roots, q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp); \
         return;                                                                                                  \
     }
         KETO_BIDI(11, 384, 256, 6)
         KETO_BIDI(10, 256, 256, 6)
         KETO_BIDI(10, 256, 64, 6)
+        KETO_BIDI(10, 256, 64, 7)
         KETO_BIDI(9, 192, 64, 6)
         KETO_BIDI(9, 128, 64, 6)
         KETO_BIDI(9, 192, 64, 7)
@@ -1698,14 +1757,15 @@ struct ketogpu_engine {
     unsigned lds_pad = 0;  // KETOGPU_LDS_PAD: extra dynamic LDS per workgroup (occupancy experiments)
 
     void report_stamps() {
-        std::vector<unsigned long long> h((size_t)65536 * 8);
+        std::vector<unsigned long long> h((size_t)65536 * 16);
         HIP_CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
-        double ph[4] = {0, 0, 0, 0}, lv = 0, used = 0;
+        double ph[4] = {0, 0, 0, 0}, lv = 0, used = 0, lp[4] = {0, 0, 0, 0};
         std::vector<double> tot;
         for (size_t b = 0; b < 65536; b++) {
-            const unsigned long long *s = &h[b * 8];
+            const unsigned long long *s = &h[b * 16];
             if (s[7] != 1) continue;
             for (int k = 0; k < 4; k++) ph[k] += (double)(s[k + 1] - s[k]);
+            for (int k = 0; k < 4; k++) lp[k] += (double)s[8 + k];
             lv += (double)s[5];
             used += (double)s[6];
             tot.push_back((double)(s[4] - s[0]));
@@ -1718,6 +1778,9 @@ struct ketogpu_engine {
                 "p99 %.0f max %.0f | levels %.2f slots %.0f\n",
                 tot.size(), ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, tot[tot.size() / 2], tot[tot.size() * 9 / 10],
                 tot[tot.size() * 99 / 100], tot.back(), lv / n, used / n);
+        if (lp[0] + lp[1] + lp[2] + lp[3] > 0)
+            fprintf(stderr, "[stamps] bidi level phases per unit: select %.0f (unused %.0f %.0f) expand %.0f\n",
+                    lp[0] / n, lp[1] / n, lp[2] / n, lp[3] / n);
         HIP_CHECK(hipMemset(stamps, 0, h.size() * 8));
     }
     // spill batch buffers (grown on demand)
@@ -1777,10 +1840,14 @@ struct ketogpu_engine {
             BidiCfg c = bidi_cfg;
             if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_cfg = c;
         }
+        if (const char *bc = getenv("KETOGPU_BIDI_WIDE")) {
+            BidiCfg c = bidi_wide;
+            if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_wide = c;
+        }
         if (getenv("KETOGPU_STAMPS")) {
-            stamps = dalloc<unsigned long long>((size_t)65536 * 8);
+            stamps = dalloc<unsigned long long>((size_t)65536 * 16);
             owned.push_back(stamps);
-            HIP_CHECK(hipMemset(stamps, 0, (size_t)65536 * 8 * 8));
+            HIP_CHECK(hipMemset(stamps, 0, (size_t)65536 * 16 * 8));
         }
         auto up = [&](auto &vec) {
             auto *p = dupload(vec);
@@ -1938,41 +2005,53 @@ struct ketogpu_engine {
         uint64_t units = (q.n + 15) / 16;
         uint64_t left = 0;
         if (use_v2) {
-            // Stage list.  With bidi: bidi (configured shape) over every unit, then bidi with
-            // the wide table PERSISTENT over stage 0's spills (their count is read on the
-            // device), statistics of the two stages in separate regions, and one host
-            // synchronization for counts and statistics.  Whatever still spills (rare) runs
-            // the host-driven unit2 cascade: unit2<16> -> unit2<4> -> unit2<1> -> global path.
-            uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
+            // Forward-only plan "v2": the host-driven unit2 cascade unit2<16> -> unit2<4> ->
+            // unit2<1> -> global path.
             if (use_bidi) {
-                const bool wide = !(bidi_cfg == kBidiWide);
-                hipEvent_t a = ev(), b = ev(), c = ev();
+                // bidi (configured shape) -> bidi with the wide table (persistent over the
+                // spilled units) -> single-request bidi with an 8192-slot table (one
+                // workgroup per CU, persistent over the wide stage's spills split 16 ways)
+                // -> global path; one host synchronization for counts and statistics
+                const bool wide = !(bidi_cfg == bidi_wide);
+                hipEvent_t a = ev(), b = ev(), c = ev(), d = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
                 launch_bidi(bidi_cfg, (unsigned)units, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                             st.stats, stamps);
                 HIP_CHECK(hipEventRecord(b, stream));
-                if (wide)
-                    launch_bidi(kBidiWide, (unsigned)std::min<uint64_t>(units, 1024), 0, q, list[0], &spill_count[0],
-                                list[1], &spill_count[1], st.stats + 4 * kStatSlots, nullptr);
+                uint32_t *l16 = list[0];
+                unsigned int *c16 = &spill_count[0];
+                if (wide) {
+                    launch_bidi(bidi_wide, (unsigned)std::min<uint64_t>(units, bidi_wide.bt == 64 ? 2048 : 1024), 0, q,
+                                list[0], &spill_count[0], list[1], &spill_count[1], st.stats + 4 * kStatSlots,
+                                nullptr);
+                    l16 = list[1];
+                    c16 = &spill_count[1];
+                }
                 HIP_CHECK(hipEventRecord(c, stream));
-                KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2,
-                                   stat_out());
+                uint32_t *l1 = l16 == list[0] ? list[1] : list[0];
+                KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(256), dim3(256), 0, stream, g, frec, brec, q.roots,
+                        q.targets, q.n, q.allowed, l16, c16, 16u, l1, &spill_count[2], st.stats + 4 * kStatSlots,
+                        nullptr);
+                HIP_CHECK(hipEventRecord(d, stream));
+                KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
                 HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost,
                                          stream));
                 HIP_CHECK(hipStreamSynchronize(stream));
                 unit_ev.push_back({a, b});
-                if (wide) unit_ev.push_back({b, c});
+                unit_ev.push_back({b, d});
                 const uint64_t *t = (const uint64_t *)h_ctr + 16;
                 rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
                 const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
-                rs.spilled_units += cnt[0] + (wide ? cnt[1] : 0);
-                rs.push_launches += wide ? 2 : 1;
-                rs.unit_launches += wide ? 2 : 1;
-                left = wide ? cnt[1] : cnt[0];
-                from = wide ? list[1] : list[0];
-                if (!left) return 0;
+                rs.spilled_units += cnt[0] + (wide ? cnt[1] : 0) + cnt[2];
+                rs.push_launches += wide ? 3 : 2;
+                rs.unit_launches += wide ? 3 : 2;
+                left = cnt[2];  // single requests for the global path
+                if (left && l1 != list[0])
+                    HIP_CHECK(hipMemcpyAsync(list[0], l1, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+                return left;
             }
+            uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
             struct Stage {
                 int u;
                 uint32_t fan;

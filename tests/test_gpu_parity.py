@@ -1,6 +1,8 @@
 """GPU parity: the MI355X engine (libketogpu.so, device_engine.hip) against the CPU
 oracle (reference DFS restated) and the golden reference assertions.  Bit-exact:
 every request's allowed bit must equal the oracle's."""
+import os
+
 import numpy as np
 import pytest
 
@@ -94,24 +96,53 @@ def test_global_path_matches_oracle(seed, collide, global_path):
 
 
 def test_unit_spill_to_global_path():
-    # a group whose closure (6000 interior groups) cannot fit a unit's LDS table
+    # both sides of the search are n nodes wide: top has n child groups g_i, the target
+    # group T is a member of n groups p_i, and only g_7 -> p_7 connects them, so
+    # no LDS table holds either side and requests fall through the whole cascade (bidi ->
+    # wide bidi -> unit2 -> global path)
+    # (g_i expand into u_i and p_i are members of z, so both families are interior nodes);
+    # 9000 per side also exceeds the single-request stage's 8192-slot table
+    n = 9000
+    rows = [(1, "top", "m", None, 1, f"g{i:05d}", "m") for i in range(n)]
+    rows += [(1, f"g{i:05d}", "m", f"u{i}", None, None, None) for i in range(n)]
+    rows += [(1, f"p{i:05d}", "m", None, 1, "T", "m") for i in range(n)]
+    rows += [(1, "z", "m", None, 1, f"p{i:05d}", "m") for i in range(n)]
+    rows += [(1, "g00007", "m", None, 1, "p00007", "m")]
+    rows += [(1, f"q{i:05d}", "m", None, 1, "T", "m") for i in range(3)]  # T also below q_i only
+    snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
+    eng = check.Engine(snap)
+    reqs = [rt.InternalRelationTuple("n", "top", "m", rt.SubjectSet("n", "T", "m")),
+            rt.InternalRelationTuple("n", "top", "m", rt.SubjectID("u8")),
+            rt.InternalRelationTuple("n", "g00009", "m", rt.SubjectSet("n", "T", "m")),  # g_9 -> u9 only
+            rt.InternalRelationTuple("n", "q00001", "m", rt.SubjectSet("n", "T", "m")),
+            rt.InternalRelationTuple("n", "p00003", "m", rt.SubjectSet("n", "T", "m"))] * 40
+    got = eng.check_many(reqs)
+    assert got == [True, True, False, True, True] * 40
+    st = eng.last_stats()
+    assert st["spilled_units"] > 0 and st["ms_unit"] > 0
+    assert st["spilled_requests"] > 0  # n-wide sides exceed even a single request's table
+
+
+def test_large_forward_closure_small_backward_side():
+    # a 6000-group forward closure with a 1-entry backward side: bidi expands the backward
+    # side and looks the root's row up, so nothing spills; the forward-only plan spills
     rows = [(1, "top", "m", None, 1, f"g{i:05d}", "m") for i in range(6000)]
     rows += [(1, f"g{i:05d}", "m", f"u{i}", None, None, None) for i in range(6000)]
     rows += [(1, "small", "m", None, 1, "g00007", "m")]
     snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
-    eng = check.Engine(snap)
-    reqs = []
+    reqs, want = [], []
     for i in range(0, 6000, 97):
         reqs.append(rt.InternalRelationTuple("n", "top", "m", rt.SubjectID(f"u{i}")))
         reqs.append(rt.InternalRelationTuple("n", "small", "m", rt.SubjectID(f"u{i}")))
-    got = eng.check_many(reqs)
-    want = []
-    for i in range(0, 6000, 97):
         want += [True, i == 7]
-    assert got == want
-    st = eng.last_stats()
-    assert st["spilled_units"] > 0 and st["ms_unit"] > 0
-    assert st["spilled_requests"] > 0  # a 6000-group closure exceeds even a single request's table
+    assert check.Engine(snap).check_many(reqs) == want
+    os.environ["KETOGPU_UNITS"] = "v2"
+    try:
+        eng = check.Engine(snap)
+    finally:
+        del os.environ["KETOGPU_UNITS"]
+    assert eng.check_many(reqs) == want
+    assert eng.last_stats()["spilled_requests"] > 0
 
 
 def test_check_ids_and_device_queries_match_oracle():

@@ -1,0 +1,113 @@
+"""Large-graph runs of the single-GPU engine (BASELINE.json north star: >= 10^8 checks/s on
+one MI355X for a 1B-tuple RBAC / folder graph).  Not the bench.py metric line: the
+graph is generated and snapshotted on the host (minutes at 1B tuples), then 1M
+HBM-resident requests are timed exactly as bench.py times them.
+
+    python tools/bench_scale.py --workload rbac --tuples 1000000000
+    python tools/bench_scale.py --workload folders --tuples 500000000
+    python tools/bench_scale.py --workload social --tuples 1000000000
+
+The CPU oracle cannot hold these graphs next to the engine, so correctness is checked by
+(1) every constructed positive must be allowed and (2) a 100k-request sample must agree
+bit-for-bit with a second engine on the same snapshot that uses the forward-only unit2
+kernels (a different algorithm: closure + reverse pull instead of bidirectional meet).
+A heartbeat line every 30 s keeps long host phases visibly alive.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import torch  # noqa: F401  (one HIP runtime in the process)
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from keto_amd import check, synth  # noqa: E402
+from keto_amd.snapshot import Snapshot  # noqa: E402
+
+T0 = time.time()
+PHASE = ["start"]
+
+
+def log(msg):
+    print(f"[scale {time.time() - T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def heartbeat():
+    while True:
+        time.sleep(30)
+        log(f"... {PHASE[0]}")
+
+
+def make(kind, tuples, checks):
+    f = tuples / {"rbac": 50e6, "folders": 500e6, "social": 1e9}[kind]
+    if kind == "rbac":  # config #2 shape scaled: users, groups, docs grow with the tuple count
+        return synth.rbac(users=int(10e6 * f), groups=int(100e3 * f), docs=int(2e6 * f), tuples=tuples, checks=checks,
+                          check_seed=synth.SEED + 1)
+    if kind == "folders":
+        return synth.folders(users=int(10e6 * f), groups=int(100e3 * f), folders=int(20e6 * f), tuples=tuples,
+                             checks=checks, check_seed=synth.SEED + 1)
+    return synth.social(users=int(100e6 * f), groups=int(10e6 * f), tuples=tuples, checks=checks,
+                        check_seed=synth.SEED + 1)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--workload", choices=["rbac", "folders", "social"], default="rbac")
+    p.add_argument("--tuples", type=int, default=1_000_000_000)
+    p.add_argument("--checks", type=int, default=1_000_000)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--sample", type=int, default=100_000)
+    a = p.parse_args()
+    threading.Thread(target=heartbeat, daemon=True).start()
+    PHASE[0] = "generating"
+    w = make(a.workload, a.tuples, a.checks)
+    t_gen = time.time() - T0
+    log(f"generated {w.counts}")
+    PHASE[0] = "building the snapshot"
+    t0 = time.time()
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    t_snap = time.time() - t0
+    st = snap.stats()
+    log(f"snapshot in {t_snap:.1f}s: {st}")
+    roots, targets = w.resolve(snap)
+    pos = w.chk_pos.astype(bool)
+    del w  # the rows are no longer needed
+    PHASE[0] = "uploading the device graph"
+    t0 = time.time()
+    eng = check.Engine(snap)
+    t_up = time.time() - t0
+    q = eng.upload(roots, targets)
+    PHASE[0] = "timing"
+    for _ in range(a.warmup):
+        q.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        q.run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rs = eng.last_stats()
+    got = q.download()
+    PHASE[0] = "cross-checking"
+    os.environ["KETOGPU_UNITS"] = "v2"
+    ref_eng = check.Engine(snap)
+    idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
+    ref = ref_eng.check_ids(roots[idx], targets[idx])
+    out = {"workload": f"{a.workload}_{a.tuples}", "checks": len(roots), "checks_per_s": round(len(roots) * a.steps / dt, 1),
+           "ms_per_step": round(dt / a.steps * 1e3, 4), "main_kernel_ms": round(rs["main_ms"], 4),
+           "main_bytes": rs["main_bytes"], "spilled_units": rs["spilled_units"],
+           "spilled_requests": rs["spilled_requests"], "allowed_fraction": round(float(got.mean()), 4),
+           "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
+           "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
+                           "against": "forward-only unit2 engine, same snapshot"},
+           "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
+           "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

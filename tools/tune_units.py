@@ -14,8 +14,14 @@ from keto_amd.snapshot import Snapshot  # noqa: E402
 
 small = "--small" in sys.argv
 scale = 100 if small else 1
-w = synth.rbac(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
-               tuples=50_000_000 // scale, checks=1_000_000)
+workload = next((a.split("=")[1] for a in sys.argv if a.startswith("--workload=")), "rbac")
+if workload == "folders":  # config #3 shape at 5M tuples
+    w = synth.folders(users=100_000, groups=1_000, folders=200_000, tuples=5_000_000, checks=1_000_000)
+elif workload == "social":  # config #4 shape at 5M tuples
+    w = synth.social(users=500_000, groups=50_000, tuples=5_000_000, checks=1_000_000)
+else:
+    w = synth.rbac(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
+                   tuples=50_000_000 // scale, checks=1_000_000)
 snap = Snapshot.from_columns(w.namespaces, w.columns)
 roots, targets = w.resolve(snap)
 plans = [p for p in sys.argv[1:] if not p.startswith("--")] or ["w4", "w8", "w16", "b16", "global"]
@@ -23,11 +29,17 @@ engines, queries = {}, {}
 for p in plans:
     if p == "global":
         os.environ["KETOGPU_PATH"] = "global"
-    else:  # plan[:hlog,threads], e.g. bidi:9,64
+    else:  # plan[:first[/wide]], e.g. bidi:9,64,128,7/10,64,256,7
         os.environ.pop("KETOGPU_PATH", None)
+        os.environ.pop("KETOGPU_BIDI", None)
+        os.environ.pop("KETOGPU_BIDI_WIDE", None)
         os.environ["KETOGPU_UNITS"] = p.split(":")[0]
         if ":" in p:
-            os.environ["KETOGPU_BIDI"] = p.split(":")[1]
+            first, _, wide = p.split(":")[1].partition("/")
+            if first:
+                os.environ["KETOGPU_BIDI"] = first
+            if wide:
+                os.environ["KETOGPU_BIDI_WIDE"] = wide
     engines[p] = check.Engine(snap, state_budget_bytes=16 << 30)
     queries[p] = engines[p].upload(roots, targets)
 ref = None
