@@ -119,6 +119,12 @@ void ketogpu_builder_free(ketogpu_builder *b);
 void ketogpu_snapshot_free(ketogpu_snapshot *s);
 int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats *out);
 
+/* Persisted snapshots (fast restart): a versioned binary image of
+ * a finished snapshot.  Loading rebuilds only the derived indexes; a file written by a
+ * different format version is refused with KETOGPU_EINVAL. */
+int ketogpu_snapshot_save(const ketogpu_snapshot *s, const char *path);
+int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out);
+
 /* Read-only view of the device graph as built on the host (for tools and tests; the
  * pointers live as long as the snapshot).  Node ids: [0, num_interior) interior,
  * [num_interior, num_expandable) other expandable nodes, the rest never expand. */

@@ -130,6 +130,8 @@ SIGNATURES = {
     "ketogpu_snapshot_free": (None, [vp]),
     "ketogpu_snapshot_stats_get": (C.c_int, [vp, C.POINTER(SnapshotStats)]),
     "ketogpu_snapshot_graph": (C.c_int, [vp, C.POINTER(GraphView)]),
+    "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),
+    "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
     "ketogpu_resolve": (C.c_int, [vp, C.POINTER(CheckRequest), C.POINTER(u32), C.POINTER(u32)]),
     "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
     "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),

@@ -89,6 +89,22 @@ class Snapshot:
         s.append(cols)
         return s.finish()
 
+    # ---- persistence (ketogpu_snapshot_save / _load)
+    def save(self, path):
+        L.check(self.L.ketogpu_snapshot_save(self.h, str(path).encode()))
+
+    @classmethod
+    def load(cls, path, namespaces=None):
+        """a snapshot written by save(); `namespaces` only labels the Python object"""
+        s = cls.__new__(cls)
+        s.L = L.lib()
+        s.namespaces = list(namespaces or [])
+        s._builder = None
+        h = C.c_void_p()
+        L.check(s.L.ketogpu_snapshot_load(str(path).encode(), C.byref(h)))
+        s.h = h
+        return s
+
     # ---- queries
     def stats(self):
         st = L.SnapshotStats()

@@ -194,3 +194,17 @@ def test_synthetic_configs_match_oracle(kind, unit_plan):
     want = orc.check_batch(w.requests(range(len(roots))), nthreads=8)
     np.testing.assert_array_equal(got, want)
     assert 0.3 < got.mean() < 0.9
+
+
+def test_loaded_snapshot_answers_identically(tmp_path):
+    from keto_amd import synth
+    w = synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=5000, seed=11)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    snap.save(tmp_path / "rbac.snap")
+    back = Snapshot.load(tmp_path / "rbac.snap", w.namespaces)
+    roots, targets = w.resolve(snap)
+    r2, t2 = w.resolve(back)
+    np.testing.assert_array_equal(roots, r2)
+    np.testing.assert_array_equal(targets, t2)
+    np.testing.assert_array_equal(check.Engine(back).check_ids(roots, targets),
+                                  check.Engine(snap).check_ids(roots, targets))

@@ -160,3 +160,53 @@ def test_snapshot_stats_and_classes():
     for v in range(g["Nx"]):
         row = fc[fo[v]:fo[v + 1]]
         assert np.all(row < g["Ni"]) and np.all(np.diff(row.astype(np.int64)) > 0)
+
+
+@pytest.mark.parametrize("seed,collide", [(91, False), (92, True)])
+def test_snapshot_save_load_round_trip(tmp_path, seed, collide):
+    namespaces, rows = randgraph.make_graph(seed, n_rows=400, poison=True, collide=collide, empty_ns=True)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=3, sort=True)
+    path = tmp_path / "snap.bin"
+    snap.save(path)
+    back = Snapshot.load(path, namespaces)
+    assert back.stats() == snap.stats()
+    g0, g1 = snap.graph(), back.graph()
+    for k in ("fint_off", "fint_col", "rev_off", "rev_col"):
+        np.testing.assert_array_equal(g0[k], g1[k])
+    reqs = randgraph.make_requests(seed, namespaces, rows, n=200)
+    for ns, o, r, subj in reqs:
+        try:
+            a = snap.resolve(ns, o, r, rt.subject_from_dict(subj))
+        except L.KetoError as e:
+            a = e.code
+        try:
+            b = back.resolve(ns, o, r, rt.subject_from_dict(subj))
+        except L.KetoError as e:
+            b = e.code
+        assert a == b
+    e0, e1 = expand.Engine(snap), expand.Engine(back)
+    for ns, o, r, subj in reqs[:60]:
+        s = rt.SubjectSet(ns, o, r)
+        try:
+            want = e0.build_tree_json(s, 4)
+        except expand.NotFound:
+            want = "not_found"
+        try:
+            got = e1.build_tree_json(s, 4)
+        except expand.NotFound:
+            got = "not_found"
+        assert got == want
+
+
+def test_snapshot_load_rejects_foreign_files(tmp_path):
+    p = tmp_path / "junk.bin"
+    p.write_bytes(b"not a snapshot at all")
+    with pytest.raises(L.KetoError) as e:
+        Snapshot.load(p)
+    assert e.value.code == L.EINVAL
+    snap = Snapshot.from_rows([("n", 1)], [(1, "o", "r", "u", None, None, None)])
+    snap.save(tmp_path / "ok.bin")
+    data = (tmp_path / "ok.bin").read_bytes()
+    (tmp_path / "cut.bin").write_bytes(data[:len(data) // 2])
+    with pytest.raises(L.KetoError):
+        Snapshot.load(tmp_path / "cut.bin")
