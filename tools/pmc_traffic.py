@@ -24,6 +24,7 @@ from collections import defaultdict
 FAMILIES = [
     ("bidi_kernel<16>", r"bidi_kernel<16, (9|10), "),
     ("bidi wide-table spill stage", r"bidi_kernel<16, 11, "),
+    ("bidi single-request stage", r"bidi_kernel<1, 13, "),
     ("unit2_kernel<16>", r"unit2_kernel<16>"),
     ("unit2_kernel<4>+<1> (spill passes)", r"unit2_kernel<(4|1)>"),
     ("unit_kernel", r"[^2]unit_kernel<"),
