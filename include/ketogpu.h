@@ -119,6 +119,15 @@ void ketogpu_builder_free(ketogpu_builder *b);
 void ketogpu_snapshot_free(ketogpu_snapshot *s);
 int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats *out);
 
+/* Write-path freshness (R14): the next snapshot version = the base's
+ * rows with one TransactRelationTuples batch applied (internal/persistence/sql/
+ * relationtuples.go:271-278): inserts join their group after equal rows (commit_time
+ * order), then every row matching a delete is removed (:178-201).  Row order follows
+ * the SQLite semantics of KETOGPU_BUILD_SORT.  The base stays valid; engines built on
+ * the new version answer with the write applied.  inserts/deletes may be NULL. */
+int ketogpu_snapshot_apply(const ketogpu_snapshot *base, const ketogpu_row_batch *inserts,
+                           const ketogpu_row_batch *deletes, ketogpu_snapshot **out);
+
 /* Persisted snapshots (fast restart): a versioned binary image of
  * a finished snapshot.  Loading rebuilds only the derived indexes; a file written by a
  * different format version is refused with KETOGPU_EINVAL. */

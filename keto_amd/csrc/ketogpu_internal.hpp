@@ -102,6 +102,15 @@ struct Namespace {
     std::string name;
 };
 
+// One keto_relation_tuples row with interned strings (StrPool ids); kind 0 = subject id
+// row (sid), 1 = subject-set row (ss_*).  seq orders equal keys (commit_time).
+struct TupleRow {
+    int32_t ns, ss_ns;
+    uint32_t obj, rel, sid, ss_obj, ss_rel;
+    uint8_t kind;
+    uint64_t seq;
+};
+
 // One (namespace_id, object, relation) group of rows, in DB order.
 struct Group {
     int32_t ns;
@@ -110,6 +119,7 @@ struct Group {
     uint32_t valid;          // rows before the first bad row
     uint32_t full_len;       // all rows of the group
     int64_t first_bad;       // index of the first row with an unknown namespace, or -1
+    uint64_t tail;           // into Snapshot::tail_rows: rows [first_bad, full_len) (kept for updates)
 };
 
 // Query result of one subject set / root query after page-poison truncation.
@@ -131,6 +141,7 @@ struct Snapshot {
     StrPool pool;
     std::vector<Group> groups;          // DB order
     std::vector<uint32_t> group_col;    // subjects (node ids) of the groups' valid prefixes
+    std::vector<TupleRow> tail_rows;    // rows from each group's first bad row on
 
     // ---- nodes: [0, Ni) interior, [Ni, Nx) source-expandable, [Nx, N) non-expandable
     uint32_t N = 0, Ni = 0, Nx = 0;

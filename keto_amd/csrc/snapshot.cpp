@@ -169,12 +169,7 @@ struct ketogpu_builder {
     std::string cur_obj, cur_rel;  // raw bytes of the open group (fast path)
     TripleMap seen_groups;         // detects rows that are not grouped
     // KETOGPU_BUILD_SORT: rows buffered as interned ids
-    struct RawRow {
-        int32_t ns, ss_ns;
-        uint32_t obj, rel, sid, ss_obj, ss_rel;
-        uint8_t kind;
-        uint64_t seq;
-    };
+    using RawRow = TupleRow;
     std::vector<RawRow> raw;
     uint64_t rows = 0, bad_rows = 0;
     std::vector<uint8_t> ns_known_dense;  // namespace ids in [0, 65536) fast path
@@ -219,7 +214,7 @@ struct ketogpu_builder {
                         "rows are not in ORDER BY order: group (namespace_id, object, relation) "
                         "appears twice (use KETOGPU_BUILD_SORT)");
         seen_groups.get_or_insert(ns, obj, rel, (uint32_t)s->groups.size());
-        cur = Group{ns, obj, rel, s->group_col.size(), 0, 0, -1};
+        cur = Group{ns, obj, rel, s->group_col.size(), 0, 0, -1, 0};
         open = true;
     }
     // one row, already grouped
@@ -233,14 +228,16 @@ struct ketogpu_builder {
         // toInternal fails for unknown namespace ids (relationtuples.go:48-51,64-67)
         bool bad = !ns_known(ns) || (kind && !ns_known(ss_ns));
         if (bad) bad_rows++;
+        if (cur.first_bad < 0 && bad) {
+            cur.first_bad = cur.full_len;
+            cur.tail = s->tail_rows.size();
+        }
         if (cur.first_bad < 0) {
-            if (bad) {
-                cur.first_bad = cur.full_len;
-            } else {
-                uint32_t v = kind ? set_node(ss_ns, ss_obj, ss_rel) : id_node(sid);
-                s->group_col.push_back(v);
-                cur.valid++;
-            }
+            uint32_t v = kind ? set_node(ss_ns, ss_obj, ss_rel) : id_node(sid);
+            s->group_col.push_back(v);
+            cur.valid++;
+        } else {  // invisible to check/expand past the poisoned page, kept for updates
+            s->tail_rows.push_back(TupleRow{ns, ss_ns, obj, rel, sid, ss_obj, ss_rel, kind, 0});
         }
         cur.full_len++;
     }
@@ -587,6 +584,116 @@ int ketogpu_builder_finish(ketogpu_builder *b, ketogpu_snapshot **out) {
 }
 
 void ketogpu_builder_free(ketogpu_builder *b) { delete b; }
+
+// Write-path freshness (R14).  The next snapshot version is the
+// base's rows with a TransactRelationTuples batch applied (relationtuples.go:271-278):
+// inserted rows join their group after equal rows (commit_time is the last ORDER BY key,
+// :215; InsertRelationTuple stamps time.Now(), :128-149), then every row matching a
+// delete (namespace id, object, relation, subject) is removed, duplicates included
+// (DeleteRelationTuples, :178-201).  The merge uses the SQLite ORDER BY semantics of
+// KETOGPU_BUILD_SORT; a base read in another backend's order fails loudly (EINVAL) when
+// the merged stream is not grouped.  O(rows) on the host: the new version is complete
+// and immutable, and engines swap to it (keto_amd/freshness.py).
+int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batch *inserts,
+                           const ketogpu_row_batch *deletes, ketogpu_snapshot **out) {
+    try {
+        if (!basep || !out) throw Error(KETOGPU_EINVAL, "null argument");
+        *out = nullptr;
+        const Snapshot &B = *reinterpret_cast<const Snapshot *>(basep);
+        std::vector<ketogpu_namespace> nss;
+        for (const Namespace &n : B.namespaces) nss.push_back(ketogpu_namespace{n.id, n.name.c_str()});
+        ketogpu_build_opts opts{B.page_size, 0};
+        ketogpu_builder *raw_b = nullptr;
+        int rc = ketogpu_builder_new(nss.data(), nss.size(), &opts, &raw_b);
+        if (rc) return rc;
+        std::unique_ptr<ketogpu_builder> b(raw_b);
+        Snapshot &S = *b->s;
+        for (size_t i = 1; i < B.pool.size(); i++) {  // same string ids as the base
+            std::string_view x = B.pool.get((uint32_t)i);
+            S.pool.intern(x.data(), x.size());
+        }
+        // the write batch as rows of the new pool (same parsing as builder_append)
+        auto rows_of = [&](const ketogpu_row_batch *r, uint64_t seq0) {
+            std::vector<TupleRow> v;
+            if (!r || !r->n) return v;
+            if (!r->namespace_id || !r->object_off || !r->relation_off || !r->subject_kind)
+                throw Error(KETOGPU_EINVAL, "row batch misses a required column");
+            for (size_t i = 0; i < r->n; i++) {
+                std::string_view obj = col(r->object_data, r->object_off, i), rel = col(r->relation_data, r->relation_off, i);
+                TupleRow t{r->namespace_id[i], 0, S.pool.intern(obj.data(), obj.size()),
+                           S.pool.intern(rel.data(), rel.size()), 0, 0, 0, (uint8_t)(r->subject_kind[i] ? 1 : 0),
+                           seq0 + i};
+                if (t.kind) {
+                    if (!r->ss_namespace_id || !r->ss_object_off || !r->ss_relation_off)
+                        throw Error(KETOGPU_EINVAL, "subject-set row without subject_set columns");
+                    std::string_view so = col(r->ss_object_data, r->ss_object_off, i);
+                    std::string_view sr = col(r->ss_relation_data, r->ss_relation_off, i);
+                    t.ss_ns = r->ss_namespace_id[i];
+                    t.ss_obj = S.pool.intern(so.data(), so.size());
+                    t.ss_rel = S.pool.intern(sr.data(), sr.size());
+                } else {
+                    if (!r->subject_id_off) throw Error(KETOGPU_EINVAL, "subject-id row without subject_id column");
+                    std::string_view si = col(r->subject_id_data, r->subject_id_off, i);
+                    t.sid = S.pool.intern(si.data(), si.size());
+                }
+                v.push_back(t);
+            }
+            return v;
+        };
+        SortCmp cmp{S.pool};
+        std::vector<TupleRow> ins = rows_of(inserts, 1ull << 62), del = rows_of(deletes, 0);
+        std::stable_sort(ins.begin(), ins.end(), cmp);
+        for (auto &d : del) d.seq = 0;  // a delete matches every commit_time
+        std::sort(del.begin(), del.end(), cmp);
+        auto same = [](const TupleRow &a, const TupleRow &c) {
+            return a.ns == c.ns && a.obj == c.obj && a.rel == c.rel && a.kind == c.kind &&
+                   (a.kind ? (a.ss_ns == c.ss_ns && a.ss_obj == c.ss_obj && a.ss_rel == c.ss_rel) : a.sid == c.sid);
+        };
+        auto deleted = [&](TupleRow r) {
+            r.seq = 0;
+            auto it = std::lower_bound(del.begin(), del.end(), r, cmp);
+            return it != del.end() && same(*it, r);
+        };
+        auto emit = [&](const TupleRow &r) {
+            if (!deleted(r)) b->add(r.ns, r.obj, r.rel, r.kind, r.sid, r.ss_ns, r.ss_obj, r.ss_rel);
+        };
+        size_t ii = 0;
+        uint64_t seq = 0;
+        for (const Group &g : B.groups) {
+            for (uint32_t k = 0; k < g.full_len; k++) {
+                TupleRow r;
+                if (g.first_bad < 0 || k < (uint32_t)g.first_bad) {
+                    const uint32_t v = B.group_col[g.begin + k];
+                    r = TupleRow{g.ns, 0, g.obj, g.rel, 0, 0, 0, B.node_kind[v], 0};
+                    if (r.kind == KETOGPU_SUBJECT_SET) {
+                        r.ss_ns = B.node_ns[v];
+                        r.ss_obj = B.node_a[v];
+                        r.ss_rel = B.node_b[v];
+                    } else {
+                        r.sid = B.node_a[v];
+                    }
+                } else {
+                    r = B.tail_rows[g.tail + (k - (uint32_t)g.first_bad)];
+                }
+                r.seq = seq++;
+                while (ii < ins.size() && cmp(ins[ii], r)) emit(ins[ii++]);
+                emit(r);
+            }
+        }
+        while (ii < ins.size()) emit(ins[ii++]);
+        ketogpu_snapshot *o = nullptr;
+        rc = ketogpu_builder_finish(b.release(), &o);
+        if (rc) return rc;
+        *out = o;
+    } catch (const Error &e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_last_error("out of host memory");
+        return KETOGPU_ENOMEM;
+    }
+    return KETOGPU_OK;
+}
 
 void ketogpu_snapshot_free(ketogpu_snapshot *s) { delete reinterpret_cast<Snapshot *>(s); }
 

@@ -17,7 +17,7 @@ using namespace ketogpu;
 namespace {
 
 constexpr char kMagic[8] = {'K', 'E', 'T', 'O', 'S', 'N', 'A', 'P'};
-constexpr uint32_t kFormat = 1;
+constexpr uint32_t kFormat = 2;
 
 struct File {
     FILE *f = nullptr;
@@ -104,6 +104,7 @@ int ketogpu_snapshot_save(const ketogpu_snapshot *sp, const char *path) {
         f.put_pool(s.pool);
         f.put_vec(s.groups);
         f.put_vec(s.group_col);
+        f.put_vec(s.tail_rows);
         f.put<uint32_t>(s.N);
         f.put<uint32_t>(s.Ni);
         f.put<uint32_t>(s.Nx);
@@ -161,6 +162,7 @@ int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out) {
         f.get_pool(s->pool);
         f.get_vec(s->groups);
         f.get_vec(s->group_col);
+        f.get_vec(s->tail_rows);
         s->N = f.get<uint32_t>();
         s->Ni = f.get<uint32_t>();
         s->Nx = f.get<uint32_t>();

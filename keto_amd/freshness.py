@@ -1,0 +1,77 @@
+"""Read-your-writes over immutable snapshots (R14).
+
+The reference reads the database on every check, so a check issued after a successful
+write sees it (internal/persistence/sql/relationtuples.go:271-278 then :203-258).  The
+GPU engines answer from an immutable device snapshot instead, so writes go through a
+VersionedEngine: `transact` applies the batch to the current snapshot
+(ketogpu_snapshot_apply: same ORDER BY, commit_time and delete-all-duplicates rules as
+the SQL write path), builds the engines of the new version and swaps them in before it
+returns the new version number.  Every check or expand issued after `transact` returned
+runs on a version that contains the write; a check in flight keeps the version it
+started on (the old engine lives until its last reference is dropped).  Unknown
+namespace names fail the whole transaction (GetNamespaceByName -> ErrNotFound), as in
+the reference.
+
+Cost: O(rows) host work plus one device-graph upload per transaction; batch writes (or
+coalesce them in a writer queue) on large graphs.  A device-side delta overlay that
+avoids the rebuild is the planned next step.
+"""
+import threading
+
+from . import check, expand, persistence
+from .relationtuple import InternalRelationTuple, NilSubject
+
+
+class VersionedEngine:
+    def __init__(self, snapshot, device=0, **engine_opts):
+        self.device = device
+        self.engine_opts = engine_opts
+        self._lock = threading.Lock()  # one writer at a time
+        self.version = 0
+        self._install(snapshot)
+
+    def _install(self, snapshot):
+        eng = check.Engine(snapshot, device=self.device, **self.engine_opts)
+        state = (snapshot, eng, expand.Engine(snapshot))
+        self._state = state  # one reference swap: readers see the old or the new version
+        return state
+
+    # ---------------------------------------------------------------- writes
+    def _rows(self, tuples):
+        rows = []
+        for t in tuples:
+            if isinstance(t, dict):
+                t = InternalRelationTuple.from_dict(t)
+            if t.subject is None:
+                raise NilSubject("subject is not allowed to be nil")
+            rows.extend(persistence.rows_from_tuples(self._state[0].namespaces, [t]))
+        return rows
+
+    def transact(self, insert=(), delete=()):
+        """TransactRelationTuples: insert, then delete; returns the new version"""
+        with self._lock:
+            snap = self._state[0]
+            new = snap.apply(self._rows(insert), self._rows(delete))
+            self._install(new)
+            self.version += 1
+            return self.version
+
+    def WriteRelationTuples(self, *tuples):
+        return self.transact(insert=tuples)
+
+    def DeleteRelationTuples(self, *tuples):
+        return self.transact(delete=tuples)
+
+    # ----------------------------------------------------------------- reads
+    @property
+    def snapshot(self):
+        return self._state[0]
+
+    def SubjectIsAllowed(self, t):
+        return self._state[1].SubjectIsAllowed(t)
+
+    def check_many(self, tuples):
+        return self._state[1].check_many(tuples)
+
+    def BuildTree(self, subject, rest_depth):
+        return self._state[2].BuildTree(subject, rest_depth)

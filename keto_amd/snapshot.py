@@ -89,6 +89,30 @@ class Snapshot:
         s.append(cols)
         return s.finish()
 
+    # ---- freshness (ketogpu_snapshot_apply)
+    def apply(self, insert_rows=(), delete_rows=()):
+        """the next version: raw rows (namespace_id, object, relation, subject_id|None, ss_ns,
+        ss_obj, ss_rel) inserted, then every row matching a delete removed"""
+        def batch(rows):
+            if not rows:
+                return None, None
+            cols = persistence.columnar(list(rows))
+            rb = L.RowBatch(len(rows), _ptr(cols["namespace_id"]), _ptr(cols["object_data"]), _ptr(cols["object_off"]),
+                            _ptr(cols["relation_data"]), _ptr(cols["relation_off"]), _ptr(cols["subject_kind"]),
+                            _ptr(cols["subject_id_data"]), _ptr(cols["subject_id_off"]),
+                            _ptr(cols["ss_namespace_id"]), _ptr(cols["ss_object_data"]), _ptr(cols["ss_object_off"]),
+                            _ptr(cols["ss_relation_data"]), _ptr(cols["ss_relation_off"]))
+            return rb, cols
+        ins, keep_i = batch(insert_rows)
+        dele, keep_d = batch(delete_rows)
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_snapshot_apply(self.h, C.byref(ins) if ins else None, C.byref(dele) if dele else None,
+                                              C.byref(h)))
+        del keep_i, keep_d
+        s = Snapshot.__new__(Snapshot)
+        s.L, s.namespaces, s._builder, s.h = self.L, list(self.namespaces), None, h
+        return s
+
     # ---- persistence (ketogpu_snapshot_save / _load)
     def save(self, path):
         L.check(self.L.ketogpu_snapshot_save(self.h, str(path).encode()))
@@ -118,8 +142,10 @@ class Snapshot:
         nx, n = v.num_expandable, v.num_nodes
         fo = np.ctypeslib.as_array(v.fint_off, (nx + 1,)).copy()
         ro = np.ctypeslib.as_array(v.rev_off, (n + 1,)).copy()
-        fc = np.ctypeslib.as_array(v.fint_col, (max(int(fo[-1]), 1),))[:int(fo[-1])].copy()
-        rc = np.ctypeslib.as_array(v.rev_col, (max(int(ro[-1]), 1),))[:int(ro[-1])].copy()
+        def col(ptr, n):  # an empty column may have no storage
+            return np.ctypeslib.as_array(ptr, (n,)).copy() if n else np.zeros(0, dtype=np.uint32)
+        fc = col(v.fint_col, int(fo[-1]))
+        rc = col(v.rev_col, int(ro[-1]))
         return {"N": n, "Nx": nx, "Ni": v.num_interior, "fint_off": fo, "fint_col": fc, "rev_off": ro, "rev_col": rc}
 
     def resolve(self, namespace, obj, relation, subject):
