@@ -167,8 +167,10 @@ def main():
                             for k, (b, ms, n) in fam.items() if ms > 0}}
         cpu = None
         parity = None
+        sql = None
         if not a.no_cpu_baseline:
             cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds)
+            sql = sql_baseline(min(10.0, a.cpu_seconds))
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
@@ -177,7 +179,7 @@ def main():
             "config": {"workload": "config2_rbac" + ("_small" if a.small else ""), **sizes,
                        "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
                        "parallelism": f"query-shard x{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total")},
             "allowed_fraction": round(float(allowed.mean()), 4),
@@ -240,6 +242,47 @@ def main_partitioned(a, rank, world, local):
         dist.destroy_process_group()
 
 
+def sql_baseline(seconds):
+    """the reference's storage access per check — every subject-set expansion
+    issues GetRelationTuples' COUNT + ORDER BY/LIMIT/OFFSET page queries (relationtuples.go:
+    203-258, persister.go:129-157) against SQLite with the reference's index — restated in
+    tests/sqlite_reference.py (Python, one thread), on a 1M-tuple graph of the config #2
+    generator (1/50 scale).  The cost regime of the reference, not the metric."""
+    from keto_amd import persistence, synth
+    from tests.sqlite_reference import SqliteReference
+    t0 = time.time()
+    w = synth.rbac(users=200_000, groups=2_000, docs=40_000, tuples=1_000_000, checks=20_000,
+                   check_seed=synth.SEED + 99)
+    c = w.columns
+
+    def strs(name):
+        data, off = c[name + "_data"].tobytes(), c[name + "_off"]
+        return [data[off[i]:off[i + 1]].decode() for i in range(len(off) - 1)]
+    obj, rel, sid, so, sr = (strs(k) for k in ("object", "relation", "subject_id", "ss_object", "ss_relation"))
+    store = persistence.TupleStore(w.namespaces)
+    kind, ns, ssns = c["subject_kind"], c["namespace_id"], c["ss_namespace_id"]
+    store.conn.executemany(
+        "INSERT INTO keto_relation_tuples (shard_id, nid, namespace_id, object, relation, subject_id, "
+        "subject_set_namespace_id, subject_set_object, subject_set_relation, commit_time) VALUES (?,?,?,?,?,?,?,?,?,?)",
+        ((str(i), store.nid, int(ns[i]), obj[i], rel[i], None if kind[i] else sid[i],
+          int(ssns[i]) if kind[i] else None, so[i] if kind[i] else None, sr[i] if kind[i] else None, i)
+         for i in range(len(ns))))
+    ref = SqliteReference(store)
+    t_load = time.time() - t0
+    done = 0
+    t0 = time.perf_counter()
+    for q in w.requests(range(w.n_checks)):
+        ref.check(q[0], q[1], q[2], ("id", q[3]["subject_id"]))
+        done += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 1), "unit": "checks/s", "cores": 1, "kind": "port-sql",
+            "sample": f"{done} checks of a 1M-tuple config-2-shaped graph; every expansion runs the reference's "
+                      f"COUNT + paged ORDER BY queries on in-memory SQLite (tests/sqlite_reference.py, Python); "
+                      f"load {t_load:.1f}s"}
+
+
 def cpu_baseline(w, gpu_allowed, seconds):
     """The oracle (exact restatement of the reference DFS) on host cores over a bounded
     sample of the same requests; its answers double as a bit-exact parity sample."""
@@ -263,8 +306,13 @@ def cpu_baseline(w, gpu_allowed, seconds):
     ans = orc.check_batch(w.requests(sample), nthreads=threads)
     ts = time.perf_counter() - t0
     mism = int((ans != gpu_allowed[sample]).sum())
+    one = idx[:max(200, m // threads)]  # the same work on one core
+    t0 = time.perf_counter()
+    orc.check_batch(w.requests(one), nthreads=1)
+    rate1 = len(one) / (time.perf_counter() - t0)
     del O
     return ({"value": round(len(sample) / ts, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+             "value_1_core": round(rate1, 1),
              "sample": f"{len(sample)} of the {w.n_checks} config-2 requests (uniform sample), full 50M-tuple graph; "
                        f"oracle/keto_oracle.c on {threads} threads of {cpu_model()}; store build {t_build:.1f}s"},
             {"sample": len(sample), "mismatches": mism})

@@ -1198,9 +1198,10 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const bool a = tid < U && ((act >> tid) & 1u);
             const uint32_t cf = a ? S.cost[0][tid] : 0, cb = a ? S.cost[1][tid] : 0;
             const int j = tid & 15;
-            const bool rp = a && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);  // fint(r) unread
-            const bool tp = a && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);  // rev(t) unread
             const bool fc = a && !cf, bc = a && !cb;
+            // seed rows still unread (only needed when a side is closed)
+            const bool rp = bc && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);
+            const bool tp = fc && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);
             const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
             const bool open = a && !closed;
             const bool lkb = open && fc, lkf = open && bc;
