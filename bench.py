@@ -95,6 +95,7 @@ def main():
     rank, world, local = dist_init(a.gpus)
     if a.mode == "partitioned":
         return main_partitioned(a, rank, world, local)
+    from keto_amd import _lib as L
     from keto_amd import check, synth
     from keto_amd.snapshot import Snapshot
 
@@ -116,6 +117,10 @@ def main():
     q = eng.upload(roots, targets)
     t_h2d = time.time() - t0
 
+    # plan selection (KETOGPU_UNITS=auto): the engine's first two large batches run
+    # both first stages and keep the faster; done here so the timed steps never do it
+    for _ in range(2):
+        q.run()
     for _ in range(a.warmup):
         q.run()
     barrier(world)
@@ -139,7 +144,7 @@ def main():
     out = None
     if rank == 0:
         # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time
-        plan = os.environ.get("KETOGPU_UNITS", "bidi")
+        plan = L.RunStats.PLANS.get(st["plan"], "unit")  # KETOGPU_UNITS=auto: the plan the engine kept
         main = {"bidi": "bidi_kernel<16>", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
         fam = {
             main: (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
@@ -180,6 +185,7 @@ def main():
                        "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
                        "parallelism": f"query-shard x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
+            "plan": plan,
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total")},
             "allowed_fraction": round(float(allowed.mean()), 4),

@@ -264,6 +264,12 @@ typedef struct {
     uint64_t unit_launches;     /* unit-kernel launches (cascade passes)          */
     uint64_t main_bytes;        /* algorithmic HBM bytes of the first unit pass   */
     double main_ms;             /* its device time (hipEvent)                     */
+    int32_t plan;               /* first stage of the run: 0 global path only, 1 bidi,
+                                 * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1.
+                                 * KETOGPU_UNITS=auto (default) tries bidi and v2 on the
+                                 * first two batches of >= 65536 requests, then keeps the
+                                 * faster; those two calls run both (same results)     */
+    uint32_t reserved;
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

@@ -909,6 +909,11 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // side, nothing inserted).  No depth cutoff (R2).  Used when the snapshot has no
 // ambiguous keys (R4 flags are raised by forward rows) and record begins fit u32;
 // dynamic roots and table/list overflow spill to the next stage.
+// Dead ends are looked up, not stored: a node with no interior predecessors is forward-
+// visited only as r or as an entry of r's own row, and a node with no interior successors
+// is backward-visited only as t or as an entry of t's own reverse row; so once the other
+// side's seed row has been read (in an earlier level: its inserts are complete), a push
+// of such a node only looks it up.  Leaf groups (only subject-ID members) take no slot.
 constexpr uint32_t kBothMax = 12;      // both sides expand while both pending sums are <= this
 constexpr uint32_t kSeedBothMax = 32;  // seeds pushed eagerly when both seed rows are <= this
 
@@ -933,6 +938,7 @@ struct BidiShared {
     uint32_t root[U];
     uint16_t rslot[U], tslot[U];  // table slots of the seeds r_j, t_j
     uint32_t sel[2], lookup[2];   // per direction: bits expanded this level / lookup-only bits
+    uint32_t sread[2];            // per direction: bits for which a push of a dead-end node is lookup-only
     uint32_t n_used, n_e, n_p[2], spill, found, active;
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
 };
@@ -1001,7 +1007,7 @@ __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert,
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, bool want, uint32_t u, uint32_t deg,
                                           uint32_t begin, uint32_t m, int d, int nxt) {
-    const uint32_t lk = m & S.lookup[d];
+    const uint32_t lk = m & (S.lookup[d] | (deg ? 0u : S.sread[d]));
     int h = -1;
     bool inserted = false;
     if (want) {
@@ -1106,7 +1112,10 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
     }
     if (tid < 2 * U) S.cost[tid / U][tid % U] = 0;
-    if (tid < 2) S.lookup[tid] = 0;
+    if (tid < 2) {
+        S.lookup[tid] = 0;
+        S.sread[tid] = 0;
+    }
     __syncthreads();
     uint64_t rows = 0, edges = 0;
     uint32_t n_levels = 0;
@@ -1200,8 +1209,10 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const int j = tid & 15;
             const bool fc = a && !cf, bc = a && !cb;
             // seed rows still unread (only needed when a side is closed)
-            const bool rp = bc && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);
-            const bool tp = fc && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);
+            const bool rpend = a && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);
+            const bool rp = bc && rpend;
+            const bool tpend = a && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);
+            const bool tp = fc && tpend;
             const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
             const bool open = a && !closed;
             const bool lkb = open && fc, lkf = open && bc;
@@ -1209,8 +1220,11 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const bool fwd = lkf || both || (open && !fc && !bc && cf <= cb);
             const bool bwd = lkb || both || (open && !fc && !bc && cf > cb);
             const uint64_t bcl = __ballot(closed), bf = __ballot(fwd), bb = __ballot(bwd);
-            const uint64_t lf = __ballot(lkf), lb = __ballot(lkb);
+            const uint64_t lf = __ballot(lkf), lb = __ballot(lkb), tr = __ballot(a && !tpend);
+            const uint64_t rr = __ballot(a && !rpend);
             if (tid == 0) {
+                S.sread[0] = (uint32_t)tr;
+                S.sread[1] = (uint32_t)rr;
                 S.active = act & ~(uint32_t)bcl;
                 S.sel[0] = (uint32_t)bf;
                 S.sel[1] = (uint32_t)bb;
@@ -1722,6 +1736,13 @@ struct ketogpu_engine {
     int wave_u = 8;
     bool use_v2 = true;
     bool use_bidi = true;
+    // plan "auto" (default): the first kTrialRuns batches of >= kTrialMin requests run
+    // both first stages (bidi, v2) back to back, each a complete evaluation, in
+    // alternating order; the engine then keeps the plan with the smaller summed time
+    static constexpr uint64_t kTrialMin = 1 << 16;
+    static constexpr int kTrialRuns = 2;
+    int trials_left = 0;
+    double trial_ms[2] = {0, 0};  // [0] v2, [1] bidi
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
     // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run with bidi_wide
     struct BidiCfg {
@@ -1830,12 +1851,13 @@ struct ketogpu_engine {
         // per 4/8/16 requests.  Spills go on to 4-request and 1-request units, then the
         // global path.
         const char *plan = getenv("KETOGPU_UNITS");
-        std::string p = plan ? plan : "bidi";
+        std::string p = plan ? plan : "auto";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        use_v2 = p == "v2" || p == "bidi";
+        use_v2 = p == "v2" || p == "bidi" || p == "auto";
         if (use_v2 && s.fint_col.size() >= (1ull << 32)) use_v2 = false;  // record begins are u32
         // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
-        use_bidi = p == "bidi" && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
+        use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
+        trials_left = p == "auto" && use_bidi ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
         if (const char *bc = getenv("KETOGPU_BIDI")) {  // "hlog,threads,lists,load", e.g. "9,64,192,6"
             BidiCfg c = bidi_cfg;
@@ -2243,9 +2265,24 @@ struct ketogpu_engine {
 
     void run(ketogpu_queries &qq) {
         HIP_CHECK(hipSetDevice(device));
+        if (trials_left && qq.n >= kTrialMin) {
+            const bool first_bidi = trials_left & 1;
+            for (int k = 0; k < 2; k++) {
+                use_bidi = first_bidi ^ (k == 1);
+                run_once(qq);
+                trial_ms[use_bidi] += last.ms_total;
+            }
+            if (--trials_left == 0) use_bidi = trial_ms[1] <= trial_ms[0];
+            return;
+        }
+        run_once(qq);
+    }
+
+    void run_once(ketogpu_queries &qq) {
         Batch q = qq.batch();
         ketogpu_run_stats rs{};
         rs.checks = q.n;
+        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? 1 : use_v2 ? 2 : 4;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();

@@ -53,7 +53,9 @@ def unit_plan(request, monkeypatch):
     (one-wave, 512-slot tables), bidi with the wide 2048-slot table, or forward-only unit2"""
     if request.param == "v2":
         monkeypatch.setenv("KETOGPU_UNITS", "v2")
-    elif request.param == "bidi-wide":
+    else:
+        monkeypatch.setenv("KETOGPU_UNITS", "bidi")
+    if request.param == "bidi-wide":
         monkeypatch.setenv("KETOGPU_BIDI", "11,256,384,6")
     return request.param
 
@@ -208,3 +210,29 @@ def test_loaded_snapshot_answers_identically(tmp_path):
     np.testing.assert_array_equal(targets, t2)
     np.testing.assert_array_equal(check.Engine(back).check_ids(roots, targets),
                                   check.Engine(snap).check_ids(roots, targets))
+
+
+@pytest.mark.parametrize("kind", ["rbac", "folders"])
+def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
+    """KETOGPU_UNITS=auto (default): the first two batches of >= 65536 requests run both
+    first stages (bidi and v2) and the engine keeps the faster; every call is exact"""
+    from keto_amd import synth
+    monkeypatch.delenv("KETOGPU_UNITS", raising=False)
+    w = {"rbac": lambda: synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=70000, seed=9),
+         "folders": lambda: synth.folders(users=8000, groups=300, folders=12000, tuples=150000, checks=70000,
+                                          seed=9)}[kind]()
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    roots, targets = w.resolve(snap)
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
+        w.requests(range(len(roots))), nthreads=8)
+    eng = check.Engine(snap)
+    np.testing.assert_array_equal(eng.check_ids(roots[:1000], targets[:1000]), want[:1000])
+    assert eng.last_stats()["plan"] == 1  # below the trial size: bidi
+    plans = set()
+    for _ in range(4):
+        np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+        plans.add(eng.last_stats()["plan"])
+    assert plans <= {1, 2}
+    kept = eng.last_stats()["plan"]
+    np.testing.assert_array_equal(eng.check_ids(roots[:5000], targets[:5000]), want[:5000])
+    assert eng.last_stats()["plan"] == kept

@@ -9,8 +9,8 @@ HBM-resident requests are timed exactly as bench.py times them.
 
 The CPU oracle cannot hold these graphs next to the engine, so correctness is checked by
 (1) every constructed positive must be allowed and (2) a 100k-request sample must agree
-bit-for-bit with a second engine on the same snapshot that uses the forward-only unit2
-kernels (a different algorithm: closure + reverse pull instead of bidirectional meet).
+bit-for-bit with a second engine on the same snapshot that runs the other first stage
+(bidi vs forward-only unit2: bidirectional meet vs closure + reverse pull).
 A heartbeat line every 30 s keeps long host phases visibly alive.
 """
 import argparse
@@ -53,6 +53,11 @@ def make(kind, tuples, checks):
                         check_seed=synth.SEED + 1)
 
 
+def check_plan(k):
+    from keto_amd import _lib as L
+    return L.RunStats.PLANS.get(k, "unit")
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", choices=["rbac", "folders", "social"], default="rbac")
@@ -93,7 +98,8 @@ def main():
     rs = eng.last_stats()
     got = q.download()
     PHASE[0] = "cross-checking"
-    os.environ["KETOGPU_UNITS"] = "v2"
+    other = "v2" if rs["plan"] == 1 else "bidi"  # the plan the timed engine did not keep
+    os.environ["KETOGPU_UNITS"] = other
     ref_eng = check.Engine(snap)
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
@@ -103,7 +109,8 @@ def main():
            "spilled_requests": rs["spilled_requests"], "allowed_fraction": round(float(got.mean()), 4),
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
-                           "against": "forward-only unit2 engine, same snapshot"},
+                           "against": f"{other} engine, same snapshot"},
+           "plan": check_plan(rs["plan"]),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
            "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}
     print(json.dumps(out), flush=True)
