@@ -973,9 +973,9 @@ __device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
     uint64_t bal = __ballot(want);
     uint32_t base = 0;
     if (bal) {
-        int leader = __ffsll((unsigned long long)bal) - 1;
+        int leader = __ffsll((unsigned long long)bal) - 1;  // wave-uniform
         if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (uint32_t)__popcll(bal));
-        base = __shfl(base, leader, 64);
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);  // v_readlane, not an LDS permute
     }
     return base + lanes_below(bal);
 }
@@ -986,15 +986,13 @@ __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert,
     constexpr int H = 1 << HLOG;
     uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
     for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
-        uint32_t kv = key[hh];
+        // insert: compare-and-swap first (one LDS round trip per probe, whether the slot
+        // is empty, holds u or holds another key)
+        const uint32_t kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
         if (kv == kEmpty) {
             if (!insert) return -1;
-            uint32_t prev = atomicCAS(&key[hh], kEmpty, u);
-            if (prev == kEmpty) {
-                inserted = true;
-                return (int)hh;
-            }
-            kv = prev;
+            inserted = true;
+            return (int)hh;
         }
         if (kv == u) return (int)hh;
     }
@@ -1017,10 +1015,8 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, boo
     }
     const int lane = threadIdx.x & 63;
     uint64_t bal = __ballot(inserted);
-    if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
-        uint32_t c = (uint32_t)__popcll(bal);
-        if (atomicAdd(&S.n_used, c) + c > (uint32_t)BidiShared<U, HLOG, F, BT, LF>::HMAX) S.spill = 1;
-    }
+    // table load: counted without a return value, compared with HMAX after the next barrier
+    if (bal && lane == __ffsll((unsigned long long)bal) - 1) atomicAdd(&S.n_used, (uint32_t)__popcll(bal));
     bool app = false;
     if (h >= 0) {
         const int vs = 32 * d;
@@ -1055,24 +1051,50 @@ template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
                                             BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, uint32_t k,
                                             const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
-    const uint32_t total = block_scan_sh<BT>(my_deg, S);
+    uint32_t total, start = 0;
+    if constexpr (BT == 64) {
+        // one wave, entry j on lane j (k <= 64): register scan, no LDS round trips
+        const uint32_t incl = wave_incl_sum_u32(my_deg);
+        start = incl - my_deg;
+        total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    } else {
+        total = block_scan_sh<BT>(my_deg, S);
+    }
     for (uint32_t eb = 0; eb < total; eb += BT) {
         uint32_t e = eb + threadIdx.x;
         bool want = e < total;
         uint32_t u = 0, deg = 0, bg = 0, m = 0;
         int d = 0;
+        uint32_t lo = 0, lo_start = 0;
+        if constexpr (BT == 64) {
+            // owner of edge e = the last entry starting at or before it: each entry that
+            // overlaps this chunk writes its index at its first position in the chunk
+            // (positions are distinct), then a prefix maximum fills the gaps; positions the
+            // chunk does not write hold owners of earlier edges, never larger (cleared for
+            // the first chunk)
+            const int lane = threadIdx.x;
+            if (eb == 0) S.c_pre[lane] = 0xFFFFFFFFu;
+            if (my_deg && start < eb + 64 && start + my_deg > eb) S.c_pre[(start > eb ? start : eb) - eb] = (uint32_t)lane;
+            __syncthreads();
+            const int o = wave_incl_max_i32((int)S.c_pre[lane]);
+            lo = (uint32_t)(o < 0 ? 0 : o);
+            lo_start = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lo << 2), (int)start);
+        }
         if (want) {
-            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
-            while (hi - lo > 1) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (S.c_pre[mid] <= e)
-                    lo = mid;
-                else
-                    hi = mid;
+            if constexpr (BT != 64) {
+                uint32_t hi = k;  // largest j with c_pre[j] <= e
+                while (hi - lo > 1) {
+                    uint32_t mid = (lo + hi) >> 1;
+                    if (S.c_pre[mid] <= e)
+                        lo = mid;
+                    else
+                        hi = mid;
+                }
+                lo_start = S.c_pre[lo];
             }
             d = sd[lo] >> 15;
             m = S.e_mask[lo] & S.active & ~*(volatile uint32_t *)&S.found;
-            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
+            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - lo_start)];
             u = rc.node;
             deg = rc.deg;
             bg = rc.begin;
@@ -1192,11 +1214,16 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                                     S.e_begin, 0, edges);
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
+    bool spilled = false;
     for (;;) {
         __syncthreads();
         const uint32_t cnt = S.n_p[cur];
         const uint32_t act = S.active & ~S.found;
-        if (S.spill || !cnt || !act) break;
+        if (S.spill || (S.n_used > (uint32_t)SH::HMAX && act)) {  // undecided requests, table over its load
+            spilled = true;
+            break;
+        }
+        if (!cnt || !act) break;
         n_levels++;
         unsigned long long tp0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
         const int nxt = cur ^ 1;
@@ -1239,7 +1266,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         // pending sums drop) and expanded right away, open requests' other bits stay
         // pending (the entry is carried to the next list)
         const uint32_t act2 = S.active;
-        for (uint32_t base = 0; base < cnt && !S.spill; base += BT) {  // S.spill: read after a barrier
+        for (uint32_t base = 0; base < cnt && !S.spill && S.n_used <= (uint32_t)SH::HMAX; base += BT) {  // read after a barrier
             const uint32_t k = cnt - base < (uint32_t)BT ? cnt - base : (uint32_t)BT;
             const uint32_t i = base + tid;
             uint32_t take = 0, rest = 0, sd = 0, dg = 0, bg = 0;
@@ -1280,7 +1307,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         cur = nxt;
     }
     __syncthreads();
-    if (S.spill) {
+    if (spilled || S.spill) {
         if (tid == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
         return;
     }
@@ -1769,6 +1796,9 @@ struct ketogpu_engine {
         KETO_BIDI(9, 128, 64, 6)
         KETO_BIDI(9, 192, 64, 7)
         KETO_BIDI(9, 128, 64, 7)
+        KETO_BIDI(8, 128, 64, 7)
+        KETO_BIDI(8, 96, 64, 7)
+        KETO_BIDI(8, 128, 64, 6)
 #undef KETO_BIDI
         throw Error(KETOGPU_EINVAL, "KETOGPU_BIDI: unsupported configuration");
     }

@@ -21,6 +21,34 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
     return v;
 }
 
+// 64-lane inclusive scans of a u32 / i32 held one per lane, without LDS: DPP row shifts
+// (1, 2, 4, 8) scan each 16-lane row, then the three lower row totals are read with
+// v_readlane and added.  Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    const int row = (int)(__lane_id() >> 4);
+    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+// inclusive prefix maximum over lanes (values >= -1; -1 = none)
+__device__ __forceinline__ int wave_incl_max_i32(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));
+    const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
+    const int r2 = __builtin_amdgcn_readlane(x, 47);
+    const int row = (int)(__lane_id() >> 4);
+    const int c = row == 0 ? -1 : row == 1 ? r0 : row == 2 ? max(r0, r1) : max(max(r0, r1), r2);
+    return max(x, c);
+}
+
 // Append (key, row length) to a frontier list with one atomic per wave.  Every lane of
 // the wave must call this (inactive lanes pass want = false).
 __device__ __forceinline__ void wave_append(bool want, uint64_t key, uint64_t deg, int lane, unsigned long long *ctr,
