@@ -148,7 +148,7 @@ def main():
         main = {"bidi": "bidi_kernel<16>", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
         fam = {
             main: (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
-            "spill stages (bidi wide table, unit2 cascade)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
+            "spill stages (bidi w,q,s cascade or unit2 cascade)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
                                                     max(st["unit_launches"] - 1, 0)),
             "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - st["unit_launches"]),
             "pull_kernel": (st["bytes_pull"], st["ms_pull"], st["rounds"]),

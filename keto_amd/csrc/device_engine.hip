@@ -59,6 +59,7 @@ struct DevGraph {
     const uint32_t *rev_col;
     const uint32_t *row_amb;  // nullptr when the snapshot has no ambiguous keys
     uint32_t Ni, Nx, N;
+    uint32_t both_max, seed_max;  // bidi: both-sides and eager-seed thresholds (kBothMax, kSeedBothMax)
 };
 
 struct DevState {
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         const bool v = tid < U && ((S.active >> tid) & 1u);
         const uint32_t bit = 1u << (tid & 15);
         const uint32_t rdeg = (uint32_t)(fe - fb), tdeg = (uint32_t)(re - rb);
-        const bool eager = rdeg <= kSeedBothMax && tdeg <= kSeedBothMax;
+        const bool eager = rdeg <= g.seed_max && tdeg <= g.seed_max;
         for (int side = 0; side < 2; side++) {
             const uint32_t u = side ? t : r, deg = side ? tdeg : rdeg;
             bool inserted = false;
@@ -1243,7 +1244,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
             const bool open = a && !closed;
             const bool lkb = open && fc, lkf = open && bc;
-            const bool both = open && !fc && !bc && cf <= kBothMax && cb <= kBothMax;
+            const bool both = open && !fc && !bc && cf <= g.both_max && cb <= g.both_max;
             const bool fwd = lkf || both || (open && !fc && !bc && cf <= cb);
             const bool bwd = lkb || both || (open && !fc && !bc && cf > cb);
             const uint64_t bcl = __ballot(closed), bf = __ballot(fwd), bb = __ballot(bwd);
@@ -1771,12 +1772,11 @@ struct ketogpu_engine {
     int trials_left = 0;
     double trial_ms[2] = {0, 0};  // [0] v2, [1] bidi
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
-    // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run with bidi_wide
+    // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run on the spill stages
     struct BidiCfg {
         int hlog, bt, f, lf;
         bool operator==(const BidiCfg &o) const { return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf; }
     };
-    BidiCfg bidi_wide{11, 256, 384, 6};  // KETOGPU_BIDI_WIDE: the spill stage
     BidiCfg bidi_cfg{9, 64, 128, 7};
 
     void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
@@ -1801,6 +1801,41 @@ struct ketogpu_engine {
         KETO_BIDI(8, 128, 64, 6)
 #undef KETO_BIDI
         throw Error(KETOGPU_EINVAL, "KETOGPU_BIDI: unsupported configuration");
+    }
+    // spill stages after the first bidi pass: U requests per unit, persistent grid
+    struct SpillStage {
+        int u;      // requests per unit (16, 4 or 1)
+        char kind;  // 'w' 2048-slot 16-request table (4 waves), 'h' 1024-slot 16-request (one wave),
+                    // 'q' 4096-slot 4-request (4 waves), 'r' 2048-slot 4-request (one wave),
+                    // 's' 8192-slot single request (4 waves, one workgroup per CU)
+    };
+    // KETOGPU_CASCADE; w -> q -> s measured best on configs #2-#4 (profiles/r01/tune_cascades.txt)
+    std::vector<SpillStage> cascade{{16, 'w'}, {4, 'q'}, {1, 's'}};
+
+    void launch_stage(const SpillStage &sg, const Batch &q, const uint32_t *in, const unsigned int *in_count,
+                      uint32_t fan, uint32_t *out, unsigned int *out_count, unsigned long long *stats) {
+        switch (sg.kind) {
+        case 'w':
+            KLAUNCH((bidi_kernel<16, 11, 384, 256, 6>), dim3(1024), dim3(256), 0, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+            return;
+        case 'q':
+            KLAUNCH((bidi_kernel<4, 12, 512, 256, 7>), dim3(512), dim3(256), 0, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+            return;
+        case 'h':
+            KLAUNCH((bidi_kernel<16, 10, 256, 64, 6>), dim3(2048), dim3(64), 0, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+            return;
+        case 'r':
+            KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(1280), dim3(64), 0, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+            return;
+        default:
+            KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(256), dim3(256), 0, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+            return;
+        }
     }
     const FRec *frec = nullptr;  // v2 edge records (parallel to fint_col)
     const FRec *brec = nullptr;  // v3 reverse records (parallel to rev_col)
@@ -1840,6 +1875,9 @@ struct ketogpu_engine {
     uint32_t *spill_units = nullptr, *spill_roots = nullptr, *spill_targets = nullptr;
     uint64_t *spill_allowed = nullptr, *spill_flags = nullptr;
     unsigned int *spill_count = nullptr;
+
+    bool cascade_log = getenv("KETOGPU_CASCADE_LOG") != nullptr;  // per-stage spill counts on stderr
+    hipEvent_t unit_end = nullptr;  // last event of the bidi cascade (already complete after its sync)
 
     hipEvent_t ev() {
         if (ev_used == ev_pool.size()) {
@@ -1893,9 +1931,16 @@ struct ketogpu_engine {
             BidiCfg c = bidi_cfg;
             if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_cfg = c;
         }
-        if (const char *bc = getenv("KETOGPU_BIDI_WIDE")) {
-            BidiCfg c = bidi_wide;
-            if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_wide = c;
+        if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
+            std::vector<SpillStage> c;
+            for (const char *p = cs; *p; p++) {
+                if (*p == 'w' || *p == 'h') c.push_back({16, *p});
+                else if (*p == 'q' || *p == 'r') c.push_back({4, *p});
+                else if (*p == 's') c.push_back({1, 's'});
+            }
+            if (c.empty() || c.back().kind != 's' || c.size() > 6)
+                throw Error(KETOGPU_EINVAL, "KETOGPU_CASCADE: stages w|h|q|r|s ending with s, at most 6");
+            cascade = c;
         }
         if (getenv("KETOGPU_STAMPS")) {
             stamps = dalloc<unsigned long long>((size_t)65536 * 16);
@@ -1915,6 +1960,12 @@ struct ketogpu_engine {
         g.Ni = s.Ni;
         g.Nx = s.Nx;
         g.N = s.N;
+        g.both_max = kBothMax;
+        g.seed_max = kSeedBothMax;
+        if (const char *bt = getenv("KETOGPU_BIDI_TUNE")) {  // "both,seed" (tuning runs)
+            unsigned a = kBothMax, b = kSeedBothMax;
+            if (sscanf(bt, "%u,%u", &a, &b) >= 1) g.both_max = a, g.seed_max = b;
+        }
         {
             std::vector<uint32_t> hk(((size_t)s.Ni + 31) / 32 + 1, 0);
             for (uint32_t v = 0; v < s.Ni; v++)
@@ -2061,47 +2112,49 @@ struct ketogpu_engine {
             // Forward-only plan "v2": the host-driven unit2 cascade unit2<16> -> unit2<4> ->
             // unit2<1> -> global path.
             if (use_bidi) {
-                // bidi (configured shape) -> bidi with the wide table (persistent over the
-                // spilled units) -> single-request bidi with an 8192-slot table (one
-                // workgroup per CU, persistent over the wide stage's spills split 16 ways)
-                // -> global path; one host synchronization for counts and statistics
-                const bool wide = !(bidi_cfg == bidi_wide);
-                hipEvent_t a = ev(), b = ev(), c = ev(), d = ev();
+                // bidi (configured shape) over every unit, then the spill stages of
+                // `cascade` (persistent over the previous stage's spilled units, counts read
+                // on the device), then the global path for single requests that exceed the
+                // last table; one host synchronization for counts and statistics
+                hipEvent_t a = ev(), b = ev(), d = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
                 launch_bidi(bidi_cfg, (unsigned)units, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                             st.stats, stamps);
                 HIP_CHECK(hipEventRecord(b, stream));
-                uint32_t *l16 = list[0];
-                unsigned int *c16 = &spill_count[0];
-                if (wide) {
-                    launch_bidi(bidi_wide, (unsigned)std::min<uint64_t>(units, bidi_wide.bt == 64 ? 2048 : 1024), 0, q,
-                                list[0], &spill_count[0], list[1], &spill_count[1], st.stats + 4 * kStatSlots,
-                                nullptr);
-                    l16 = list[1];
-                    c16 = &spill_count[1];
+                int cur = 0, u_prev = 16;
+                for (size_t k = 0; k < cascade.size(); k++) {
+                    const SpillStage sg = cascade[k];
+                    launch_stage(sg, q, list[cur], &spill_count[k], (uint32_t)(u_prev / sg.u), list[cur ^ 1],
+                                 &spill_count[k + 1], st.stats + 4 * kStatSlots);
+                    cur ^= 1;
+                    u_prev = sg.u;
                 }
-                HIP_CHECK(hipEventRecord(c, stream));
-                uint32_t *l1 = l16 == list[0] ? list[1] : list[0];
-                KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(256), dim3(256), 0, stream, g, frec, brec, q.roots,
-                        q.targets, q.n, q.allowed, l16, c16, 16u, l1, &spill_count[2], st.stats + 4 * kStatSlots,
-                        nullptr);
                 HIP_CHECK(hipEventRecord(d, stream));
+                const size_t ns = cascade.size() + 1;
                 KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
                 HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost,
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, ns * sizeof(unsigned int), hipMemcpyDeviceToHost,
                                          stream));
                 HIP_CHECK(hipStreamSynchronize(stream));
+                unit_end = d;
                 unit_ev.push_back({a, b});
                 unit_ev.push_back({b, d});
                 const uint64_t *t = (const uint64_t *)h_ctr + 16;
                 rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
                 const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
-                rs.spilled_units += cnt[0] + (wide ? cnt[1] : 0) + cnt[2];
-                rs.push_launches += wide ? 3 : 2;
-                rs.unit_launches += wide ? 3 : 2;
-                left = cnt[2];  // single requests for the global path
-                if (left && l1 != list[0])
-                    HIP_CHECK(hipMemcpyAsync(list[0], l1, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+                if (cascade_log) {
+                    fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)units);
+                    for (size_t k = 0; k < ns; k++) fprintf(stderr, " %u", cnt[k]);
+                    fprintf(stderr, "\n");
+                }
+                for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
+                rs.push_launches += ns;
+                rs.unit_launches += ns;
+                left = cnt[ns - 1];
+                if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
+                if (left && cur != 0)  // single requests for the global path, read from list[0]
+                    HIP_CHECK(hipMemcpyAsync(list[0], list[cur], left * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                             stream));
                 return left;
             }
             uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
@@ -2343,11 +2396,20 @@ struct ketogpu_engine {
         } else {
             run_global(q, rs, push_ev, pull_ev);
         }
-        HIP_CHECK(hipEventRecord(t_end, stream));
-        HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         uint64_t t3[3];
-        read_unit_stats(t3);  // both statistics regions; synchronizes the stream
-        uint64_t examined = h_ctr[8];
+        uint64_t examined = 0;
+        if (use_units && !wave_u && use_bidi && q.n && !rs.spilled_requests) {
+            // bidi cascade without global-path requests: run_units already synchronized,
+            // reduced and read the unit statistics (one host synchronization per run)
+            t_end = unit_end;
+            const uint64_t *t = (const uint64_t *)h_ctr + 16;
+            for (int k = 0; k < 3; k++) t3[k] = t[k] + t[3 + k];
+        } else {
+            HIP_CHECK(hipEventRecord(t_end, stream));
+            HIP_CHECK(hipMemcpyAsync(h_ctr + 8, st.stats, sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+            read_unit_stats(t3);  // both statistics regions; synchronizes the stream
+            examined = h_ctr[8];
+        }
         // unit path: 16 B per row opened (offset pair), 4 B per interior edge, 4 B per
         // reverse entry, 4+4 B per request (root, target), 8 B per result word
         rs.unit_rows = t3[0];

@@ -22,8 +22,10 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [
-    ("bidi_kernel<16>", r"bidi_kernel<16, (9|10), "),
-    ("bidi wide-table spill stage", r"bidi_kernel<16, 11, "),
+    ("bidi_kernel<16>", r"bidi_kernel<16, 9, "),
+    ("bidi spill stage w (16 requests, 2048 slots)", r"bidi_kernel<16, 11, "),
+    ("bidi spill stage h (16 requests, 1024 slots)", r"bidi_kernel<16, 10, "),
+    ("bidi spill stage q/r (4 requests)", r"bidi_kernel<4, "),
     ("bidi single-request stage", r"bidi_kernel<1, 13, "),
     ("unit2_kernel<16>", r"unit2_kernel<16>"),
     ("unit2_kernel<4>+<1> (spill passes)", r"unit2_kernel<(4|1)>"),
@@ -94,6 +96,14 @@ def summarise(src, workload):
             for part in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if part in c:
                     k[part.lower() + "_frac"] = c[part] / c["SQ_WAVE_CYCLES"]
+        if c.get("SQ_WAVES", 0) > 0:  # instructions per wave (one wave = one unit for the bidi kernels)
+            for part in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SMEM"):
+                if part in c:
+                    k[part.lower() + "_per_wave"] = c[part] / c["SQ_WAVES"]
+        if c.get("SQ_INSTS_VALU") and k.get("avg_duration_ms"):
+            # VALU issue share: a wave64 VALU instruction holds its SIMD's VALU for 4 cycles;
+            # 1024 SIMDs at 2.4 GHz (MI355X_MICROARCH.md)
+            k["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 4 / (1024 * 2.4e9 * k["avg_duration_ms"] * 1e-3)
         out["kernels"][fam] = k
     out["note"] = ("FETCH_SIZE/WRITE_SIZE are KB per dispatch; hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
                    "(gfx950 read correction, MI355X_MICROARCH.md 'HBM'); *_raw without the doubling.  The counters "

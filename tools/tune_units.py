@@ -29,17 +29,21 @@ engines, queries = {}, {}
 for p in plans:
     if p == "global":
         os.environ["KETOGPU_PATH"] = "global"
-    else:  # plan[:first[/wide]], e.g. bidi:9,64,128,7/10,64,256,7
+    else:  # plan[:first[/cascade]][@both,seed], e.g. bidi:9,64,128,7/q,s@12,32
         os.environ.pop("KETOGPU_PATH", None)
         os.environ.pop("KETOGPU_BIDI", None)
-        os.environ.pop("KETOGPU_BIDI_WIDE", None)
-        os.environ["KETOGPU_UNITS"] = p.split(":")[0]
-        if ":" in p:
-            first, _, wide = p.split(":")[1].partition("/")
+        os.environ.pop("KETOGPU_CASCADE", None)
+        os.environ.pop("KETOGPU_BIDI_TUNE", None)
+        spec, _, tune = p.partition("@")  # bidi[:first[/wide]][@both,seed]
+        if tune:
+            os.environ["KETOGPU_BIDI_TUNE"] = tune
+        os.environ["KETOGPU_UNITS"] = spec.split(":")[0]
+        if ":" in spec:
+            first, _, wide = spec.split(":")[1].partition("/")
             if first:
                 os.environ["KETOGPU_BIDI"] = first
             if wide:
-                os.environ["KETOGPU_BIDI_WIDE"] = wide
+                os.environ["KETOGPU_CASCADE"] = wide
     engines[p] = check.Engine(snap, state_budget_bytes=16 << 30)
     queries[p] = engines[p].upload(roots, targets)
 ref = None
