@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libketogpu.so")
+LIB_PATH = os.environ.get("KETOGPU_LIB") or os.path.join(HERE, "libketogpu.so")  # override: A/B builds
 
 OK, ENOTFOUND, EINVAL, EDEVICE, ENOMEM = 0, 1, 2, 3, 4
 SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
