@@ -1046,65 +1046,122 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, boo
     }
 }
 
+// one source predecessor u of t (u >= Ni): it meets only r itself, so it is compared with
+// the requests' roots instead of being stored
+template <int U, int HLOG, int F, int BT, int LF>
+__device__ __forceinline__ void bidi_source_meet(BidiShared<U, HLOG, F, BT, LF> &S, uint32_t u, uint32_t m) {
+    uint32_t hit = 0;
+    for (uint32_t b = m; b; b &= b - 1)
+        if (S.root[__ffs(b) - 1] == u) hit |= b & (~b + 1);
+    if (hit) atomicOr(&S.found, hit);
+}
+
+// One-wave units (BT == 64): entry j on lane j (k <= 64).  Register scan of the degrees, an
+// owner map per 64-edge chunk (each entry that overlaps the chunk writes its index at its
+// first position in it — positions are distinct — and a prefix maximum fills the gaps;
+// positions a chunk does not write hold owners of earlier edges, never larger), and the
+// record loads software-pipelined one chunk ahead of the pushes.
+template <int U, int HLOG, int F, int BT, int LF>
+__device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *frec, const FRec *brec,
+                                              BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, const uint16_t *sd,
+                                              const uint32_t *begin, int nxt, uint64_t &edges) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t incl = wave_incl_sum_u32(my_deg);
+    const uint32_t start = incl - my_deg;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (!total) return;
+    S.c_pre[lane] = 0xFFFFFFFFu;
+    struct Edge {
+        uint32_t lo;  // owning entry
+        uint32_t ls;  // its first edge
+        int d;        // its direction
+        FRec rc;      // the record of edge eb + lane
+    };
+    // Owner of edge eb + lane, then its record.  `more` false: no chunk at eb — the load is
+    // still issued (the previous chunk's edge again, an L2 hit), because a load under a
+    // branch is merged by a register copy that waits for it right away.
+    auto fetch = [&](uint32_t eb, Edge &x, bool more, const Edge &prev) {
+        uint32_t e;
+        if (more) {
+            if (my_deg && start < eb + 64 && start + my_deg > eb) S.c_pre[(start > eb ? start : eb) - eb] = lane;
+            __syncthreads();
+            const int o = wave_incl_max_i32((int)S.c_pre[lane]);
+            x.lo = (uint32_t)(o < 0 ? 0 : o);
+            x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
+            x.d = sd[x.lo] >> 15;
+            e = min(eb + lane, total - 1);  // lanes past the end re-read the last edge
+        } else {
+            x.lo = prev.lo;
+            x.ls = prev.ls;
+            x.d = prev.d;
+            e = min(eb - 64 + lane, total - 1);
+        }
+        x.rc = (x.d ? brec : frec)[(uint64_t)begin[x.lo] + (e - x.ls)];
+    };
+    auto push = [&](uint32_t eb, const Edge &x) {
+        uint32_t m = 0;
+        if (eb + lane < total) {
+            m = S.e_mask[x.lo] & S.active & ~S.found;
+            edges++;
+            if (x.d && x.rc.node >= g.Ni) {
+                bidi_source_meet<U, HLOG, F, BT, LF>(S, x.rc.node, m);
+                m = 0;
+            }
+        }
+        bidi_push<U, HLOG, F, BT, LF>(S, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, x.d, nxt);
+    };
+    // two register sets in turn, so the next chunk's loads fly during this chunk's pushes
+    // without a loop-carried copy
+    Edge a{}, b{};
+    fetch(0, a, true, b);
+    for (uint32_t eb = 0;;) {
+        const bool more = eb + 64 < total;  // wave-uniform
+        fetch(eb + 64, b, more, a);
+        push(eb, a);
+        if (!more) break;
+        eb += 64;
+        const bool more2 = eb + 64 < total;
+        fetch(eb + 64, a, more2, b);
+        push(eb, b);
+        if (!more2) break;
+        eb += 64;
+    }
+}
+
 // Expand k entries (entry j: sd[j], begin[j], S.e_mask[j]); `my_deg` is the degree this
 // thread contributes for entry threadIdx.x (0 when it has none).  Block-uniform loop.
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
                                             BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, uint32_t k,
                                             const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
-    uint32_t total, start = 0;
     if constexpr (BT == 64) {
-        // one wave, entry j on lane j (k <= 64): register scan, no LDS round trips
-        const uint32_t incl = wave_incl_sum_u32(my_deg);
-        start = incl - my_deg;
-        total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    } else {
-        total = block_scan_sh<BT>(my_deg, S);
+        bidi_expand64<U, HLOG, F, BT, LF>(g, frec, brec, S, my_deg, sd, begin, nxt, edges);
+        return;
     }
+    const uint32_t total = block_scan_sh<BT>(my_deg, S);
     for (uint32_t eb = 0; eb < total; eb += BT) {
         uint32_t e = eb + threadIdx.x;
         bool want = e < total;
         uint32_t u = 0, deg = 0, bg = 0, m = 0;
         int d = 0;
-        uint32_t lo = 0, lo_start = 0;
-        if constexpr (BT == 64) {
-            // owner of edge e = the last entry starting at or before it: each entry that
-            // overlaps this chunk writes its index at its first position in the chunk
-            // (positions are distinct), then a prefix maximum fills the gaps; positions the
-            // chunk does not write hold owners of earlier edges, never larger (cleared for
-            // the first chunk)
-            const int lane = threadIdx.x;
-            if (eb == 0) S.c_pre[lane] = 0xFFFFFFFFu;
-            if (my_deg && start < eb + 64 && start + my_deg > eb) S.c_pre[(start > eb ? start : eb) - eb] = (uint32_t)lane;
-            __syncthreads();
-            const int o = wave_incl_max_i32((int)S.c_pre[lane]);
-            lo = (uint32_t)(o < 0 ? 0 : o);
-            lo_start = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lo << 2), (int)start);
-        }
         if (want) {
-            if constexpr (BT != 64) {
-                uint32_t hi = k;  // largest j with c_pre[j] <= e
-                while (hi - lo > 1) {
-                    uint32_t mid = (lo + hi) >> 1;
-                    if (S.c_pre[mid] <= e)
-                        lo = mid;
-                    else
-                        hi = mid;
-                }
-                lo_start = S.c_pre[lo];
+            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
+            while (hi - lo > 1) {
+                uint32_t mid = (lo + hi) >> 1;
+                if (S.c_pre[mid] <= e)
+                    lo = mid;
+                else
+                    hi = mid;
             }
             d = sd[lo] >> 15;
-            m = S.e_mask[lo] & S.active & ~*(volatile uint32_t *)&S.found;
-            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - lo_start)];
+            m = S.e_mask[lo] & S.active & ~S.found;
+            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
             u = rc.node;
             deg = rc.deg;
             bg = rc.begin;
             edges++;
-            if (d && u >= g.Ni) {  // a source predecessor of t: it meets only r itself
-                uint32_t hit = 0;
-                for (uint32_t b = m; b; b &= b - 1)
-                    if (S.root[__ffs(b) - 1] == u) hit |= b & (~b + 1);
-                if (hit) atomicOr(&S.found, hit);
+            if (d && u >= g.Ni) {
+                bidi_source_meet<U, HLOG, F, BT, LF>(S, u, m);
                 m = 0;
             }
             want = m != 0;
