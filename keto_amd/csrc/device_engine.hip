@@ -926,8 +926,8 @@ struct BidiShared {
     static constexpr int H = 1 << HLOG;
     static constexpr int HMAX = H * LF / 8;
     static constexpr int EM = BT > 2 * U ? BT : 2 * U;
-    uint32_t key[H];
-    unsigned long long st[H];
+    alignas(16) uint32_t key[H];
+    alignas(16) unsigned long long st[H];
     uint16_t p_sd[2][F];  // pending lists (ping-pong): slot | dir << 15
     uint32_t p_begin[2][F], p_deg[2][F];
     uint16_t e_sd[2 * U];  // eager seed rows: forward of r_j, backward of t_j
@@ -937,11 +937,17 @@ struct BidiShared {
     uint32_t wave_sum[BT / 64];
     uint32_t cost[2][U];          // pending degree sums per direction and request
     uint32_t root[U];
-    uint16_t rslot[U], tslot[U];  // table slots of the seeds r_j, t_j
     uint32_t sel[2], lookup[2];   // per direction: bits expanded this level / lookup-only bits
     uint32_t sread[2];            // per direction: bits for which a push of a dead-end node is lookup-only
     uint32_t n_used, n_e, n_p[2], spill, found, active;
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
+};
+
+// per-level selection, wave-uniform: open requests, bits expanded per direction, lookup-only
+// bits, and bits for which a dead-end push is lookup-only (one-wave units keep it in SGPRs)
+struct BidiLevel {
+    uint32_t active;
+    uint32_t sel[2], lookup[2], sread[2];
 };
 
 // exclusive block scan of one u32 per thread (BT threads) into S.c_pre; returns the total
@@ -1000,13 +1006,13 @@ __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert,
     return -1;
 }
 
-// Push mask m into node u in direction d.  Bits in S.lookup[d] belong to requests whose
+// Push mask m into node u in direction d.  Bits in L.lookup[d] belong to requests whose
 // other side is closed: for them u is only looked up (a meet or nothing), never inserted
 // nor made pending.  New pending bits add deg to their requests' pending sums.
 template <int U, int HLOG, int F, int BT, int LF>
-__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, bool want, uint32_t u, uint32_t deg,
-                                          uint32_t begin, uint32_t m, int d, int nxt) {
-    const uint32_t lk = m & (S.lookup[d] | (deg ? 0u : S.sread[d]));
+__device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, const BidiLevel &L, bool want, uint32_t u,
+                                          uint32_t deg, uint32_t begin, uint32_t m, int d, int nxt) {
+    const uint32_t lk = m & ((d ? L.lookup[1] : L.lookup[0]) | (deg ? 0u : (d ? L.sread[1] : L.sread[0])));
     int h = -1;
     bool inserted = false;
     if (want) {
@@ -1063,8 +1069,8 @@ __device__ __forceinline__ void bidi_source_meet(BidiShared<U, HLOG, F, BT, LF> 
 // record loads software-pipelined one chunk ahead of the pushes.
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *frec, const FRec *brec,
-                                              BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, const uint16_t *sd,
-                                              const uint32_t *begin, int nxt, uint64_t &edges) {
+                                              BidiShared<U, HLOG, F, BT, LF> &S, const BidiLevel &L, uint32_t my_deg,
+                                              const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
@@ -1101,14 +1107,14 @@ __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *fre
     auto push = [&](uint32_t eb, const Edge &x) {
         uint32_t m = 0;
         if (eb + lane < total) {
-            m = S.e_mask[x.lo] & S.active & ~S.found;
+            m = S.e_mask[x.lo] & L.active & ~S.found;
             edges++;
             if (x.d && x.rc.node >= g.Ni) {
                 bidi_source_meet<U, HLOG, F, BT, LF>(S, x.rc.node, m);
                 m = 0;
             }
         }
-        bidi_push<U, HLOG, F, BT, LF>(S, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, x.d, nxt);
+        bidi_push<U, HLOG, F, BT, LF>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, x.d, nxt);
     };
     // two register sets in turn, so the next chunk's loads fly during this chunk's pushes
     // without a loop-carried copy
@@ -1132,10 +1138,11 @@ __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *fre
 // thread contributes for entry threadIdx.x (0 when it has none).  Block-uniform loop.
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
-                                            BidiShared<U, HLOG, F, BT, LF> &S, uint32_t my_deg, uint32_t k,
-                                            const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
+                                            BidiShared<U, HLOG, F, BT, LF> &S, const BidiLevel &L, uint32_t my_deg,
+                                            uint32_t k, const uint16_t *sd, const uint32_t *begin, int nxt,
+                                            uint64_t &edges) {
     if constexpr (BT == 64) {
-        bidi_expand64<U, HLOG, F, BT, LF>(g, frec, brec, S, my_deg, sd, begin, nxt, edges);
+        bidi_expand64<U, HLOG, F, BT, LF>(g, frec, brec, S, L, my_deg, sd, begin, nxt, edges);
         return;
     }
     const uint32_t total = block_scan_sh<BT>(my_deg, S);
@@ -1154,7 +1161,7 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
                     hi = mid;
             }
             d = sd[lo] >> 15;
-            m = S.e_mask[lo] & S.active & ~S.found;
+            m = S.e_mask[lo] & L.active & ~S.found;
             FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
             u = rc.node;
             deg = rc.deg;
@@ -1166,7 +1173,7 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
             }
             want = m != 0;
         }
-        bidi_push<U, HLOG, F, BT, LF>(S, want, u, deg, bg, m, d, nxt);
+        bidi_push<U, HLOG, F, BT, LF>(S, L, want, u, deg, bg, m, d, nxt);
     }
 }
 
@@ -1183,10 +1190,9 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t c0 = unit * U;
     const int shift = (int)(c0 & 63);
-    for (int i = tid; i < SH::H; i += BT) {
-        S.key[i] = kEmpty;
-        S.st[i] = 0;
-    }
+    // clear the table with 16-byte stores (4 keys or 2 state words per store)
+    for (int i = tid; i < SH::H / 4; i += BT) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+    for (int i = tid; i < SH::H / 2; i += BT) reinterpret_cast<uint4 *>(S.st)[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) {
         S.n_used = S.n_e = S.n_p[0] = S.n_p[1] = S.spill = S.found = S.active = 0;
         S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
@@ -1199,6 +1205,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     __syncthreads();
     uint64_t rows = 0, edges = 0;
     uint32_t n_levels = 0;
+    int rslot = 0, tslot = 0;  // table slots of this lane's request's seeds (wave 0, lane j = request j)
     uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
     uint64_t fb = 0, fe = 0, rb = 0, re = 0;
     if (tid < U) {
@@ -1238,9 +1245,9 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             bool app = false;
             if (h >= 0) {
                 if (side == 0)
-                    S.rslot[tid] = (uint16_t)h;
+                    rslot = h;
                 else
-                    S.tslot[tid] = (uint16_t)h;
+                    tslot = h;
                 const bool pend = !eager && deg;
                 unsigned long long bits = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
                 if (pend) bits |= (unsigned long long)bit << (32 * side + 16);
@@ -1268,7 +1275,8 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     }
     __syncthreads();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
-    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, (uint32_t)tid < 2 * U ? S.e_deg[tid] : 0, 2 * U, S.e_sd,
+    BidiLevel L{S.active, {0, 0}, {0, 0}, {0, 0}};  // the seed rows: every push inserts
+    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, (uint32_t)tid < 2 * U ? S.e_deg[tid] : 0, 2 * U, S.e_sd,
                                     S.e_begin, 0, edges);
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
@@ -1276,7 +1284,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     for (;;) {
         __syncthreads();
         const uint32_t cnt = S.n_p[cur];
-        const uint32_t act = S.active & ~S.found;
+        const uint32_t act = L.active & ~S.found;
         if (S.spill || (S.n_used > (uint32_t)SH::HMAX && act)) {  // undecided requests, table over its load
             spilled = true;
             break;
@@ -1294,9 +1302,9 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const int j = tid & 15;
             const bool fc = a && !cf, bc = a && !cb;
             // seed rows still unread (only needed when a side is closed)
-            const bool rpend = a && ((S.st[S.rslot[j]] >> (16 + j)) & 1ull);
+            const bool rpend = a && ((S.st[rslot] >> (16 + j)) & 1ull);
             const bool rp = bc && rpend;
-            const bool tpend = a && ((S.st[S.tslot[j]] >> (48 + j)) & 1ull);
+            const bool tpend = a && ((S.st[tslot] >> (48 + j)) & 1ull);
             const bool tp = fc && tpend;
             const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
             const bool open = a && !closed;
@@ -1307,23 +1315,29 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const uint64_t bcl = __ballot(closed), bf = __ballot(fwd), bb = __ballot(bwd);
             const uint64_t lf = __ballot(lkf), lb = __ballot(lkb), tr = __ballot(a && !tpend);
             const uint64_t rr = __ballot(a && !rpend);
+            L = BidiLevel{act & ~(uint32_t)bcl, {(uint32_t)bf, (uint32_t)bb}, {(uint32_t)lf, (uint32_t)lb},
+                          {(uint32_t)tr, (uint32_t)rr}};
             if (tid == 0) {
-                S.sread[0] = (uint32_t)tr;
-                S.sread[1] = (uint32_t)rr;
-                S.active = act & ~(uint32_t)bcl;
-                S.sel[0] = (uint32_t)bf;
-                S.sel[1] = (uint32_t)bb;
-                S.lookup[0] = (uint32_t)lf;
-                S.lookup[1] = (uint32_t)lb;
+                if constexpr (BT > 64) {  // other waves read the selection from LDS
+                    S.active = L.active;
+                    S.sel[0] = L.sel[0];
+                    S.sel[1] = L.sel[1];
+                    S.lookup[0] = L.lookup[0];
+                    S.lookup[1] = L.lookup[1];
+                    S.sread[0] = L.sread[0];
+                    S.sread[1] = L.sread[1];
+                }
                 S.n_p[nxt] = 0;
             }
         }
         __syncthreads();
+        if constexpr (BT > 64)
+            L = BidiLevel{S.active, {S.sel[0], S.sel[1]}, {S.lookup[0], S.lookup[1]}, {S.sread[0], S.sread[1]}};
         unsigned long long tp1 = stamp ? __builtin_amdgcn_s_memtime() : 0;
         // chunks of BT pending entries: the chosen direction's bits are taken (their
         // pending sums drop) and expanded right away, open requests' other bits stay
         // pending (the entry is carried to the next list)
-        const uint32_t act2 = S.active;
+        const uint32_t act2 = L.active;
         for (uint32_t base = 0; base < cnt && !S.spill && S.n_used <= (uint32_t)SH::HMAX; base += BT) {  // read after a barrier
             const uint32_t k = cnt - base < (uint32_t)BT ? cnt - base : (uint32_t)BT;
             const uint32_t i = base + tid;
@@ -1334,7 +1348,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                 bg = S.p_begin[cur][i];
                 const uint32_t d = sd >> 15, s = sd & 0x7FFFu;
                 const uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
-                take = pb & S.sel[d];
+                take = pb & (d ? L.sel[1] : L.sel[0]);
                 rest = pb & act2 & ~take;
                 const uint32_t clr = pb & ~rest;
                 if (clr) {
@@ -1353,7 +1367,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                     S.spill = 1;
                 }
             }
-            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, take ? dg : 0, k, S.p_sd[cur] + base,
+            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, take ? dg : 0, k, S.p_sd[cur] + base,
                                             S.p_begin[cur] + base, nxt, edges);
             __syncthreads();
         }
