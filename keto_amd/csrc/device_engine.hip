@@ -1177,13 +1177,45 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
     }
 }
 
-// one unit (requests [U*unit, U*unit + U)) by the whole workgroup
+// The seeds of request `threadIdx.x` of a unit (lanes < U): its root and target, then the
+// offsets of both seed rows (two dependent loads).  A persistent first stage that loaded
+// them one unit ahead measured slower than one workgroup per unit (static striding 0.475
+// vs 0.435 ms per 1M requests: tail imbalance and 107 VGPRs; a device-scope work counter
+// 0.89 ms: every record-load wait also waited for the counter's atomic).
+struct BidiSeed {
+    uint32_t r, t;
+    uint64_t fb, fe, rb, re;
+};
+
+template <int U>
+__device__ __forceinline__ void bidi_load_rt(uint64_t unit, uint64_t units, const uint32_t *roots,
+                                             const uint32_t *targets, uint64_t n, uint32_t &r, uint32_t &t) {
+    r = t = KETOGPU_NODE_NONE;
+    const uint64_t c = unit * U + threadIdx.x;
+    if (threadIdx.x < U && unit < units && c < n) {
+        r = roots[c];
+        t = targets[c];
+    }
+}
+
+__device__ __forceinline__ BidiSeed bidi_load_rows(const DevGraph &g, uint32_t r, uint32_t t) {
+    BidiSeed s{t == KETOGPU_NODE_NONE ? KETOGPU_NODE_NONE : r, t, 0, 0, 0, 0};
+    if (s.r != KETOGPU_NODE_NONE && s.r < kDynBase) {
+        s.fb = g.fint_off[s.r];
+        s.fe = g.fint_off[s.r + 1];
+        s.rb = g.rev_off[t];
+        s.re = g.rev_off[t + 1];
+    }
+    return s;
+}
+
+// one unit (requests [U*unit, U*unit + U)) by the whole workgroup; `seed` as loaded by
+// bidi_load_rt + bidi_load_rows on lanes < U
 template <int U, int HLOG, int F, int BT, int LF>
 __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, const DevGraph &g, const FRec *frec,
-                                          const FRec *brec, const uint32_t *roots, const uint32_t *targets, uint64_t n,
-                                          uint64_t *allowed, const uint64_t unit, uint32_t *spill_out,
-                                          unsigned int *spill_count, unsigned long long *stats,
-                                          unsigned long long *stamp) {
+                                          const FRec *brec, const BidiSeed &seed, uint64_t *allowed,
+                                          const uint64_t unit, uint32_t *spill_out, unsigned int *spill_count,
+                                          unsigned long long *stats, unsigned long long *stamp) {
     static_assert(U <= 16, "16 request bits per direction");
     using SH = BidiShared<U, HLOG, F, BT, LF>;
     const int tid = threadIdx.x;
@@ -1206,20 +1238,10 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     uint64_t rows = 0, edges = 0;
     uint32_t n_levels = 0;
     int rslot = 0, tslot = 0;  // table slots of this lane's request's seeds (wave 0, lane j = request j)
-    uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
-    uint64_t fb = 0, fe = 0, rb = 0, re = 0;
+    const uint32_t r = seed.r, t = seed.t;
+    const uint64_t fb = seed.fb, fe = seed.fe, rb = seed.rb, re = seed.re;
     if (tid < U) {
-        uint64_t c = c0 + tid;
-        if (c < n) {
-            r = roots[c];
-            t = targets[c];
-        }
-        if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
         if (r != KETOGPU_NODE_NONE && r < kDynBase) {
-            fb = g.fint_off[r];
-            fe = g.fint_off[r + 1];
-            rb = g.rev_off[t];
-            re = g.rev_off[t + 1];
             rows += 2;
             if (re > rb) atomicOr(&S.active, 1u << tid);  // nothing reaches a t without predecessors
         }
@@ -1412,19 +1434,25 @@ __global__ __launch_bounds__(BT) void bidi_kernel(DevGraph g, const FRec *frec, 
                                                   unsigned int *spill_count, unsigned long long *stats,
                                                   unsigned long long *stamps) {
     __shared__ BidiShared<U, HLOG, F, BT, LF> S;
+    const uint64_t units = (n + U - 1) / U;
     if (!in_count) {
         unsigned long long *stamp =
             (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
-        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed,
-                                      parents ? parents[blockIdx.x] : blockIdx.x, spill_out, spill_count, stats, stamp);
+        const uint64_t unit = parents ? parents[blockIdx.x] : blockIdx.x;
+        uint32_t r, t;
+        bidi_load_rt<U>(unit, units, roots, targets, n, r, t);
+        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out,
+                                      spill_count, stats, stamp);
         return;
     }
     // persistent: every listed unit of the previous stage splits into `fan` units of U
     const uint64_t cnt = (uint64_t)*in_count * fan;
     for (uint64_t b = blockIdx.x; b < cnt; b += gridDim.x) {
-        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, roots, targets, n, allowed,
-                                      (uint64_t)parents[b / fan] * fan + b % fan, spill_out, spill_count, stats,
-                                      nullptr);
+        const uint64_t unit = (uint64_t)parents[b / fan] * fan + b % fan;
+        uint32_t r, t;
+        bidi_load_rt<U>(unit, units, roots, targets, n, r, t);
+        bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out,
+                                      spill_count, stats, nullptr);
         __syncthreads();
     }
 }
