@@ -1895,6 +1895,8 @@ struct ketogpu_engine {
         KETO_BIDI(9, 128, 64, 6)
         KETO_BIDI(9, 192, 64, 7)
         KETO_BIDI(9, 128, 64, 7)
+        KETO_BIDI(9, 64, 64, 7)
+        KETO_BIDI(9, 96, 64, 7)
         KETO_BIDI(8, 128, 64, 7)
         KETO_BIDI(8, 96, 64, 7)
         KETO_BIDI(8, 128, 64, 6)
