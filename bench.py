@@ -36,6 +36,9 @@ def parse():
     p.add_argument("--small", action="store_true", help="1/100-size graph for quick runs (not the metric)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU work of the baseline sample")
+    p.add_argument("--parity", choices=["full", "sample"], default="full",
+                   help="full: every request of the timed batch is diffed against the oracle (about 90 s of "
+                        "16-thread CPU work at config #2); sample: only the baseline sample")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
     p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
@@ -170,12 +173,18 @@ def main():
                 "bytes_per_launch": int(b_dom / max(n_launch, 1)), "ms_per_launch": round(ms_dom / max(n_launch, 1), 4),
                 "kernels": {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": b, "launches": n}
                             for k, (b, ms, n) in fam.items() if ms > 0}}
+        stream = stream_copy_gbps(local)
+        roof["stream_copy_GBps"] = round(stream, 1)  # measured device-copy bandwidth
+        roof["frac_of_stream"] = round(achieved / stream, 4) if stream > 0 else None
         cpu = None
         parity = None
         sql = None
         if not a.no_cpu_baseline:
-            cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds)
+            cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds, full=a.parity == "full")
             sql = sql_baseline(min(10.0, a.cpu_seconds))
+        pos = np.asarray(w.chk_pos, dtype=bool)
+        parity = dict(parity or {}, constructed_positives=int(pos.sum()),
+                      constructed_positives_denied=int((pos & ~allowed.astype(bool)).sum()))
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
@@ -188,6 +197,7 @@ def main():
             "plan": plan,
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total")},
+            "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(n, 1), 2),
             "allowed_fraction": round(float(allowed.mean()), 4),
             "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2), "h2d_queries": round(t_h2d, 4)},
             "pcie_inclusive_checks_per_s": round(n / t_host, 1),
@@ -289,9 +299,27 @@ def sql_baseline(seconds):
                       f"load {t_load:.1f}s"}
 
 
-def cpu_baseline(w, gpu_allowed, seconds):
+def stream_copy_gbps(device, nbytes=1 << 30, iters=10):
+    """device-to-device copy bandwidth (read + write bytes / time) of a 1 GiB buffer: the
+    measured ceiling beside the 8 TB/s spec"""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{device}")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1)
+    del a, b
+    return 2 * nbytes * iters / (ms * 1e-3) / 1e9
+
+
+def cpu_baseline(w, gpu_allowed, seconds, full=True):
     """The oracle (exact restatement of the reference DFS) on host cores over a bounded
-    sample of the same requests; its answers double as a bit-exact parity sample."""
+    sample of the same requests; its answers double as a bit-exact parity sample, and with
+    `full` the rest of the batch is diffed too (every timed run is checked)."""
     from oracle import oracle as O
     from tests import randgraph
     threads = min(16, os.cpu_count() or 1)
@@ -312,6 +340,14 @@ def cpu_baseline(w, gpu_allowed, seconds):
     ans = orc.check_batch(w.requests(sample), nthreads=threads)
     ts = time.perf_counter() - t0
     mism = int((ans != gpu_allowed[sample]).sum())
+    checked = len(sample)
+    if full and m < len(idx):
+        rest = idx[m:]
+        t0 = time.perf_counter()
+        ans_rest = orc.check_batch(w.requests(rest), nthreads=threads)
+        log(f"parity: remaining {len(rest)} requests diffed in {time.perf_counter() - t0:.1f}s")
+        mism += int((ans_rest != gpu_allowed[rest]).sum())
+        checked += len(rest)
     one = idx[:max(200, m // threads)]  # the same work on one core
     t0 = time.perf_counter()
     orc.check_batch(w.requests(one), nthreads=1)
@@ -321,7 +357,8 @@ def cpu_baseline(w, gpu_allowed, seconds):
              "value_1_core": round(rate1, 1),
              "sample": f"{len(sample)} of the {w.n_checks} config-2 requests (uniform sample), full 50M-tuple graph; "
                        f"oracle/keto_oracle.c on {threads} threads of {cpu_model()}; store build {t_build:.1f}s"},
-            {"sample": len(sample), "mismatches": mism})
+            {"checked": checked, "of": int(w.n_checks), "mismatches": mism,
+             "against": "oracle/keto_oracle.c (exact restatement of internal/check/engine.go)"})
 
 
 if __name__ == "__main__":

@@ -50,6 +50,25 @@ class Engine:
         self.L = L.lib()
         self.snapshot = snapshot
 
+    def tree_size(self, subject: Subject, rest_depth: int) -> int:
+        """number of nodes of BuildTree's tree (0 for a nil tree), built and dropped in C++
+        without Python objects (throughput measurements)"""
+        h = C.c_void_p()
+        subj = subject_struct(subject)
+        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), int(rest_depth), C.byref(h))
+        if rc == L.ENOTFOUND:
+            raise NotFound(self.L.ketogpu_last_error().decode("utf-8", "replace"))
+        L.check(rc)
+        if not h.value:
+            return 0
+        try:
+            nodes = C.POINTER(L.TreeNode)()
+            n = C.c_size_t()
+            L.check(self.L.ketogpu_tree_nodes(h, C.byref(nodes), C.byref(n)))
+            return int(n.value)
+        finally:
+            self.L.ketogpu_tree_free(h)
+
     def BuildTree(self, subject: Subject, rest_depth: int) -> Optional[Tree]:
         h = C.c_void_p()
         subj = subject_struct(subject)

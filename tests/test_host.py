@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from keto_amd import _lib as L
-from keto_amd import expand, persistence
+from keto_amd import expand, persistence, synth
 from keto_amd import relationtuple as rt
 from keto_amd.snapshot import Snapshot
 from oracle import oracle as O
@@ -136,6 +136,22 @@ def test_expand_matches_oracle_on_random_tables(seed, page_size, poison, collide
                 except expand.NotFound:
                     got, gerr = None, "not_found"
                 assert (got, gerr) == (want, werr), (s, depth)
+
+
+def test_tree_size_counts_build_tree_nodes():
+    # tools/bench_scale.py times expand with tree_size (no Python objects): same trees
+    def count(t):
+        return 0 if t is None else 1 + sum(count(c) for c in t.children)
+    w = synth.folders(users=2000, groups=50, folders=3000, tuples=30000, checks=50, seed=5)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    ex = expand.Engine(snap)
+    sizes = []
+    for ns, o, r, _ in w.requests(range(50)):
+        for depth in (0, 1, 3, 10):
+            s = rt.SubjectSet(ns, o, r)
+            sizes.append(ex.tree_size(s, depth))
+            assert sizes[-1] == count(ex.BuildTree(s, depth))
+    assert max(sizes) > 10
 
 
 def test_snapshot_stats_and_classes():

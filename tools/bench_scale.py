@@ -66,6 +66,7 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--sample", type=int, default=100_000)
+    p.add_argument("--expand-sample", type=int, default=200, help="BuildTree roots timed per max-depth")
     a = p.parse_args()
     threading.Thread(target=heartbeat, daemon=True).start()
     PHASE[0] = "generating"
@@ -80,6 +81,7 @@ def main():
     log(f"snapshot in {t_snap:.1f}s: {st}")
     roots, targets = w.resolve(snap)
     pos = w.chk_pos.astype(bool)
+    expand_roots = [q[:3] for q in w.requests(range(min(a.expand_sample, w.n_checks)))]
     del w  # the rows are no longer needed
     PHASE[0] = "uploading the device graph"
     t0 = time.time()
@@ -103,6 +105,18 @@ def main():
     ref_eng = check.Engine(snap)
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
+    PHASE[0] = "expand"
+    from keto_amd import expand
+    from keto_amd.relationtuple import SubjectSet
+    xe = expand.Engine(snap)
+    exp = {}
+    for depth in (3, 5, 10):  # config #3: expand at max-depth 3, 5, 10 (host DFS, R10)
+        t0 = time.perf_counter()
+        nodes = [xe.tree_size(SubjectSet(ns, o, r), depth) for ns, o, r in expand_roots]
+        dt_e = time.perf_counter() - t0
+        exp[f"max_depth_{depth}"] = {"trees_per_s": round(len(nodes) / dt_e, 1),
+                                     "nodes_per_tree": round(float(np.mean(nodes)), 1), "max_nodes": int(max(nodes))}
+    log(f"expand: {exp}")
     out = {"workload": f"{a.workload}_{a.tuples}", "checks": len(roots), "checks_per_s": round(len(roots) * a.steps / dt, 1),
            "ms_per_step": round(dt / a.steps * 1e3, 4), "main_kernel_ms": round(rs["main_ms"], 4),
            "main_bytes": rs["main_bytes"], "spilled_units": rs["spilled_units"],
@@ -111,6 +125,7 @@ def main():
            "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
                            "against": f"{other} engine, same snapshot"},
            "plan": check_plan(rs["plan"]),
+           "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
            "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}
     print(json.dumps(out), flush=True)
