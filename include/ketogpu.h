@@ -48,8 +48,18 @@ extern "C" {
 #define KETOGPU_NODE_NONE 0xFFFFFFFFu /* no such node / root with no tuples      */
 
 /* builder flags */
-#define KETOGPU_BUILD_SORT 1u /* rows are NOT in ORDER BY order: sort them with SQLite
-                                  semantics (NULLs first, BINARY collation) */
+#define KETOGPU_BUILD_SORT 1u /* rows are NOT in ORDER BY order: sort them with the
+                                  snapshot's row order (below) */
+/* Row order of the backend the rows come from.  The ORDER BY of
+ * relationtuples.go:215 is executed by the backend, and only NULL placement and string
+ * collation differ between backends: SQLite (tests, default), MySQL with a binary
+ * collation and CockroachDB put NULLs first; Postgres puts NULLs last — so a Postgres
+ * group lists its subject-id rows (subject_id NOT NULL) before its subject-set rows.
+ * Strings compare bytewise in both orders (SQLite BINARY, MySQL *_bin, Postgres "C"
+ * collation, CockroachDB).  Locale collations are not modelled (expand order under them is
+ * unpinned).  The order only matters where the library itself places rows: sorting
+ * (KETOGPU_BUILD_SORT) and ketogpu_snapshot_apply; rows appended in order are kept. */
+#define KETOGPU_ORDER_NULLS_LAST 2u /* Postgres ORDER BY (NULLS LAST, C collation) */
 
 typedef struct ketogpu_builder ketogpu_builder;
 typedef struct ketogpu_snapshot ketogpu_snapshot;
@@ -123,7 +133,7 @@ int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats
  * rows with one TransactRelationTuples batch applied (internal/persistence/sql/
  * relationtuples.go:271-278): inserts join their group after equal rows (commit_time
  * order), then every row matching a delete is removed (:178-201).  Row order follows
- * the SQLite semantics of KETOGPU_BUILD_SORT.  The base stays valid; engines built on
+ * the base snapshot's row order (KETOGPU_ORDER_*).  The base stays valid; engines built on
  * the new version answer with the write applied.  inserts/deletes may be NULL. */
 int ketogpu_snapshot_apply(const ketogpu_snapshot *base, const ketogpu_row_batch *inserts,
                            const ketogpu_row_batch *deletes, ketogpu_snapshot **out);

@@ -14,6 +14,8 @@ OK, ENOTFOUND, EINVAL, EDEVICE, ENOMEM = 0, 1, 2, 3, 4
 SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
 NODE_NONE = 0xFFFFFFFF
 BUILD_SORT = 1
+ORDER_NULLS_LAST = 2  # Postgres row order (include/ketogpu.h KETOGPU_ORDER_NULLS_LAST)
+ORDERS = {"sqlite": 0, "mysql-bin": 0, "cockroach": 0, "postgres": ORDER_NULLS_LAST}
 NODE_UNION, NODE_LEAF = 0, 1
 
 

@@ -134,6 +134,7 @@ struct Snapshot {
     // ---- configuration
     std::vector<Namespace> namespaces;  // config order, unique names and ids
     int page_size = 100;
+    bool nulls_last = false;            // KETOGPU_ORDER_NULLS_LAST: the backend's row order
     int32_t empty_name_ns = 0;          // id of the namespace named "" (if has_empty_name_ns)
     bool has_empty_name_ns = false;
 

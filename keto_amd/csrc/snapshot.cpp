@@ -250,9 +250,13 @@ inline std::string_view col(const char *data, const uint64_t *off, size_t i) {
     return std::string_view(data + off[i], off[i + 1] - off[i]);
 }
 
-// SQLite ORDER BY semantics for KETOGPU_BUILD_SORT (NULLs first, BINARY collation)
+// The backend's ORDER BY (relationtuples.go:215) for KETOGPU_BUILD_SORT and apply: bytewise
+// strings; NULLs first (SQLite, MySQL binary collations, CockroachDB) or last (Postgres,
+// KETOGPU_ORDER_NULLS_LAST).  Only subject_id is NULL for some rows of a group (subject-set
+// rows), so NULL placement decides whether subject sets or subject ids come first.
 struct SortCmp {
     const StrPool &p;
+    bool nulls_last = false;
     int cs(uint32_t a, uint32_t b) const {
         if (a == b) return 0;
         std::string_view x = p.get(a), y = p.get(b);
@@ -265,7 +269,7 @@ struct SortCmp {
         int c;
         if ((c = cs(a.obj, b.obj))) return c < 0;
         if ((c = cs(a.rel, b.rel))) return c < 0;
-        if (a.kind != b.kind) return a.kind > b.kind;  // subject sets (NULL subject_id) first
+        if (a.kind != b.kind) return nulls_last ? a.kind < b.kind : a.kind > b.kind;  // NULL subject_id = set row
         if (!a.kind) {
             if ((c = cs(a.sid, b.sid))) return c < 0;
         } else {
@@ -280,7 +284,7 @@ struct SortCmp {
 void finish_snapshot(ketogpu_builder *b) {
     Snapshot &S = *b->s;
     if (b->flags & KETOGPU_BUILD_SORT) {
-        std::stable_sort(b->raw.begin(), b->raw.end(), SortCmp{S.pool});
+        std::stable_sort(b->raw.begin(), b->raw.end(), SortCmp{S.pool, S.nulls_last});
         for (auto &r : b->raw) b->add(r.ns, r.obj, r.rel, r.kind, r.sid, r.ss_ns, r.ss_obj, r.ss_rel);
         std::vector<ketogpu_builder::RawRow>().swap(b->raw);
     }
@@ -494,7 +498,10 @@ int ketogpu_builder_new(const ketogpu_namespace *namespaces, size_t num_namespac
         if (opts) {
             if (opts->page_size < 0) throw Error(KETOGPU_EINVAL, "negative page size");
             if (opts->page_size) S.page_size = opts->page_size;
+            if (opts->flags & ~(KETOGPU_BUILD_SORT | KETOGPU_ORDER_NULLS_LAST))
+                throw Error(KETOGPU_EINVAL, "unknown builder flags");
             b->flags = opts->flags;
+            S.nulls_last = (opts->flags & KETOGPU_ORDER_NULLS_LAST) != 0;
         }
         *out = b.release();
         return KETOGPU_OK;
@@ -590,9 +597,9 @@ void ketogpu_builder_free(ketogpu_builder *b) { delete b; }
 // inserted rows join their group after equal rows (commit_time is the last ORDER BY key,
 // :215; InsertRelationTuple stamps time.Now(), :128-149), then every row matching a
 // delete (namespace id, object, relation, subject) is removed, duplicates included
-// (DeleteRelationTuples, :178-201).  The merge uses the SQLite ORDER BY semantics of
-// KETOGPU_BUILD_SORT; a base read in another backend's order fails loudly (EINVAL) when
-// the merged stream is not grouped.  O(rows) on the host: the new version is complete
+// (DeleteRelationTuples, :178-201).  The merge uses the base's row order (KETOGPU_ORDER_*,
+// the order of KETOGPU_BUILD_SORT); a base whose rows are not in that order fails loudly
+// (EINVAL) when the merged stream is not grouped.  O(rows) on the host: the new version is complete
 // and immutable, and engines swap to it (keto_amd/freshness.py).
 int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batch *inserts,
                            const ketogpu_row_batch *deletes, ketogpu_snapshot **out) {
@@ -602,7 +609,7 @@ int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batc
         const Snapshot &B = *reinterpret_cast<const Snapshot *>(basep);
         std::vector<ketogpu_namespace> nss;
         for (const Namespace &n : B.namespaces) nss.push_back(ketogpu_namespace{n.id, n.name.c_str()});
-        ketogpu_build_opts opts{B.page_size, 0};
+        ketogpu_build_opts opts{B.page_size, B.nulls_last ? KETOGPU_ORDER_NULLS_LAST : 0u};
         ketogpu_builder *raw_b = nullptr;
         int rc = ketogpu_builder_new(nss.data(), nss.size(), &opts, &raw_b);
         if (rc) return rc;
@@ -640,7 +647,7 @@ int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batc
             }
             return v;
         };
-        SortCmp cmp{S.pool};
+        SortCmp cmp{S.pool, S.nulls_last};
         std::vector<TupleRow> ins = rows_of(inserts, 1ull << 62), del = rows_of(deletes, 0);
         std::stable_sort(ins.begin(), ins.end(), cmp);
         for (auto &d : del) d.seq = 0;  // a delete matches every commit_time

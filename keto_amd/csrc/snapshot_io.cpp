@@ -17,7 +17,7 @@ using namespace ketogpu;
 namespace {
 
 constexpr char kMagic[8] = {'K', 'E', 'T', 'O', 'S', 'N', 'A', 'P'};
-constexpr uint32_t kFormat = 2;
+constexpr uint32_t kFormat = 3;  // 3: row order flag
 
 struct File {
     FILE *f = nullptr;
@@ -99,6 +99,7 @@ int ketogpu_snapshot_save(const ketogpu_snapshot *sp, const char *path) {
             f.put_str(n.name);
         }
         f.put<int32_t>(s.page_size);
+        f.put<uint8_t>(s.nulls_last);
         f.put<int32_t>(s.empty_name_ns);
         f.put<uint8_t>(s.has_empty_name_ns);
         f.put_pool(s.pool);
@@ -156,6 +157,7 @@ int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out) {
             s->namespaces.push_back(std::move(n));
         }
         s->page_size = f.get<int32_t>();
+        s->nulls_last = f.get<uint8_t>() != 0;
         s->empty_name_ns = f.get<int32_t>();
         s->has_empty_name_ns = f.get<uint8_t>() != 0;
         s->pool = StrPool();

@@ -18,6 +18,16 @@ from . import relationtuple as rt
 
 ORDER_BY = ("nid, namespace_id, object, relation, subject_id, subject_set_namespace_id, subject_set_object, "
             "subject_set_relation, commit_time")
+# Postgres executes the same ORDER BY with NULLs last (ASC); SQLite >= 3.30 states that
+# with NULLS LAST, so a SQLite table can serve rows in a Postgres ("C" collation) order.
+ORDER_BY_NULLS_LAST = ("nid, namespace_id, object, relation, subject_id NULLS LAST, "
+                       "subject_set_namespace_id NULLS LAST, subject_set_object NULLS LAST, "
+                       "subject_set_relation NULLS LAST, commit_time")
+
+
+def order_by(order="sqlite"):
+    """the ORDER BY clause of relationtuples.go:215 as backend `order` executes it"""
+    return ORDER_BY_NULLS_LAST if order == "postgres" else ORDER_BY
 
 SCHEMA = """
 CREATE TABLE IF NOT EXISTS keto_relation_tuples
@@ -52,12 +62,13 @@ class UnknownNamespace(LookupError):
 class TupleStore:
     """keto_relation_tuples of one network (nid) plus the namespace configuration."""
 
-    def __init__(self, namespaces, conn=None, nid=None, page_size=100):
+    def __init__(self, namespaces, conn=None, nid=None, page_size=100, order="sqlite"):
         self.conn = conn or sqlite3.connect(":memory:")
         self.conn.executescript(SCHEMA)
         self.namespaces = [(n, i) for n, i in namespaces]  # config order
         self.nid = nid or str(uuid.uuid4())
         self.page_size = page_size
+        self.order = order  # the backend whose row order reads emulate (order_by)
         self._ct = 0
 
     # namespace_memory.go:29-47 (first match)
@@ -100,7 +111,8 @@ class TupleStore:
         """the loader's single ordered read, as columnar batches (ketogpu_row_batch)"""
         cur = self.conn.execute(
             "SELECT namespace_id, object, relation, subject_id, subject_set_namespace_id, subject_set_object, "
-            f"subject_set_relation FROM keto_relation_tuples WHERE nid = ? ORDER BY {ORDER_BY}", (self.nid,))
+            f"subject_set_relation FROM keto_relation_tuples WHERE nid = ? ORDER BY {order_by(self.order)}",
+            (self.nid,))
         while True:
             rows = cur.fetchmany(batch_rows)
             if not rows:

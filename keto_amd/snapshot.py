@@ -26,11 +26,15 @@ def subject_struct(subject):
 
 
 class Snapshot:
-    def __init__(self, namespaces, page_size=100, sort=False):
+    """`order` names the backend whose ORDER BY the rows follow (include/ketogpu.h
+    KETOGPU_ORDER_*): "sqlite" (default), "mysql-bin", "cockroach" (NULLs first) or
+    "postgres" (NULLs last); it decides where sorting and apply() place rows."""
+
+    def __init__(self, namespaces, page_size=100, sort=False, order="sqlite"):
         self.L = L.lib()
         self.namespaces = [(n, int(i)) for n, i in namespaces]
         arr = (L.Namespace * max(len(self.namespaces), 1))(*[L.Namespace(i, L.b(n)) for n, i in self.namespaces])
-        opts = L.BuildOpts(page_size, L.BUILD_SORT if sort else 0)
+        opts = L.BuildOpts(page_size, (L.BUILD_SORT if sort else 0) | L.ORDERS[order])
         h = C.c_void_p()
         L.check(self.L.ketogpu_builder_new(arr, len(self.namespaces), C.byref(opts), C.byref(h)))
         self._builder = h
@@ -67,14 +71,14 @@ class Snapshot:
     # ---- constructors
     @classmethod
     def from_store(cls, store: persistence.TupleStore, batch_rows=1 << 16):
-        s = cls(store.namespaces, store.page_size)
+        s = cls(store.namespaces, store.page_size, order=getattr(store, "order", "sqlite"))
         for cols in store.iter_ordered_batches(batch_rows):
             s.append(cols)
         return s.finish()
 
     @classmethod
-    def from_rows(cls, namespaces, rows, page_size=100, sort=True):
-        s = cls(namespaces, page_size, sort=sort)
+    def from_rows(cls, namespaces, rows, page_size=100, sort=True, order="sqlite"):
+        s = cls(namespaces, page_size, sort=sort, order=order)
         if rows:
             s.append(persistence.columnar(rows))
         return s.finish()
@@ -84,8 +88,8 @@ class Snapshot:
         return cls.from_rows(namespaces, persistence.rows_from_tuples(namespaces, tuples), page_size, sort=True)
 
     @classmethod
-    def from_columns(cls, namespaces, cols, page_size=100, sort=False):
-        s = cls(namespaces, page_size, sort=sort)
+    def from_columns(cls, namespaces, cols, page_size=100, sort=False, order="sqlite"):
+        s = cls(namespaces, page_size, sort=sort, order=order)
         s.append(cols)
         return s.finish()
 

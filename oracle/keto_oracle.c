@@ -38,6 +38,7 @@ struct ko_store {
     char *arena;
     size_t arena_len, arena_cap;
     int page_size;
+    int nulls_last; /* Postgres ORDER BY: NULLs sort last (subject-set rows after subject ids) */
     int finalized;
 };
 
@@ -92,6 +93,7 @@ int ko_add_namespace(ko_store *s, int32_t id, const char *name) {
 }
 
 void ko_set_page_size(ko_store *s, int page_size) { s->page_size = page_size > 0 ? page_size : 100; }
+void ko_set_nulls_last(ko_store *s, int nulls_last) { s->nulls_last = nulls_last != 0; }
 
 static int add_row_len(ko_store *s, int32_t nsid, const char *obj, size_t lobj, const char *rel,
                        size_t lrel, int kind, const char *sid, size_t lsid, int32_t ssns,
@@ -154,13 +156,16 @@ int ko_add_rows_columnar(ko_store *s, size_t n, const int32_t *namespace_id,
  *          subject_set_object, subject_set_relation, commit_time
  * (relationtuples.go:215) with SQLite semantics: NULLs sort first, TEXT uses BINARY
  * collation (memcmp, shorter prefix first), INTEGER numerically.  A subject-set row has
- * subject_id NULL, a subject-id row has all subject_set_* NULL.  Ties keep insertion order. */
+ * subject_id NULL, a subject-id row has all subject_set_* NULL.  Ties keep insertion order.
+ * With nulls_last (Postgres ASC order under the "C" collation) NULLs sort last instead,
+ * which only moves a group's subject-set rows after its subject-id rows. */
 static int cmp_rows(const ko_store *s, const ko_row *a, const ko_row *b) {
     int c;
     if (a->ns_id != b->ns_id) return a->ns_id < b->ns_id ? -1 : 1;
     if ((c = strcmp(STR(s, a->obj), STR(s, b->obj)))) return c;
     if ((c = strcmp(STR(s, a->rel), STR(s, b->rel)))) return c;
-    if (a->kind != b->kind) return a->kind == KO_SUBJECT_SET ? -1 : 1; /* NULL subject_id first */
+    if (a->kind != b->kind) /* the NULL subject_id of a subject-set row */
+        return (a->kind == KO_SUBJECT_SET) != (s->nulls_last != 0) ? -1 : 1;
     if (a->kind == KO_SUBJECT_ID) {
         if ((c = strcmp(STR(s, a->sid), STR(s, b->sid)))) return c;
     } else {

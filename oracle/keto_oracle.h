@@ -52,6 +52,8 @@ void ko_store_free(ko_store *s);
 /* namespaces in configuration order (lookups take the first match) */
 int ko_add_namespace(ko_store *s, int32_t id, const char *name);
 void ko_set_page_size(ko_store *s, int page_size);
+/* row order of the backend: 0 SQLite (NULLs first, default), 1 Postgres (NULLs last) */
+void ko_set_nulls_last(ko_store *s, int nulls_last);
 /* one row of keto_relation_tuples; subject_id == NULL means a subject set */
 int ko_add_row(ko_store *s, int32_t namespace_id, const char *object, const char *relation,
                const char *subject_id, int32_t ss_namespace_id, const char *ss_object,

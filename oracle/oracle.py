@@ -32,6 +32,7 @@ def lib():
         L.ko_store_free.argtypes = [vp]
         L.ko_add_namespace.argtypes = [vp, i32, cp]
         L.ko_set_page_size.argtypes = [vp, C.c_int]
+        L.ko_set_nulls_last.argtypes = [vp, C.c_int]
         L.ko_add_row.argtypes = [vp, i32, cp, cp, cp, i32, cp, cp, i64]
         L.ko_add_rows_columnar.argtypes = [vp, C.c_size_t] + [vp] * 14
         L.ko_finalize.argtypes = [vp, C.c_int]
@@ -70,13 +71,16 @@ def subject_args(d):
 class Store:
     """keto_relation_tuples + namespace config, read through the reference's queries."""
 
-    def __init__(self, namespaces, page_size=100):
+    def __init__(self, namespaces, page_size=100, order="sqlite"):
+        """order: the backend whose ORDER BY is restated — "sqlite" (NULLs first, the
+        reference's tests) or "postgres" (NULLs last, "C" collation)"""
         self.L = lib()
         self.h = self.L.ko_store_new()
         self.namespaces = list(namespaces)  # [(name, id)] in config order
         for name, nid in self.namespaces:
             self.L.ko_add_namespace(self.h, nid, _b(name))
         self.L.ko_set_page_size(self.h, page_size)
+        self.L.ko_set_nulls_last(self.h, {"sqlite": 0, "postgres": 1}[order])
         self._ct = 0
 
     def __del__(self):

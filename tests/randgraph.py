@@ -81,12 +81,25 @@ def oracle_store_columns(namespaces, cols, page_size=100, presorted=True):
     return st.finalize(presorted=presorted)
 
 
-def oracle_store(namespaces, rows, page_size=100):
+def oracle_store(namespaces, rows, page_size=100, order="sqlite"):
     from oracle import oracle as O
-    st = O.Store(namespaces, page_size)
+    st = O.Store(namespaces, page_size, order=order)
     for (ns, o, r, sid, sns, so, sr) in rows:
         if sid is not None:
             st.add_row(ns, o, r, subject_id=sid)
         else:
             st.add_row(ns, o, r, ss_ns_id=sns, ss_obj=so, ss_rel=sr)
     return st.finalize()
+
+
+def backend_sorted(rows, order="sqlite"):
+    """rows as the backend returns them for the reference's ORDER BY (relationtuples.go:215),
+    bytewise strings; NULLs first (sqlite) or last (postgres).  Stable: equal rows keep
+    their insertion (commit_time) order."""
+    def key(r):
+        ns, o, rel, sid, sns, so, sr = r
+        null_sid = sid is None
+        first = null_sid if order == "postgres" else not null_sid  # False sorts first
+        return (ns, o.encode(), rel.encode(), first, (sid or "").encode(), sns or 0, (so or "").encode(),
+                (sr or "").encode())
+    return sorted(rows, key=key)

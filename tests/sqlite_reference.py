@@ -24,6 +24,7 @@ class SqliteReference:
         self.db = db
         self.conn = db.conn
         self.page_size = db.page_size
+        self.order = getattr(db, "order", "sqlite")
 
     # internal/driver/config/namespace_memory.go:29-47
     def ns_by_name(self, name):
@@ -55,7 +56,8 @@ class SqliteReference:
         ps = self.page_size
         rows = self.conn.execute(
             f"SELECT namespace_id, object, relation, subject_id, subject_set_namespace_id, subject_set_object, "
-            f"subject_set_relation FROM keto_relation_tuples WHERE {w} ORDER BY {ORDER} LIMIT ? OFFSET ?",
+            f"subject_set_relation FROM keto_relation_tuples WHERE {w} ORDER BY {persistence.order_by(self.order)} "
+            f"LIMIT ? OFFSET ?",
             args + [ps, (page - 1) * ps]).fetchall()
         total_pages = (total + ps - 1) // ps
         has_next = page < total_pages
