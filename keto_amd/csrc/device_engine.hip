@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kBlock) void seed_dynamic_kernel(DevGraph g, DevSta
         if (app) {
             uint64_t pos = atomicAdd(ctr1, (unsigned long long)((1ull << kCntShift) | deg));
             uint64_t idx = base1 + (pos >> kCntShift);
+            if ((pos & kPreMask) + deg > kPreMask) atomicOr(s.overflow, 1u);  // prefix carry
             if (idx < s.fe_cap) {
                 s.fe_key[idx] = key;
                 s.fe_pre[idx] = pos & kPreMask;
@@ -2103,12 +2104,15 @@ struct ketogpu_engine {
         budget = std::min<uint64_t>(budget, (uint64_t)free_b * 3 / 4);
         // frontier lists: 24 B per entry, touch list 8 B; vis+nxt: 16 B per (word, node)
         uint64_t lists = std::min<uint64_t>(budget / 4, (uint64_t)24 << 30);
-        st.fe_cap = std::max<uint64_t>(lists / 32, 1 << 16);
+        st.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 32, 1 << 16), kMaxListEntries);
         st.touch_cap = st.fe_cap;
         uint64_t per_word = 16ull * std::max<uint32_t>(s.Ni, 1);
         Wmax = std::max<uint64_t>(1, (budget - std::min(budget, lists)) / per_word);
         if (o && o->max_words_per_round) Wmax = std::min<uint64_t>(Wmax, o->max_words_per_round);
         Wmax = std::min<uint64_t>(Wmax, 1u << 20);
+        // a round appends each (word, node) pair at most once (plus its seeds), so a round of
+        // W <= fe_cap / (Ni + 64) words never overflows the lists (no retries at any degree)
+        Wmax = std::max<uint64_t>(1, std::min<uint64_t>(Wmax, st.fe_cap / ((uint64_t)s.Ni + 64)));
         size_t state = (size_t)Wmax * std::max<uint32_t>(s.Ni, 1);
         st.vis = dalloc<uint64_t>(state);
         owned.push_back(st.vis);

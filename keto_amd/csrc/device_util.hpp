@@ -10,6 +10,11 @@ namespace kdev {
 
 constexpr int kCntShift = 36;  // packed append counter: count << 36 | row-length prefix
 constexpr uint64_t kPreMask = (1ull << kCntShift) - 1;
+// Frontier lists appended through the packed counter must hold fewer than 2^28 entries:
+// the count field is 28 bits, and a list capacity at or above that lets the count wrap
+// before any append sees idx >= cap (an overflow nobody flags).  With capacity below it,
+// the first append past the end raises the overflow flag and the round is retried.
+constexpr uint64_t kMaxListEntries = (1ull << (64 - kCntShift)) - (1ull << 20);
 
 // 64-lane inclusive scan of a uint64 value
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -59,7 +64,11 @@ __device__ __forceinline__ void wave_append(bool want, uint64_t key, uint64_t de
     uint64_t total = __shfl(incl, 63, 64);
     if (!total) return;
     unsigned long long start = 0;
-    if (lane == 63) start = atomicAdd(ctr, (unsigned long long)total);
+    if (lane == 63) {
+        start = atomicAdd(ctr, (unsigned long long)total);
+        // a row-length prefix that carries into the count field corrupts both: flag it
+        if ((start & kPreMask) + (total & kPreMask) > kPreMask) atomicOr(overflow, 1u);
+    }
     start = __shfl(start, 63, 64);
     if (want) {
         uint64_t pos = start + incl - val;

@@ -426,12 +426,14 @@ struct ketogpu_part {
         uint64_t budget = o.state_budget_bytes ? o.state_budget_bytes : std::min<uint64_t>(free_b / 4, 32ull << 30);
         budget = std::min<uint64_t>(budget, (uint64_t)free_b / 2);
         uint64_t lists = budget / 4;
-        P.fe_cap = std::max<uint64_t>(lists / 32, 1 << 16);
+        P.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 32, 1 << 16), kMaxListEntries);
         P.touch_cap = P.fe_cap;
         P.ocap = o.record_capacity ? o.record_capacity : std::max<uint64_t>(lists / 16, 1 << 16);
         W = std::max<uint64_t>(1, (budget - std::min(budget, lists + P.ocap * 16)) / (16ull * std::max<uint32_t>(Nil, 1)));
         if (o.max_words_per_round) W = std::min<uint64_t>(W, o.max_words_per_round);
         W = std::min<uint64_t>(W, 1u << 16);
+        // each (word, owned node) pair is appended at most once per round (plus seeds)
+        W = std::max<uint64_t>(1, std::min<uint64_t>(W, P.fe_cap / ((uint64_t)Nil + 64)));
         const size_t state = (size_t)W * std::max<uint32_t>(Nil, 1);
         P.vis = own(palloc<uint64_t>(state));
         P.nxt = own(palloc<uint64_t>(state));
