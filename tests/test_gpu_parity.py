@@ -97,6 +97,22 @@ def test_global_path_matches_oracle(seed, collide, global_path):
     assert eng.last_stats()["ms_unit"] == 0.0
 
 
+def test_global_path_small_lists_power_law(global_path):
+    # a 1 MiB state budget leaves the minimum frontier lists (65536 entries), so the words
+    # per round are bounded by the list capacity (fe_cap / (Ni + 64)) on a graph whose
+    # closures are large (Zipf nesting): many rounds, every answer exact
+    from keto_amd import synth
+    w = synth.social(users=20000, groups=6000, tuples=150000, checks=6000, seed=13)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    roots, targets = w.resolve(snap)
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
+        w.requests(range(len(roots))), nthreads=8)
+    eng = check.Engine(snap, state_budget_bytes=1 << 20)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    st = eng.last_stats()
+    assert st["rounds"] > 1 and st["overflow_retries"] == 0
+
+
 def test_unit_spill_to_global_path():
     # both sides of the search are n nodes wide: top has n child groups g_i, the target
     # group T is a member of n groups p_i, and only g_7 -> p_7 connects them, so

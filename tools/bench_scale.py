@@ -66,8 +66,12 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--sample", type=int, default=100_000)
-    p.add_argument("--expand-sample", type=int, default=200, help="BuildTree roots timed per max-depth")
+    p.add_argument("--expand-sample", type=int, default=None,
+                   help="BuildTree roots timed per max-depth (default 200 for folders, config #3's expand; "
+                        "0 elsewhere: power-law groups expand into trees of millions of members)")
     a = p.parse_args()
+    if a.expand_sample is None:
+        a.expand_sample = 200 if a.workload == "folders" else 0
     threading.Thread(target=heartbeat, daemon=True).start()
     PHASE[0] = "generating"
     w = make(a.workload, a.tuples, a.checks)
@@ -99,18 +103,22 @@ def main():
     dt = time.perf_counter() - t0
     rs = eng.last_stats()
     got = q.download()
+    log(f"timed: {len(roots) * a.steps / dt:.4g} checks/s, {dt / a.steps * 1e3:.3f} ms/step, plan "
+        f"{check_plan(rs['plan'])}, spilled units {rs['spilled_units']}, spilled requests {rs['spilled_requests']}, "
+        f"positives denied {int((pos & ~got.astype(bool)).sum())}")
     PHASE[0] = "cross-checking"
     other = "v2" if rs["plan"] == 1 else "bidi"  # the plan the timed engine did not keep
     os.environ["KETOGPU_UNITS"] = other
     ref_eng = check.Engine(snap)
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
+    log(f"cross-check against the {other} engine: {int((ref != got[idx]).sum())} mismatches of {len(idx)}")
     PHASE[0] = "expand"
     from keto_amd import expand
     from keto_amd.relationtuple import SubjectSet
     xe = expand.Engine(snap)
     exp = {}
-    for depth in (3, 5, 10):  # config #3: expand at max-depth 3, 5, 10 (host DFS, R10)
+    for depth in (3, 5, 10) if expand_roots else ():  # config #3: expand at max-depth 3, 5, 10 (host DFS, R10)
         t0 = time.perf_counter()
         nodes = [xe.tree_size(SubjectSet(ns, o, r), depth) for ns, o, r in expand_roots]
         dt_e = time.perf_counter() - t0
