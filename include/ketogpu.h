@@ -276,10 +276,11 @@ typedef struct {
     double main_ms;             /* its device time (hipEvent)                     */
     int32_t plan;               /* first stage of the run: 0 global path only, 1 bidi,
                                  * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1.
-                                 * KETOGPU_UNITS=auto (default) tries bidi and v2 on the
-                                 * first two batches of >= 65536 requests, then keeps the
-                                 * faster; those two calls run both (same results)     */
-    uint32_t reserved;
+                                 * KETOGPU_UNITS=auto (default) tries bidi (128- and 64-
+                                 * entry pending lists) and v2 on the first two batches of
+                                 * >= 65536 requests, then keeps the fastest; those two
+                                 * calls run every candidate (same results)              */
+    uint32_t plan_lists;        /* bidi: pending-list entries of the first stage        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

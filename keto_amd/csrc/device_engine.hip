@@ -1865,12 +1865,17 @@ struct ketogpu_engine {
     bool use_v2 = true;
     bool use_bidi = true;
     // plan "auto" (default): the first kTrialRuns batches of >= kTrialMin requests run
-    // both first stages (bidi, v2) back to back, each a complete evaluation, in
-    // alternating order; the engine then keeps the plan with the smaller summed time
+    // every candidate first stage back to back (each a complete evaluation, in rotating
+    // order); the engine then keeps the candidate with the smallest summed time
     static constexpr uint64_t kTrialMin = 1 << 16;
     static constexpr int kTrialRuns = 2;
     int trials_left = 0;
-    double trial_ms[2] = {0, 0};  // [0] v2, [1] bidi
+    struct Candidate {
+        bool bidi;
+        int hlog, bt, f, lf;  // bidi first-stage shape (BidiCfg)
+        double ms;
+    };
+    std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
     // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run on the spill stages
     struct BidiCfg {
@@ -2029,9 +2034,19 @@ struct ketogpu_engine {
         use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
         trials_left = p == "auto" && use_bidi ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
-        if (const char *bc = getenv("KETOGPU_BIDI")) {  // "hlog,threads,lists,load", e.g. "9,64,192,6"
+        const char *bc = getenv("KETOGPU_BIDI");  // "hlog,threads,lists,load", e.g. "9,64,192,6"
+        if (bc) {
             BidiCfg c = bidi_cfg;
             if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_cfg = c;
+        }
+        if (trials_left) {
+            // candidates: the bidi shape (128-entry lists), bidi with 64-entry lists (spills
+            // sooner: better where most units spill anyway, config #4), forward-only unit2
+            // (chains, config #3); an explicit KETOGPU_BIDI shape replaces the two bidi ones
+            const BidiCfg &c = bidi_cfg;
+            candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0});
+            if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
+            candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
         }
         if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
             std::vector<SpillStage> c;
@@ -2454,13 +2469,23 @@ struct ketogpu_engine {
     void run(ketogpu_queries &qq) {
         HIP_CHECK(hipSetDevice(device));
         if (trials_left && qq.n >= kTrialMin) {
-            const bool first_bidi = trials_left & 1;
-            for (int k = 0; k < 2; k++) {
-                use_bidi = first_bidi ^ (k == 1);
+            const size_t nc = candidates.size();
+            auto select = [&](const Candidate &c) {
+                use_bidi = c.bidi;
+                bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf};
+            };
+            for (size_t k = 0; k < nc; k++) {
+                Candidate &c = candidates[(k + (size_t)trials_left) % nc];  // rotate the order per trial
+                select(c);
                 run_once(qq);
-                trial_ms[use_bidi] += last.ms_total;
+                c.ms += last.ms_total;
             }
-            if (--trials_left == 0) use_bidi = trial_ms[1] <= trial_ms[0];
+            if (--trials_left == 0) {
+                size_t best = 0;
+                for (size_t k = 1; k < nc; k++)
+                    if (candidates[k].ms < candidates[best].ms) best = k;
+                select(candidates[best]);
+            }
             return;
         }
         run_once(qq);
@@ -2471,6 +2496,7 @@ struct ketogpu_engine {
         ketogpu_run_stats rs{};
         rs.checks = q.n;
         rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? 1 : use_v2 ? 2 : 4;
+        rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
