@@ -71,7 +71,22 @@ struct DevState {
     unsigned long long *ctr;          // [0..1] level counters (ping-pong), [2] touch count
     unsigned int *overflow;
     unsigned long long *stats;        // [0] pull rev entries examined
+    // hub index (nullptr: off): hub_of[v] (v < Nx) = hub number or NONE; hub_mask[v][k]
+    // (v < Ni) bit j = v in closure+(hub 64k + j); hub_reach[request][k] bit j = the
+    // request's search reached hub 64k + j (and did not expand it)
+    const uint32_t *hub_of;
+    const uint64_t *hub_mask;
+    uint64_t *hub_reach;
+    uint32_t hub_words;
 };
+
+// record that the requests in `bits` of word w reached hub h (its closure is in hub_mask)
+__device__ __forceinline__ void hub_reached(const DevState &s, uint32_t w, uint64_t bits, uint32_t h) {
+    for (uint64_t b = bits; b; b &= b - 1) {
+        const uint64_t req = (uint64_t)w * 64 + (uint64_t)(__ffsll((unsigned long long)b) - 1);
+        atomicOr((unsigned long long *)&s.hub_reach[req * s.hub_words + (h >> 6)], 1ull << (h & 63));
+    }
+}
 
 __device__ __forceinline__ bool bit_of(const uint32_t *bm, uint32_t i) { return (bm[i >> 5] >> (i & 31)) & 1u; }
 
@@ -87,6 +102,13 @@ __device__ __forceinline__ void push_one(const DevGraph &g, const DevState &s, u
     if (!newly) return;
     if (g.row_amb && bit_of(g.row_amb, u)) atomicOr((unsigned long long *)&flags[wglob], (unsigned long long)newly);
     uint64_t d = g.fint_off[u + 1] - g.fint_off[u];
+    if (s.hub_of) {  // a hub is visited but not expanded: its closure is looked up at the pull
+        const uint32_t h = s.hub_of[u];
+        if (h != KETOGPU_NODE_NONE) {
+            hub_reached(s, w, newly, h);
+            d = 0;
+        }
+    }
     if (d) {
         uint64_t o2 = atomicOr((unsigned long long *)&s.nxt[slot], (unsigned long long)newly);
         if (!o2) {
@@ -113,6 +135,13 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(DevGraph g, DevState s, co
             uint32_t w = (uint32_t)(i >> 6);
             mask = 1ull << (i & 63);
             if (g.row_amb && bit_of(g.row_amb, r)) atomicOr((unsigned long long *)&flags[(c0 + i) >> 6], mask);
+            if (s.hub_of && d) {  // X(r) = closure+(r) for a hub root: nothing to expand
+                const uint32_t h = s.hub_of[r];
+                if (h != KETOGPU_NODE_NONE) {
+                    hub_reached(s, w, mask, h);
+                    d = 0;
+                }
+            }
             if (d) {
                 want = true;
                 key = ((uint64_t)w << 32) | r;
@@ -254,10 +283,18 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(DevGraph g, DevState s, co
                 }
                 ok = lo < dyn_full_off[k + 1] && dyn_full[lo] == t;
             }
+            // hubs this request reached: v is in X(r) if some reached hub's closure holds it
+            const uint64_t *reach = s.hub_reach ? s.hub_reach + i * s.hub_words : nullptr;
+            bool any_hub = false;
+            for (uint32_t k = 0; reach && k < s.hub_words; k++) any_hub |= reach[k] != 0;
             for (uint64_t p = g.rev_off[t], pe = g.rev_off[t + 1]; p < pe && !ok; p++) {
                 uint32_t v = g.rev_col[p];
                 examined++;
                 if (v == r || (v < g.Ni && ((vrow[v] >> b) & 1ull))) ok = true;
+                if (!ok && any_hub && v < g.Ni) {
+                    const uint64_t *hm = s.hub_mask + (size_t)v * s.hub_words;
+                    for (uint32_t k = 0; k < s.hub_words && !ok; k++) ok = (hm[k] & reach[k]) != 0;
+                }
             }
         }
     }
@@ -274,6 +311,15 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(uint64_t *vis, uint32_t N
     if (i >= n) return;
     uint64_t k = keys[i];
     vis[(size_t)(k >> 32) * Ni + (uint32_t)k] = 0;
+}
+
+// hub index build: the closures of the round's requests (hubs w0*64 ...) into hub_mask
+__global__ __launch_bounds__(kBlock) void hub_mask_kernel(const uint64_t *vis, uint32_t Ni, uint64_t nw, uint32_t w0,
+                                                          uint32_t hub_words, uint64_t *hub_mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nw * Ni; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t w = i / Ni, v = i - w * Ni;
+        hub_mask[v * hub_words + w0 + w] = vis[i];
+    }
 }
 
 // ------------------------------------------------------- LDS unit traversal
@@ -1984,6 +2030,11 @@ struct ketogpu_engine {
     unsigned int *spill_count = nullptr;
 
     bool cascade_log = getenv("KETOGPU_CASCADE_LOG") != nullptr;  // per-stage spill counts on stderr
+    // hub index of the global path (build_hubs): hubs are the expandable nodes with the
+    // most interior successors; a search stops at a hub and the pull consults its closure
+    uint32_t n_hubs = 0, hub_words = 0;
+    uint64_t *hub_mask = nullptr;
+    double hub_build_ms = 0;
     hipEvent_t unit_end = nullptr;  // last event of the bidi cascade (already complete after its sync)
 
     hipEvent_t ev() {
@@ -2147,6 +2198,67 @@ struct ketogpu_engine {
         for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats}) owned.push_back(p);  // spill_count lives in st.stats
         HIP_CHECK(hipHostMalloc((void **)&h_ctr, 64 * sizeof(uint64_t), hipHostMallocDefault));
         HIP_CHECK(hipStreamSynchronize(stream));
+        build_hubs(s);
+    }
+
+    // Hub index of the global path.  KETOGPU_HUBS = number of hubs (0 = off); default 1024
+    // on graphs with >= 2^18 interior nodes whose largest interior row has >= 1024 entries
+    // (power-law nesting, BASELINE config #4), off otherwise.  Off with ambiguous keys: R4
+    // flags are raised by the rows a search reads, and a hub's closure is not read.  The
+    // closures are computed once per engine by the global path itself (hubs as roots).
+    void build_hubs(const Snapshot &s) {
+        uint64_t maxdeg = 0;
+        for (uint32_t v = 0; v < s.Nx; v++) maxdeg = std::max<uint64_t>(maxdeg, s.fint_off[v + 1] - s.fint_off[v]);
+        uint32_t want = s.Ni >= (1u << 18) && maxdeg >= 1024 ? 1024 : 0;
+        if (const char *e = getenv("KETOGPU_HUBS")) want = (uint32_t)std::max(0, atoi(e));
+        if (!want || s.has_ambiguous || !s.Ni) return;
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<uint32_t> cand;
+        for (uint32_t v = 0; v < s.Nx; v++)
+            if (s.fint_off[v + 1] - s.fint_off[v] >= 2) cand.push_back(v);
+        const uint32_t H = (uint32_t)std::min<size_t>(want, cand.size());
+        if (!H) return;
+        auto deg = [&](uint32_t v) { return s.fint_off[v + 1] - s.fint_off[v]; };
+        std::partial_sort(cand.begin(), cand.begin() + H, cand.end(), [&](uint32_t a, uint32_t b) {
+            return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
+        });
+        cand.resize(H);
+        std::vector<uint32_t> hub_of_h(s.Nx, KETOGPU_NODE_NONE);
+        for (uint32_t i = 0; i < H; i++) hub_of_h[cand[i]] = i;
+        hub_words = (H + 63) / 64;
+        // the closures: one request per hub (root = target = the hub), global path, no hubs
+        uint32_t *d_r = dupload(cand);
+        uint64_t *d_a = dalloc<uint64_t>(hub_words), *d_f = dalloc<uint64_t>(hub_words);
+        hub_mask = dalloc<uint64_t>((size_t)s.Ni * hub_words);
+        owned.push_back(hub_mask);
+        HIP_CHECK(hipMemsetAsync(hub_mask, 0, (size_t)s.Ni * hub_words * 8, stream));
+        HIP_CHECK(hipMemsetAsync(d_f, 0, hub_words * 8, stream));
+        Batch b;
+        b.roots = d_r;
+        b.targets = d_r;
+        b.n = H;
+        b.allowed = d_a;
+        b.flags = d_f;
+        ketogpu_run_stats rs{};
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> pe, qe;
+        ev_used = 0;
+        run_global(b, rs, pe, qe, true);
+        HIP_CHECK(hipStreamSynchronize(stream));
+        for (void *p : {(void *)d_r, (void *)d_a, (void *)d_f}) (void)hipFree(p);
+        st.hub_of = up_hub(hub_of_h);
+        st.hub_mask = hub_mask;
+        st.hub_reach = dalloc<uint64_t>((size_t)Wmax * 64 * hub_words);
+        owned.push_back(st.hub_reach);
+        st.hub_words = hub_words;
+        n_hubs = H;
+        hub_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (cascade_log) fprintf(stderr, "[hubs] %u hubs (largest row %llu) built in %.1f ms\n", H,
+                                 (unsigned long long)maxdeg, hub_build_ms);
+    }
+    const uint32_t *up_hub(const std::vector<uint32_t> &v) {
+        uint32_t *p = dupload(v);
+        owned.push_back(p);
+        return p;
     }
 
     // spill lists hold unit ids (at most one per request); spill_units has two halves
@@ -2368,11 +2480,14 @@ struct ketogpu_engine {
     // Global multi-word engine, one round over requests [c0, c0 + n) of batch q (c0 a
     // multiple of 64).  Returns false on list overflow (state is then dense-reset and
     // the caller splits the round).
+    // hub_w0 != NONE: hub index build — the requests are hubs 64*hub_w0 ..., their
+    // closures go to hub_mask instead of a pull
     bool round(const Batch &q, uint64_t c0, uint64_t n, ketogpu_run_stats &rs,
                std::vector<std::pair<hipEvent_t, hipEvent_t>> &push_ev,
-               std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev) {
+               std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev, uint32_t hub_w0 = KETOGPU_NODE_NONE) {
         const uint64_t W = (n + 63) / 64;
         const uint64_t wg0 = c0 / 64;
+        if (st.hub_reach) HIP_CHECK(hipMemsetAsync(st.hub_reach, 0, W * 64 * st.hub_words * 8, stream));
         HIP_CHECK(hipMemsetAsync(st.ctr, 0, 3 * sizeof(uint64_t), stream));
         HIP_CHECK(hipMemsetAsync(st.overflow, 0, sizeof(unsigned int), stream));
         *(uint64_t *)&h_ctr[3] = 0;
@@ -2429,12 +2544,17 @@ struct ketogpu_engine {
             HIP_CHECK(hipStreamSynchronize(stream));
             return false;
         }
-        hipEvent_t a = ev(), b = ev();
-        HIP_CHECK(hipEventRecord(a, stream));
-        KLAUNCH(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
-                           q.dyn_full_off, q.dyn_full, q.allowed);
-        HIP_CHECK(hipEventRecord(b, stream));
-        pull_ev.push_back({a, b});
+        if (hub_w0 != KETOGPU_NODE_NONE) {
+            KLAUNCH(hub_mask_kernel, dim3(std::min<uint64_t>(blocks_for(W * g.Ni), 4096)), dim3(kBlock), 0, stream,
+                    st.vis, g.Ni, W, hub_w0, hub_words, hub_mask);
+        } else {
+            hipEvent_t a = ev(), b = ev();
+            HIP_CHECK(hipEventRecord(a, stream));
+            KLAUNCH(pull_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, g, st, q.roots, q.targets, c0, n,
+                    q.dyn_full_off, q.dyn_full, q.allowed);
+            HIP_CHECK(hipEventRecord(b, stream));
+            pull_ev.push_back({a, b});
+        }
         // reset every visited entry recorded in this round (levels >= 1 and touch list)
         uint64_t first = level_begin.size() > 1 ? level_begin[1] : lb;
         if (lb > first)
@@ -2450,13 +2570,13 @@ struct ketogpu_engine {
     }
 
     void run_global(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &push_ev,
-                    std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev) {
+                    std::vector<std::pair<hipEvent_t, hipEvent_t>> &pull_ev, bool hub_build = false) {
         uint64_t words = (q.n + 63) / 64;
         uint64_t W = Wmax;
         for (uint64_t w0 = 0; w0 < words;) {
             uint64_t wn = std::min<uint64_t>(W, words - w0);
             uint64_t c0 = w0 * 64, n = std::min<uint64_t>(q.n - c0, wn * 64);
-            if (!round(q, c0, n, rs, push_ev, pull_ev)) {
+            if (!round(q, c0, n, rs, push_ev, pull_ev, hub_build ? (uint32_t)w0 : KETOGPU_NODE_NONE)) {
                 rs.overflow_retries++;
                 if (wn == 1) throw Error(KETOGPU_ENOMEM, "frontier list overflow for a single 64-request word");
                 W = std::max<uint64_t>(1, wn / 2);

@@ -113,6 +113,29 @@ def test_global_path_small_lists_power_law(global_path):
     assert st["rounds"] > 1 and st["overflow_retries"] == 0
 
 
+@pytest.mark.parametrize("hubs,words", [(64, 0), (256, 3), (1000, 0)])
+def test_global_path_hub_index(hubs, words, global_path, monkeypatch):
+    # the hub index (searches stop at hubs; the pull reads the hubs' closures) forced on
+    # small graphs: power-law nesting (hub roots, hubs inside closures, several build rounds)
+    # and random tables (wildcards, poisoned pages, dynamic roots)
+    from keto_amd import synth
+    monkeypatch.setenv("KETOGPU_HUBS", str(hubs))
+    w = synth.social(users=20000, groups=6000, tuples=150000, checks=8000, seed=17)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    roots, targets = w.resolve(snap)
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
+        w.requests(range(len(roots))), nthreads=8)
+    eng = check.Engine(snap, max_words_per_round=words)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    for seed in (61, 62):
+        namespaces, rows = randgraph.make_graph(seed, n_rows=900, n_obj=40, n_users=50, poison=True, empty_ns=True)
+        snap = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
+        orc = randgraph.oracle_store(namespaces, rows, 4)
+        reqs = randgraph.make_requests(seed, namespaces, rows, n=1500)
+        got = check.Engine(snap, max_words_per_round=words).check_many(tuples_of(reqs))
+        assert got == [bool(x) for x in orc.check_batch(reqs)]
+
+
 def test_unit_spill_to_global_path():
     # both sides of the search are n nodes wide: top has n child groups g_i, the target
     # group T is a member of n groups p_i, and only g_7 -> p_7 connects them, so
