@@ -1920,6 +1920,7 @@ struct ketogpu_engine {
         bool bidi;
         int hlog, bt, f, lf;  // bidi first-stage shape (BidiCfg)
         double ms;
+        bool units = true;    // false: the global path alone (with the hub index)
     };
     std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
@@ -2083,7 +2084,7 @@ struct ketogpu_engine {
         if (use_v2 && s.fint_col.size() >= (1ull << 32)) use_v2 = false;  // record begins are u32
         // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
-        trials_left = p == "auto" && use_bidi ? kTrialRuns : 0;
+        trials_left = p == "auto" && use_bidi && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
         const char *bc = getenv("KETOGPU_BIDI");  // "hlog,threads,lists,load", e.g. "9,64,192,6"
         if (bc) {
@@ -2202,14 +2203,14 @@ struct ketogpu_engine {
     }
 
     // Hub index of the global path.  KETOGPU_HUBS = number of hubs (0 = off); default 1024
-    // on graphs with >= 2^18 interior nodes whose largest interior row has >= 1024 entries
-    // (power-law nesting, BASELINE config #4), off otherwise.  Off with ambiguous keys: R4
+    // on graphs with >= 1024 interior nodes whose largest interior row has >= 64 entries
+    // (128 B of HBM per interior node; a few ms to build), off otherwise.  Off with ambiguous keys: R4
     // flags are raised by the rows a search reads, and a hub's closure is not read.  The
     // closures are computed once per engine by the global path itself (hubs as roots).
     void build_hubs(const Snapshot &s) {
         uint64_t maxdeg = 0;
         for (uint32_t v = 0; v < s.Nx; v++) maxdeg = std::max<uint64_t>(maxdeg, s.fint_off[v + 1] - s.fint_off[v]);
-        uint32_t want = s.Ni >= (1u << 18) && maxdeg >= 1024 ? 1024 : 0;
+        uint32_t want = s.Ni >= 1024 && maxdeg >= 64 ? 1024 : 0;
         if (const char *e = getenv("KETOGPU_HUBS")) want = (uint32_t)std::max(0, atoi(e));
         if (!want || s.has_ambiguous || !s.Ni) return;
         auto t0 = std::chrono::steady_clock::now();
@@ -2254,6 +2255,9 @@ struct ketogpu_engine {
         hub_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (cascade_log) fprintf(stderr, "[hubs] %u hubs (largest row %llu) built in %.1f ms\n", H,
                                  (unsigned long long)maxdeg, hub_build_ms);
+        // with hubs, the multi-word global path alone is a candidate of the auto plan (on
+        // power-law graphs it beats the LDS stages, whose tables the big closures overflow)
+        if (trials_left && use_units) candidates.push_back({false, 0, 0, 0, 0, 0, false});
     }
     const uint32_t *up_hub(const std::vector<uint32_t> &v) {
         uint32_t *p = dupload(v);
@@ -2591,6 +2595,8 @@ struct ketogpu_engine {
         if (trials_left && qq.n >= kTrialMin) {
             const size_t nc = candidates.size();
             auto select = [&](const Candidate &c) {
+                use_units = c.units;
+                if (!c.units) return;
                 use_bidi = c.bidi;
                 bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf};
             };
