@@ -277,10 +277,15 @@ typedef struct {
     int32_t plan;               /* first stage of the run: 0 global path only, 1 bidi,
                                  * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1.
                                  * KETOGPU_UNITS=auto (default) tries bidi (128- and 64-
-                                 * entry pending lists) and v2 on the first two batches of
+                                 * entry pending lists), v2 and (with hubs) the global path
+                                 * alone on the first two batches of
                                  * >= 65536 requests, then keeps the fastest; those two
                                  * calls run every candidate (same results)              */
     uint32_t plan_lists;        /* bidi: pending-list entries of the first stage        */
+    uint32_t hubs;              /* hub index: hubs (0 = off); searches stop at hubs and
+                                 * read their precomputed closures (power-law graphs)   */
+    uint32_t hub_words;         /* 64-bit words per interior node of the hub closures   */
+    double hub_build_ms;        /* one-time hub closure build at engine creation        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

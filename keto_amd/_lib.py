@@ -82,7 +82,8 @@ class RunStats(C.Structure):
         ("push_launches", C.c_uint64), ("overflow_retries", C.c_uint64)] + [(n, C.c_uint64) for n in (
         "spilled_units", "unit_rows", "unit_edges", "unit_rev", "bytes_unit")] + [("ms_unit", C.c_double)] + [
         ("spilled_requests", C.c_uint64), ("unit_launches", C.c_uint64), ("main_bytes", C.c_uint64),
-        ("main_ms", C.c_double), ("plan", C.c_int32), ("plan_lists", C.c_uint32)]
+        ("main_ms", C.c_double), ("plan", C.c_int32), ("plan_lists", C.c_uint32),
+        ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double)]
 
     PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit"}
 

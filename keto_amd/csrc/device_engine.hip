@@ -60,6 +60,12 @@ struct DevGraph {
     const uint32_t *row_amb;  // nullptr when the snapshot has no ambiguous keys
     uint32_t Ni, Nx, N;
     uint32_t both_max, seed_max;  // bidi: both-sides and eager-seed thresholds (kBothMax, kSeedBothMax)
+    // hub index for the unit2 kernels (nullptr: off; see ketogpu_engine::build_hubs):
+    // hub_of[v] (v < Nx) = hub number or NONE, hub_mask[v][hub_words] (v < Ni) bit h = v is
+    // in the closure of hub h; forward edge records carry hub number + 1 in FRec::pad
+    const uint32_t *hub_of;
+    const uint64_t *hub_mask;
+    uint32_t hub_words;
 };
 
 struct DevState {
@@ -283,17 +289,22 @@ __global__ __launch_bounds__(kBlock) void pull_kernel(DevGraph g, DevState s, co
                 }
                 ok = lo < dyn_full_off[k + 1] && dyn_full[lo] == t;
             }
-            // hubs this request reached: v is in X(r) if some reached hub's closure holds it
-            const uint64_t *reach = s.hub_reach ? s.hub_reach + i * s.hub_words : nullptr;
-            bool any_hub = false;
-            for (uint32_t k = 0; reach && k < s.hub_words; k++) any_hub |= reach[k] != 0;
-            for (uint64_t p = g.rev_off[t], pe = g.rev_off[t + 1]; p < pe && !ok; p++) {
+            const uint64_t pb = g.rev_off[t], pe = g.rev_off[t + 1];
+            for (uint64_t p = pb; p < pe && !ok; p++) {
                 uint32_t v = g.rev_col[p];
                 examined++;
                 if (v == r || (v < g.Ni && ((vrow[v] >> b) & 1ull))) ok = true;
-                if (!ok && any_hub && v < g.Ni) {
-                    const uint64_t *hm = s.hub_mask + (size_t)v * s.hub_words;
-                    for (uint32_t k = 0; k < s.hub_words && !ok; k++) ok = (hm[k] & reach[k]) != 0;
+            }
+            // hubs this request reached: v is in X(r) if some reached hub's closure holds it.
+            // Only the non-zero words of the request's reach bitmap are compared.
+            const uint64_t *reach = s.hub_reach ? s.hub_reach + i * s.hub_words : nullptr;
+            for (uint32_t k = 0; reach && k < s.hub_words && !ok; k++) {
+                const uint64_t rk = reach[k];
+                if (!rk) continue;
+                for (uint64_t p = pb; p < pe && !ok; p++) {
+                    uint32_t v = g.rev_col[p];
+                    if (v >= g.Ni) break;  // rows are sorted: interior predecessors first
+                    ok = (s.hub_mask[(size_t)v * s.hub_words + k] & rk) != 0;
                 }
             }
         }
@@ -664,6 +675,7 @@ struct FRec {
 };
 constexpr int kFront = 512;  // frontier entries per level (spill beyond)
 constexpr int kRevCache = 16;
+constexpr int kHubList = 128;  // hubs a unit may reach (spill beyond)
 
 template <int U>
 struct Unit2Shared {
@@ -676,7 +688,11 @@ struct Unit2Shared {
     uint32_t root[U], target[U], rev_n[U];
     uint64_t rev_b[U];
     uint32_t rev_c[U][kRevCache];
-    uint32_t n_used, n_nxt, spill, res;
+    // hubs reached (hub index on): hub number, table slot (its visited bits are the
+    // requests that reached it) or 0xFFFF for a hub ROOT, whose requests are hub_bits
+    uint32_t hub_id[kHubList];
+    uint16_t hub_slot[kHubList], hub_bits[kHubList];
+    uint32_t n_used, n_nxt, spill, res, n_hub;
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
 };
 
@@ -737,13 +753,24 @@ __device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S,
         if (atomicAdd(&S.n_used, c) + c > (uint32_t)kHashMax) S.spill = 1;
     }
     bool app = false;
+    // a hub is visited but not expanded: the pull reads its closure from hub_mask
+    const bool hub = g.hub_mask && rc.pad;
+    if (inserted && hub) {
+        uint32_t j = atomicAdd(&S.n_hub, 1u);
+        if (j < (uint32_t)kHubList) {
+            S.hub_id[j] = rc.pad - 1;
+            S.hub_slot[j] = (uint16_t)h;
+        } else {
+            S.spill = 1;
+        }
+    }
     if (h >= 0) {
         uint32_t old = atomicOr(&S.st[h], m);
         uint32_t newly = m & ~old & 0xFFFFu;
         if (newly) {
             if (g.row_amb && bit_of(g.row_amb, u))
                 atomicOr((unsigned long long *)flag_word, (unsigned long long)newly << shift);
-            if (rc.deg) {
+            if (rc.deg && !hub) {
                 uint32_t o2 = atomicOr(&S.st[h], newly << 16);
                 app = !(o2 >> 16);
             }
@@ -822,11 +849,11 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
         S.st[i] = 0;
     }
     if (tid == 0) {
-        S.n_used = S.n_nxt = S.spill = S.res = 0;
+        S.n_used = S.n_nxt = S.spill = S.res = S.n_hub = 0;
         S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
     }
     uint64_t rows = 0, edges = 0, rev = 0;
-    if (tid < U) {
+    if (tid < U) {  // (the same wave as tid 0: its initialization above is visible here)
         // the request, its root row (seed) and its reverse row (pull): independent loads
         uint64_t c = c0 + tid;
         uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
@@ -844,6 +871,18 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
             rows += 2;
             if (g.row_amb && bit_of(g.row_amb, r))
                 atomicOr((unsigned long long *)flag_word, (unsigned long long)1 << (shift + tid));
+            const uint32_t hid = g.hub_mask ? g.hub_of[r] : KETOGPU_NODE_NONE;
+            if (hid != KETOGPU_NODE_NONE) {  // X(r) of a hub root is its closure: nothing to expand
+                fe = fb;
+                uint32_t j = atomicAdd(&S.n_hub, 1u);
+                if (j < (uint32_t)kHubList) {
+                    S.hub_id[j] = hid;
+                    S.hub_slot[j] = 0xFFFF;
+                    S.hub_bits[j] = (uint16_t)(1u << tid);
+                } else {
+                    S.spill = 1;
+                }
+            }
         }
         if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
         S.root[tid] = r;
@@ -912,6 +951,15 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
                 } else if (v < g.Ni) {
                     int s = key_lookup(S.key, v);
                     ok = s >= 0 && ((S.st[s] >> rj) & 1u);
+                    // v in the closure of a hub this request reached
+                    for (uint32_t j = 0, nh = S.n_hub; j < nh && !ok; j++) {
+                        const uint32_t hs = S.hub_slot[j];
+                        const uint32_t bits = hs == 0xFFFFu ? S.hub_bits[j] : S.st[hs];
+                        if ((bits >> rj) & 1u) {
+                            const uint32_t hid = S.hub_id[j];
+                            ok = (g.hub_mask[(size_t)v * g.hub_words + (hid >> 6)] >> (hid & 63)) & 1ull;
+                        }
+                    }
                 }
             }
         }
@@ -2031,8 +2079,8 @@ struct ketogpu_engine {
     unsigned int *spill_count = nullptr;
 
     bool cascade_log = getenv("KETOGPU_CASCADE_LOG") != nullptr;  // per-stage spill counts on stderr
-    // hub index of the global path (build_hubs): hubs are the expandable nodes with the
-    // most interior successors; a search stops at a hub and the pull consults its closure
+    // hub index (choose_hubs / build_hubs): hubs are the interior nodes with the most
+    // interior successors; a search stops at a hub and the pull consults its closure
     uint32_t n_hubs = 0, hub_words = 0;
     uint64_t *hub_mask = nullptr;
     double hub_build_ms = 0;
@@ -2141,11 +2189,14 @@ struct ketogpu_engine {
                 if (s.fint_off[v + 1] > s.fint_off[v]) hk[v >> 5] |= 1u << (v & 31);
             has_kids = up(hk);
         }
+        choose_hubs(s);
         if (use_v2) {
             std::vector<FRec> rec(s.fint_col.size());
             for (size_t e = 0; e < rec.size(); e++) {
                 uint32_t u = s.fint_col[e];
-                rec[e] = FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u], 0};
+                const uint32_t hid = hub_of_h.empty() ? KETOGPU_NODE_NONE : hub_of_h[u];
+                rec[e] = FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u],
+                              hid == KETOGPU_NODE_NONE ? 0u : hid + 1};
             }
             frec = up(rec);
         }
@@ -2173,7 +2224,8 @@ struct ketogpu_engine {
         uint64_t lists = std::min<uint64_t>(budget / 4, (uint64_t)24 << 30);
         st.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 32, 1 << 16), kMaxListEntries);
         st.touch_cap = st.fe_cap;
-        uint64_t per_word = 16ull * std::max<uint32_t>(s.Ni, 1);
+        // per 64-request word: vis + nxt rows and the requests' hub reach bitmaps
+        uint64_t per_word = 16ull * std::max<uint32_t>(s.Ni, 1) + 64ull * 8 * hub_words;
         Wmax = std::max<uint64_t>(1, (budget - std::min(budget, lists)) / per_word);
         if (o && o->max_words_per_round) Wmax = std::min<uint64_t>(Wmax, o->max_words_per_round);
         Wmax = std::min<uint64_t>(Wmax, 1u << 20);
@@ -2202,33 +2254,54 @@ struct ketogpu_engine {
         build_hubs(s);
     }
 
-    // Hub index of the global path.  KETOGPU_HUBS = number of hubs (0 = off); default 1024
-    // on graphs with >= 1024 interior nodes whose largest interior row has >= 64 entries
-    // (128 B of HBM per interior node; a few ms to build), off otherwise.  Off with ambiguous keys: R4
-    // flags are raised by the rows a search reads, and a hub's closure is not read.  The
-    // closures are computed once per engine by the global path itself (hubs as roots).
-    void build_hubs(const Snapshot &s) {
-        uint64_t maxdeg = 0;
-        for (uint32_t v = 0; v < s.Nx; v++) maxdeg = std::max<uint64_t>(maxdeg, s.fint_off[v + 1] - s.fint_off[v]);
-        uint32_t want = s.Ni >= 1024 && maxdeg >= 64 ? 1024 : 0;
-        if (const char *e = getenv("KETOGPU_HUBS")) want = (uint32_t)std::max(0, atoi(e));
-        if (!want || s.has_ambiguous || !s.Ni) return;
-        auto t0 = std::chrono::steady_clock::now();
+    // Hub index.  Hubs are the interior nodes with the most interior successors; a search
+    // (global path, unit2 kernels) marks a hub visited but does not expand it, and the pull
+    // finds v in X(r) when v is in the closure of a hub the request reached (hub_mask,
+    // precomputed once per engine).  On power-law nesting (BASELINE config #4) the closures
+    // of popular groups cover most of the graph, while the search that stops at the hubs
+    // stays small: with every interior node of >= kHubDeg interior successors a hub, the
+    // non-hub branching factor drops below one.  KETOGPU_HUBS = number of hubs (0 = off);
+    // default: on for graphs with >= 1024 interior nodes and an interior row of >= 64
+    // entries, H = those nodes rounded up to 64, at most 65536 and at most 1/8 of free HBM
+    // for hub_mask (Ni * H / 8 bytes).  Off with ambiguous keys: R4 flags are raised by the
+    // rows a search reads, and a hub's closure is not read.
+    static constexpr uint64_t kHubDeg = 8;
+    std::vector<uint32_t> hub_nodes, hub_of_h;
+    void choose_hubs(const Snapshot &s) {
+        if (s.has_ambiguous || !s.Ni) return;
+        auto deg = [&](uint32_t v) { return s.fint_off[v + 1] - s.fint_off[v]; };
+        uint64_t maxdeg = 0, heavy = 0;
+        for (uint32_t v = 0; v < s.Ni; v++) {
+            maxdeg = std::max<uint64_t>(maxdeg, deg(v));
+            heavy += deg(v) >= kHubDeg;
+        }
+        uint64_t want = s.Ni >= 1024 && maxdeg >= 64 ? std::min<uint64_t>((heavy + 63) / 64 * 64, 65536) : 0;
+        if (const char *e = getenv("KETOGPU_HUBS")) want = (uint64_t)std::max(0, atoi(e));
+        size_t free_b = 0, total_b = 0;
+        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        want = std::min<uint64_t>(want, (uint64_t)free_b / 8 / ((uint64_t)s.Ni * 8) * 64);
+        if (!want) return;
         std::vector<uint32_t> cand;
-        for (uint32_t v = 0; v < s.Nx; v++)
-            if (s.fint_off[v + 1] - s.fint_off[v] >= 2) cand.push_back(v);
+        for (uint32_t v = 0; v < s.Ni; v++)
+            if (deg(v) >= 2) cand.push_back(v);
         const uint32_t H = (uint32_t)std::min<size_t>(want, cand.size());
         if (!H) return;
-        auto deg = [&](uint32_t v) { return s.fint_off[v + 1] - s.fint_off[v]; };
         std::partial_sort(cand.begin(), cand.begin() + H, cand.end(), [&](uint32_t a, uint32_t b) {
             return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
         });
         cand.resize(H);
-        std::vector<uint32_t> hub_of_h(s.Nx, KETOGPU_NODE_NONE);
+        hub_of_h.assign(s.Nx, KETOGPU_NODE_NONE);
         for (uint32_t i = 0; i < H; i++) hub_of_h[cand[i]] = i;
+        hub_nodes = std::move(cand);
         hub_words = (H + 63) / 64;
-        // the closures: one request per hub (root = target = the hub), global path, no hubs
-        uint32_t *d_r = dupload(cand);
+    }
+    // the hub closures: one request per hub (root = target = the hub) on the global path
+    // with the hub index still off; vis rows are copied into hub_mask per round
+    void build_hubs(const Snapshot &s) {
+        const uint32_t H = (uint32_t)hub_nodes.size();
+        if (!H) return;
+        auto t0 = std::chrono::steady_clock::now();
+        uint32_t *d_r = dupload(hub_nodes);
         uint64_t *d_a = dalloc<uint64_t>(hub_words), *d_f = dalloc<uint64_t>(hub_words);
         hub_mask = dalloc<uint64_t>((size_t)s.Ni * hub_words);
         owned.push_back(hub_mask);
@@ -2251,10 +2324,16 @@ struct ketogpu_engine {
         st.hub_reach = dalloc<uint64_t>((size_t)Wmax * 64 * hub_words);
         owned.push_back(st.hub_reach);
         st.hub_words = hub_words;
+        g.hub_of = st.hub_of;
+        g.hub_mask = hub_mask;
+        g.hub_words = hub_words;
         n_hubs = H;
         hub_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (cascade_log) fprintf(stderr, "[hubs] %u hubs (largest row %llu) built in %.1f ms\n", H,
-                                 (unsigned long long)maxdeg, hub_build_ms);
+        if (cascade_log)
+            fprintf(stderr, "[hubs] %u hubs (interior rows >= %llu entries: smallest hub row %llu) built in %.1f ms\n",
+                    H, (unsigned long long)kHubDeg,
+                    (unsigned long long)(s.fint_off[hub_nodes.back() + 1] - s.fint_off[hub_nodes.back()]), hub_build_ms);
+        std::vector<uint32_t>().swap(hub_of_h);
         // with hubs, the multi-word global path alone is a candidate of the auto plan (on
         // power-law graphs it beats the LDS stages, whose tables the big closures overflow)
         if (trials_left && use_units) candidates.push_back({false, 0, 0, 0, 0, 0, false});
@@ -2623,6 +2702,9 @@ struct ketogpu_engine {
         rs.checks = q.n;
         rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? 1 : use_v2 ? 2 : 4;
         rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
+        rs.hubs = n_hubs;
+        rs.hub_words = hub_words;
+        rs.hub_build_ms = hub_build_ms;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();

@@ -113,12 +113,18 @@ def test_global_path_small_lists_power_law(global_path):
     assert st["rounds"] > 1 and st["overflow_retries"] == 0
 
 
+@pytest.mark.parametrize("path", ["global", "v2"])
 @pytest.mark.parametrize("hubs,words", [(64, 0), (256, 3), (1000, 0)])
-def test_global_path_hub_index(hubs, words, global_path, monkeypatch):
+def test_hub_index(path, hubs, words, monkeypatch):
     # the hub index (searches stop at hubs; the pull reads the hubs' closures) forced on
-    # small graphs: power-law nesting (hub roots, hubs inside closures, several build rounds)
-    # and random tables (wildcards, poisoned pages, dynamic roots)
+    # small graphs, on the global path and in the unit2 kernels (whose spills continue on
+    # the global path, also with hubs): power-law nesting (hub roots, hubs inside closures,
+    # several build rounds) and random tables (wildcards, poisoned pages, dynamic roots)
     from keto_amd import synth
+    if path == "global":
+        monkeypatch.setenv("KETOGPU_PATH", "global")
+    else:
+        monkeypatch.setenv("KETOGPU_UNITS", "v2")
     monkeypatch.setenv("KETOGPU_HUBS", str(hubs))
     w = synth.social(users=20000, groups=6000, tuples=150000, checks=8000, seed=17)
     snap = Snapshot.from_columns(w.namespaces, w.columns)
@@ -127,6 +133,9 @@ def test_global_path_hub_index(hubs, words, global_path, monkeypatch):
         w.requests(range(len(roots))), nthreads=8)
     eng = check.Engine(snap, max_words_per_round=words)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    st = eng.last_stats()
+    assert 0 < st["hubs"] <= hubs
+    assert st["plan"] == (0 if path == "global" else 2)
     for seed in (61, 62):
         namespaces, rows = randgraph.make_graph(seed, n_rows=900, n_obj=40, n_users=50, poison=True, empty_ns=True)
         snap = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
@@ -134,6 +143,23 @@ def test_global_path_hub_index(hubs, words, global_path, monkeypatch):
         reqs = randgraph.make_requests(seed, namespaces, rows, n=1500)
         got = check.Engine(snap, max_words_per_round=words).check_many(tuples_of(reqs))
         assert got == [bool(x) for x in orc.check_batch(reqs)]
+
+
+def test_hub_index_default_on_power_law(monkeypatch):
+    # the default hub selection on a power-law graph: every interior node with >= 8
+    # interior successors is a hub; every plan answers as the oracle does
+    from keto_amd import synth
+    w = synth.social(users=20000, groups=6000, tuples=150000, checks=8000, seed=23)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    roots, targets = w.resolve(snap)
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
+        w.requests(range(len(roots))), nthreads=8)
+    for plan in ("bidi", "v2", "auto"):
+        monkeypatch.setenv("KETOGPU_UNITS", plan)
+        eng = check.Engine(snap)
+        for _ in range(3 if plan == "auto" else 1):
+            np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+        assert eng.last_stats()["hubs"] > 0
 
 
 def test_unit_spill_to_global_path():

@@ -109,6 +109,7 @@ def main():
     PHASE[0] = "cross-checking"
     other = "v2" if rs["plan"] == 1 else "bidi"  # the plan the timed engine did not keep
     os.environ["KETOGPU_UNITS"] = other
+    os.environ["KETOGPU_HUBS"] = "0"  # the other first stage, and no hub index: an independent evaluation
     ref_eng = check.Engine(snap)
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
@@ -131,7 +132,7 @@ def main():
            "spilled_requests": rs["spilled_requests"], "allowed_fraction": round(float(got.mean()), 4),
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
-                           "against": f"{other} engine, same snapshot"},
+                           "against": f"{other} engine without the hub index, same snapshot"},
            "plan": check_plan(rs["plan"]),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
