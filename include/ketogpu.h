@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 1
+#define KETOGPU_ABI_VERSION 2 /* 2: ketogpu_run_stats gained hubs, hub_words, hub_build_ms */
 
 #define KETOGPU_OK 0
 #define KETOGPU_ENOTFOUND 1 /* unknown namespace (herodot.ErrNotFound)              */

@@ -12,7 +12,7 @@ TAG=${1:-r01}
 shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-B="bench.py --no-cpu-baseline --steps 5 --warmup 2 $*"
+B="bench.py --no-cpu-baseline --parity sample --steps 5 --warmup 2 $*"
 KRX="bidi_kernel|unit2_kernel|expand_kernel|pull_kernel"
 echo "[profile] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B \
