@@ -196,7 +196,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
             "plan": plan + (f" ({st['plan_lists']}-entry lists)" if plan == "bidi" else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
-                                          "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total")},
+                                          "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
+                                          "hubs", "hub_build_ms")},
             "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(n, 1), 2),
             "allowed_fraction": round(float(allowed.mean()), 4),
             "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2), "h2d_queries": round(t_h2d, 4)},

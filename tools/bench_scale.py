@@ -133,7 +133,7 @@ def main():
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
                            "against": f"{other} engine without the hub index, same snapshot"},
-           "plan": check_plan(rs["plan"]),
+           "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
            "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}
