@@ -179,9 +179,13 @@ def main():
         cpu = None
         parity = None
         sql = None
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and world == 1:
             cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds, full=a.parity == "full")
             sql = sql_baseline(min(10.0, a.cpu_seconds))
+        elif not a.no_cpu_baseline:
+            # N > 1: the CPU baseline is timed at N = 1 only; rank 0's batch still gets a
+            # bounded parity sample against the oracle
+            _, parity = cpu_baseline(w, allowed, 3.0, full=False)
         pos = np.asarray(w.chk_pos, dtype=bool)
         parity = dict(parity or {}, constructed_positives=int(pos.sum()),
                       constructed_positives_denied=int((pos & ~allowed.astype(bool)).sum()))
