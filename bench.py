@@ -198,7 +198,7 @@ def main():
                        "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
                        "parallelism": f"query-shard x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
-            "plan": plan + (f" ({st['plan_lists']}-entry lists)" if plan == "bidi" else ""),
+            "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)" if plan == "bidi" else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
                                           "hubs", "hub_build_ms")},

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 2 /* 2: ketogpu_run_stats gained hubs, hub_words, hub_build_ms */
+#define KETOGPU_ABI_VERSION 2 /* 2: ketogpu_run_stats gained hubs, hub_words, hub_build_ms, plan_unit */
 
 #define KETOGPU_OK 0
 #define KETOGPU_ENOTFOUND 1 /* unknown namespace (herodot.ErrNotFound)              */
@@ -286,6 +286,7 @@ typedef struct {
                                  * read their precomputed closures (power-law graphs)   */
     uint32_t hub_words;         /* 64-bit words per interior node of the hub closures   */
     double hub_build_ms;        /* one-time hub closure build at engine creation        */
+    uint32_t plan_unit;         /* bidi: requests per first-stage unit (16 or 8)        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

@@ -83,7 +83,8 @@ class RunStats(C.Structure):
         "spilled_units", "unit_rows", "unit_edges", "unit_rev", "bytes_unit")] + [("ms_unit", C.c_double)] + [
         ("spilled_requests", C.c_uint64), ("unit_launches", C.c_uint64), ("main_bytes", C.c_uint64),
         ("main_ms", C.c_double), ("plan", C.c_int32), ("plan_lists", C.c_uint32),
-        ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double)]
+        ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double),
+        ("plan_unit", C.c_uint32)]
 
     PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit"}
 

@@ -1521,8 +1521,11 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
 // Otherwise persistent: the workgroups stride over the *in_count units listed in
 // parents (the previous stage's spills), so the stage is launched without the host
 // reading that count first.
-template <int U, int HLOG, int F, int BT, int LF>
-__global__ __launch_bounds__(BT) void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+// WPE > 1 asks the compiler for at least WPE waves per SIMD (VGPR budget 512 / WPE): with
+// 5 KB of LDS, 8-request units could run 32 per CU at WPE 8
+template <int U, int HLOG, int F, int BT, int LF, int WPE = 1>
+__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(WPE)))
+void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                   const uint32_t *roots, const uint32_t *targets, uint64_t n,
                                                   uint64_t *allowed, const uint32_t *parents,
                                                   const unsigned int *in_count, uint32_t fan, uint32_t *spill_out,
@@ -1969,25 +1972,32 @@ struct ketogpu_engine {
         int hlog, bt, f, lf;  // bidi first-stage shape (BidiCfg)
         double ms;
         bool units = true;    // false: the global path alone (with the hub index)
+        int u = 16;           // bidi: requests per first-stage unit
+        int wpe = 1;          // bidi: minimum waves per SIMD of the first stage
     };
     std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
     // (KETOGPU_BIDI="hlog,threads,lists,load"); spilled units re-run on the spill stages
     struct BidiCfg {
         int hlog, bt, f, lf;
-        bool operator==(const BidiCfg &o) const { return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf; }
+        int u = 16;   // requests per unit (16, or 8: half the LDS per unit)
+        int wpe = 1;  // minimum waves per SIMD asked of the compiler (bidi_kernel WPE)
+        bool operator==(const BidiCfg &o) const {
+            return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe;
+        }
     };
     BidiCfg bidi_cfg{9, 64, 128, 7};
 
     void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp) {
-#define KETO_BIDI(HL, F, BT, LF)                                                                                  \
-    if (c == BidiCfg{HL, BT, F, LF}) {                                                                           \
-        KLAUNCH((bidi_kernel<16, HL, F, BT, LF>), dim3(grid), dim3(BT), pad, stream, g, frec, brec,   \
-                           q.roots, q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp); \
+#define KETO_BIDI_U(U, HL, F, BT, LF, WPE)                                                                        \
+    if (c == BidiCfg{HL, BT, F, LF, U, WPE}) {                                                                   \
+        KLAUNCH((bidi_kernel<U, HL, F, BT, LF, WPE>), dim3(grid), dim3(BT), pad, stream, g, frec, brec,          \
+                q.roots, q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp);          \
         return;                                                                                                  \
     }
+#define KETO_BIDI(HL, F, BT, LF) KETO_BIDI_U(16, HL, F, BT, LF, 1)
         KETO_BIDI(11, 384, 256, 6)
         KETO_BIDI(10, 256, 256, 6)
         KETO_BIDI(10, 256, 64, 6)
@@ -2001,7 +2011,11 @@ struct ketogpu_engine {
         KETO_BIDI(8, 128, 64, 7)
         KETO_BIDI(8, 96, 64, 7)
         KETO_BIDI(8, 128, 64, 6)
+        KETO_BIDI_U(8, 8, 64, 64, 7, 1)
+        KETO_BIDI_U(8, 8, 64, 64, 7, 6)
+        KETO_BIDI_U(8, 8, 64, 64, 7, 8)
 #undef KETO_BIDI
+#undef KETO_BIDI_U
         throw Error(KETOGPU_EINVAL, "KETOGPU_BIDI: unsupported configuration");
     }
     // spill stages after the first bidi pass: U requests per unit, persistent grid
@@ -2137,14 +2151,16 @@ struct ketogpu_engine {
         const char *bc = getenv("KETOGPU_BIDI");  // "hlog,threads,lists,load", e.g. "9,64,192,6"
         if (bc) {
             BidiCfg c = bidi_cfg;
-            if (sscanf(bc, "%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf) >= 1) bidi_cfg = c;
+            if (sscanf(bc, "%d,%d,%d,%d,%d,%d", &c.hlog, &c.bt, &c.f, &c.lf, &c.u, &c.wpe) >= 1) bidi_cfg = c;
         }
         if (trials_left) {
             // candidates: the bidi shape (128-entry lists), bidi with 64-entry lists (spills
             // sooner: better where most units spill anyway, config #4), forward-only unit2
             // (chains, config #3); an explicit KETOGPU_BIDI shape replaces the two bidi ones
+            // (8-request units — 5 KB of LDS, KETOGPU_BIDI=8,64,64,7,8[,wpe] — measured slower on
+            // config #2: 0.48-0.53 vs 0.39 ms, profiles/r01/tune_u8.txt; not a candidate)
             const BidiCfg &c = bidi_cfg;
-            candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0});
+            candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0, true, c.u, c.wpe});
             if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
             candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
         }
@@ -2433,19 +2449,25 @@ struct ketogpu_engine {
                 // last table; one host synchronization for counts and statistics
                 hipEvent_t a = ev(), b = ev(), d = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
-                launch_bidi(bidi_cfg, (unsigned)units, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
+                const uint64_t bunits = (q.n + bidi_cfg.u - 1) / bidi_cfg.u;
+                launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                             st.stats, stamps);
                 HIP_CHECK(hipEventRecord(b, stream));
-                int cur = 0, u_prev = 16;
-                for (size_t k = 0; k < cascade.size(); k++) {
-                    const SpillStage sg = cascade[k];
+                // spill stages of no more requests per unit than the stage before (an 8-request
+                // first stage skips the 16-request stage w)
+                std::vector<SpillStage> stages;
+                for (const SpillStage &sg : cascade)
+                    if (sg.u <= (stages.empty() ? bidi_cfg.u : stages.back().u)) stages.push_back(sg);
+                int cur = 0, u_prev = bidi_cfg.u;
+                for (size_t k = 0; k < stages.size(); k++) {
+                    const SpillStage sg = stages[k];
                     launch_stage(sg, q, list[cur], &spill_count[k], (uint32_t)(u_prev / sg.u), list[cur ^ 1],
                                  &spill_count[k + 1], st.stats + 4 * kStatSlots);
                     cur ^= 1;
                     u_prev = sg.u;
                 }
                 HIP_CHECK(hipEventRecord(d, stream));
-                const size_t ns = cascade.size() + 1;
+                const size_t ns = stages.size() + 1;
                 KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
                 HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
                 HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, ns * sizeof(unsigned int), hipMemcpyDeviceToHost,
@@ -2458,7 +2480,7 @@ struct ketogpu_engine {
                 rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
                 const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
                 if (cascade_log) {
-                    fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)units);
+                    fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)bunits);
                     for (size_t k = 0; k < ns; k++) fprintf(stderr, " %u", cnt[k]);
                     fprintf(stderr, "\n");
                 }
@@ -2677,7 +2699,7 @@ struct ketogpu_engine {
                 use_units = c.units;
                 if (!c.units) return;
                 use_bidi = c.bidi;
-                bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf};
+                bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf, c.u, c.wpe};
             };
             for (size_t k = 0; k < nc; k++) {
                 Candidate &c = candidates[(k + (size_t)trials_left) % nc];  // rotate the order per trial
@@ -2702,6 +2724,7 @@ struct ketogpu_engine {
         rs.checks = q.n;
         rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? 1 : use_v2 ? 2 : 4;
         rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
+        rs.plan_unit = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.u : 0;
         rs.hubs = n_hubs;
         rs.hub_words = hub_words;
         rs.hub_build_ms = hub_build_ms;
