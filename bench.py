@@ -255,6 +255,8 @@ def main_partitioned(a, rank, world, local):
                "parity": {"sample": int(n_req), "mismatches": int((got != ref).sum()),
                           "against": "single-GPU engine"},
                "partition": {k: int(v) for k, v in st.items()},
+               "direction": {0: "forward", 1: "backward"}.get(eng.direction, "undecided"),
+               "direction_trials_ns_per_check": {{0: "forward", 1: "backward"}[k]: v for k, v in eng._trial.items()},
                "exchange": {"records": int(eng.records), "levels": int(eng.levels), "retries": int(eng.retries)}}
         print(json.dumps(out), flush=True)
     barrier(world)

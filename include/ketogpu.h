@@ -329,6 +329,14 @@ void ketogpu_part_free(ketogpu_part *p);
 uint64_t ketogpu_part_round_words(const ketogpu_part *p);
 /* same (roots, targets) host arrays on every rank, n <= 64 * round_words */
 int ketogpu_part_begin(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n);
+/* Same round, in a chosen direction (partition.hip header): KETOGPU_PART_FORWARD grows the
+ * roots' closures X(r) (what ketogpu_part_begin does), KETOGPU_PART_BACKWARD grows the
+ * targets' ancestor sets B(t) along interior-predecessor rows and pulls from the roots'
+ * rows.  Same answers; every rank must use the same direction in a round. */
+#define KETOGPU_PART_FORWARD 0
+#define KETOGPU_PART_BACKWARD 1
+int ketogpu_part_begin_dir(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n,
+                           int32_t direction);
 /* this step's outgoing records grouped by destination rank into send_dev; counts[world] */
 int ketogpu_part_emit(ketogpu_part *p, ketogpu_record *send_dev, uint64_t capacity, uint64_t *counts);
 /* OR received records into the owned state; *frontier = owned entries of the next level */

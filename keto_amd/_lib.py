@@ -163,6 +163,7 @@ SIGNATURES = {
     "ketogpu_part_free": (None, [vp]),
     "ketogpu_part_round_words": (C.c_uint64, [vp]),
     "ketogpu_part_begin": (C.c_int, [vp, vp, vp, sz]),
+    "ketogpu_part_begin_dir": (C.c_int, [vp, vp, vp, sz, C.c_int32]),
     "ketogpu_part_emit": (C.c_int, [vp, vp, C.c_uint64, vp]),
     "ketogpu_part_apply": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ketogpu_part_expand": (C.c_int, [vp]),

@@ -17,6 +17,15 @@
 //   end        this rank's hit bits; the answer is their OR over ranks
 // The check formula is the one the single-GPU engines use: allowed(r, t)
 // <=> r in rev(t) or rev(t) ∩ X(r) != {} with X(r) the interior closure of r.
+// A round runs in one of two directions (ketogpu_part_begin_dir), the same steps:
+//   forward    as above: the BFS grows X(r) from the roots' owners along forward interior
+//              rows; the pull asks whether an interior v in rev(t) is in X(r)
+//   backward   the BFS grows B(t) = interior nodes that reach t, seeded by the targets'
+//              owners with the interior entries of rev(t) (r in rev(t) is a hit there),
+//              along interior-predecessor rows; the pull sends (request, u) for u in
+//              fint(r) from the roots' owners: u in B(t) <=> r reaches t in >= 2 edges.
+// Which side is cheaper depends on the graph (RBAC: documents fan out to many groups, a
+// user reaches few); keto_amd/partition.py times both and keeps the faster.
 // Snapshots with ambiguous Subject.String() keys (R4) are refused: their exact
 // re-evaluation needs the whole graph on one host.
 #include <hip/hip_runtime.h>
@@ -58,6 +67,9 @@ struct PartDev {
     const uint32_t *lt;      // [N] local reverse row of an owned node or NONE
     const uint64_t *lr_off;  // [Ntl + 1] reverse rows of owned nodes (global ids, sorted)
     const uint32_t *lr_col;
+    const uint64_t *lb_off;  // [Nil + 1] interior predecessors of owned interior nodes (backward rows)
+    const uint32_t *lb_col;
+    uint32_t dir;            // round direction: 0 forward, 1 backward
     uint64_t *vis, *nxt;     // [W][Nil]
     uint64_t *fe_key, *fe_pre, *fe_mask;
     uint64_t fe_cap;
@@ -90,11 +102,45 @@ __device__ __forceinline__ void emit_rec(bool want, uint32_t a, uint32_t b, uint
     }
 }
 
-// owned roots: (word, u, bit) for every interior successor u
+// forward: owned roots, (word, u, bit) for every interior successor u.  Backward: owned
+// targets, r in rev(t) is a hit, (word, v, bit) for every interior v in rev(t).
 __global__ __launch_bounds__(kPB) void part_seed_kernel(PartDev P) {
     const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
     uint64_t b = 0, e = 0, m = 0;
     uint32_t w = 0;
+    if (P.dir) {
+        uint32_t r = KETOGPU_NODE_NONE;
+        if (i < P.n) {
+            const uint32_t t = P.targets[i];
+            r = P.roots[i];
+            if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
+                const uint32_t lt = P.lt[t];
+                if (lt != KETOGPU_NODE_NONE) {
+                    b = P.lr_off[lt];
+                    e = P.lr_off[lt + 1];
+                    w = (uint32_t)(i >> 6);
+                    m = 1ull << (i & 63);
+                }
+            }
+        }
+        bool hit = false;
+        for (uint64_t k = b;; k++) {
+            const bool more = k < e && !hit;
+            if (!__ballot(more)) break;
+            bool q = false;
+            uint32_t v = 0;
+            if (more) {
+                v = P.lr_col[k];
+                if (v == r)
+                    hit = true;
+                else
+                    q = v < P.Ni;
+            }
+            emit_rec(q, w, v, m, P);
+        }
+        if (hit) atomicOr((unsigned long long *)&P.allowed[i >> 6], 1ull << (i & 63));
+        return;
+    }
     if (i < P.n) {
         uint32_t r = P.roots[i], t = P.targets[i];
         if (r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE && r < P.Nx) {
@@ -157,7 +203,7 @@ __global__ __launch_bounds__(kPB) void part_expand_kernel(PartDev P, uint64_t en
                 w = (uint32_t)(k >> 32);
                 const uint32_t l = (uint32_t)k;
                 m = P.fe_mask[ent];
-                u = P.lf_col[P.lf_off[l] + (e - s_pre[lo])];
+                u = P.dir ? P.lb_col[P.lb_off[l] + (e - s_pre[lo])] : P.lf_col[P.lf_off[l] + (e - s_pre[lo])];
             }
             emit_rec(want, w, u, m, P);
         }
@@ -222,7 +268,7 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
                 const uint64_t newly = nw & ~old;
                 if (newly) {
                     key = ((uint64_t)r.a << 32) | l;
-                    const uint64_t d = P.lf_off[l + 1] - P.lf_off[l];
+                    const uint64_t d = P.dir ? P.lb_off[l + 1] - P.lb_off[l] : P.lf_off[l + 1] - P.lf_off[l];
                     if (d) {
                         const uint64_t o2 = atomicOr((unsigned long long *)&P.nxt[slot], (unsigned long long)newly);
                         if (!o2) {
@@ -252,11 +298,31 @@ __global__ __launch_bounds__(kPB) void part_gather_kernel(PartDev P, uint64_t b,
     P.nxt[slot] = 0;
 }
 
-// owned targets: direct hits (r in rev(t)) and queries (request, interior v in rev(t))
+// forward: owned targets, direct hits (r in rev(t)) and queries (request, interior v in
+// rev(t)).  Backward: owned roots, queries (request, u) for u in fint(r).
 __global__ __launch_bounds__(kPB) void part_pull_emit_kernel(PartDev P) {
     const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
     uint64_t b = 0, e = 0;
     uint32_t r = KETOGPU_NODE_NONE;
+    if (P.dir) {
+        if (i < P.n) {
+            const uint32_t t = P.targets[i];
+            r = P.roots[i];
+            if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
+                const uint32_t l = P.lx[r];
+                if (l != KETOGPU_NODE_NONE) {
+                    b = P.lf_off[l];
+                    e = P.lf_off[l + 1];
+                }
+            }
+        }
+        for (uint64_t k = b;; k++) {
+            const bool more = k < e;
+            if (!__ballot(more)) break;
+            emit_rec(more, (uint32_t)i, more ? P.lf_col[k] : 0, 0, P);
+        }
+        return;
+    }
     if (i < P.n) {
         const uint32_t t = P.targets[i];
         r = P.roots[i];
@@ -396,6 +462,15 @@ struct ketogpu_part {
             lf_col.insert(lf_col.end(), s.fint_col.begin() + s.fint_off[v], s.fint_col.begin() + s.fint_off[v + 1]);
             lf_off.push_back(lf_col.size());
         }
+        // backward rows: interior predecessors of owned interior nodes = the prefix of
+        // their (sorted) reverse rows below Ni
+        std::vector<uint64_t> lb_off{0};
+        std::vector<uint32_t> lb_col;
+        for (uint32_t l = 0; l < Nil; l++) {
+            const uint32_t *b = s.rev_col.data() + s.rev_off[order[l]], *e = s.rev_col.data() + s.rev_off[order[l] + 1];
+            lb_col.insert(lb_col.end(), b, std::lower_bound(b, e, s.Ni));
+            lb_off.push_back(lb_col.size());
+        }
         std::vector<uint32_t> lt(s.N, NONE);
         std::vector<uint64_t> lr_off{0};
         std::vector<uint32_t> lr_col;
@@ -416,6 +491,8 @@ struct ketogpu_part {
         P.lt = upload(lt);
         P.lr_off = upload(lr_off);
         P.lr_col = upload(lr_col);
+        P.lb_off = upload(lb_off);
+        P.lb_col = upload(lb_col);
         stats.owned_interior = Nil;
         stats.owned_expandable = order.size();
         stats.owned_forward_edges = lf_col.size();
@@ -464,8 +541,11 @@ struct ketogpu_part {
     }
     uint32_t overflow_bits() const { return (uint32_t)h[4]; }
 
-    void begin(const uint32_t *roots, const uint32_t *targets, uint64_t n) {
+    void begin(const uint32_t *roots, const uint32_t *targets, uint64_t n, int dir) {
+        if (dir != KETOGPU_PART_FORWARD && dir != KETOGPU_PART_BACKWARD)
+            throw Error(KETOGPU_EINVAL, "partition: direction must be KETOGPU_PART_FORWARD or _BACKWARD");
         if (dirty) reset(true);
+        P.dir = (uint32_t)dir;
         if (n > W * 64) throw Error(KETOGPU_EINVAL, "partition: more requests than one round holds");
         for (uint64_t i = 0; i < n; i++)
             if ((roots[i] != NONE && roots[i] >= P.Nx) || (targets[i] != NONE && targets[i] >= P.N))
@@ -637,7 +717,17 @@ int ketogpu_part_begin(ketogpu_part *p, const uint32_t *roots, const uint32_t *t
     if (!p || (n && (!roots || !targets))) throw Error(KETOGPU_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(p->mu);
     PHIP(hipSetDevice(p->device));
-    p->begin(roots, targets, n);
+    p->begin(roots, targets, n, KETOGPU_PART_FORWARD);
+    PAPI_END
+}
+
+int ketogpu_part_begin_dir(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n,
+                           int32_t direction) {
+    PAPI_BEGIN
+    if (!p || (n && (!roots || !targets))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    p->begin(roots, targets, n, direction);
     PAPI_END
 }
 

@@ -15,6 +15,8 @@ check.Engine.check_ids answers (the same reachability formula, R2: no depth cuto
 """
 import ctypes as C
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -35,6 +37,9 @@ def tensor_to_records(t):
     """int32 tensor (n, 4) -> (a, b, m) numpy arrays"""
     rec = np.ascontiguousarray(t.cpu().numpy()).view([("a", "<u4"), ("b", "<u4"), ("m", "<u8")]).reshape(-1)
     return rec["a"].copy(), rec["b"].copy(), rec["m"].copy()
+
+
+FORWARD, BACKWARD = 0, 1  # include/ketogpu.h KETOGPU_PART_FORWARD / _BACKWARD
 
 
 class DevicePartition:
@@ -58,10 +63,10 @@ class DevicePartition:
     def round_words(self):
         return int(self.L.ketogpu_part_round_words(self.h))
 
-    def begin(self, roots, targets):
+    def begin(self, roots, targets, direction=FORWARD):
         self._req = (np.ascontiguousarray(roots, dtype=np.uint32), np.ascontiguousarray(targets, dtype=np.uint32))
         r, t = self._req
-        L.check(self.L.ketogpu_part_begin(self.h, r.ctypes.data, t.ctypes.data, len(r)))
+        L.check(self.L.ketogpu_part_begin_dir(self.h, r.ctypes.data, t.ctypes.data, len(r), direction))
 
     def _pack(self, fn):
         rc = fn(self.h, self.send.data_ptr(), self.cap, self.counts.ctypes.data)
@@ -125,7 +130,14 @@ class PartitionedEngine:
     (roots, targets) and gets the full answer.  `local` is the rank's step implementation
     (DevicePartition by default)."""
 
-    def __init__(self, snapshot, device=0, group=None, local=None, **opts):
+    def __init__(self, snapshot, device=0, group=None, local=None, direction="auto", **opts):
+        """direction: "forward" (grow the roots' closures), "backward" (grow the targets'
+        ancestor sets) or "auto": the first two full rounds run one direction each, timed
+        (max over ranks, so every rank decides alike), and the faster is kept"""
+        if direction not in ("auto", "forward", "backward"):
+            raise ValueError("direction must be auto, forward or backward")
+        self.direction = {"forward": FORWARD, "backward": BACKWARD}.get(direction)
+        self._trial = {}  # direction -> ns per request of its trial round
         self.group = group
         if dist.is_available() and dist.is_initialized():
             self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
@@ -162,10 +174,10 @@ class PartitionedEngine:
         return recv
 
     # -------------------------------------------------------------------- rounds
-    def _round(self, roots, targets):
+    def _round(self, roots, targets, direction):
         """one round; None when a rank's buffers overflowed (every rank aborts)"""
         loc = self.local
-        loc.begin(roots, targets)
+        loc.begin(roots, targets, direction)
         while True:
             st, send, counts = loc.emit()
             if self._allreduce([st], dist.ReduceOp.MAX if self.world > 1 else None)[0]:
@@ -203,7 +215,16 @@ class PartitionedEngine:
         i = 0
         while i < n:
             m = min(per, n - i)
-            got = self._round(roots[i:i + m], targets[i:i + m])
+            d = self.direction
+            if d is None:  # auto: a trial round per direction, then the faster one
+                d = FORWARD if FORWARD not in self._trial else BACKWARD
+            t0 = time.perf_counter()
+            got = self._round(roots[i:i + m], targets[i:i + m], d)
+            if self.direction is None and got is not None:
+                ns = int((time.perf_counter() - t0) * 1e9 / max(m, 1))
+                self._trial[d] = self._allreduce([ns], dist.ReduceOp.MAX if self.world > 1 else None)[0]
+                if len(self._trial) == 2:
+                    self.direction = min(self._trial, key=lambda k: (self._trial[k], k))
             if got is None:
                 if m <= 64:
                     raise L.KetoError(L.ENOMEM, "partition buffers overflow for a single 64-request word")

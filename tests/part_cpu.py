@@ -47,15 +47,31 @@ class CpuPartition:
     def _own(self, v):
         return int(owner(v, self.world)) == self.rank
 
-    def begin(self, roots, targets):
+    def _ipred(self, v):
+        return [int(p) for p in self._rev(v) if p < self.Ni]
+
+    def _row(self, v):
+        """the BFS row of v in the round's direction"""
+        return self._ipred(v) if self.dir else [int(u) for u in self._fint(v)]
+
+    def begin(self, roots, targets, direction=0):
         self.roots, self.targets = [int(x) for x in roots], [int(x) for x in targets]
+        self.dir = direction
         self.vis = defaultdict(int)
         self.nxt = {}
         self.hits = set()
         self.out = []
         for i, (r, t) in enumerate(zip(self.roots, self.targets)):
-            if r != NONE and t != NONE and r < self.Nx and self._own(r):
+            if r == NONE or t == NONE or r >= self.Nx:
+                continue
+            if not direction and self._own(r):  # forward: seeds from the root's row
                 self.out += [(i >> 6, int(u), 1 << (i & 63)) for u in self._fint(r)]
+            elif direction and self._own(t):  # backward: r in rev(t) is a hit, interior entries seed
+                row = [int(x) for x in self._rev(t)]
+                if r in row:
+                    self.hits.add(i)
+                else:
+                    self.out += [(i >> 6, v, 1 << (i & 63)) for v in row if v < self.Ni]
 
     def _pack(self):
         out, self.out = self.out, []
@@ -79,18 +95,24 @@ class CpuPartition:
             new = mask & ~self.vis[(w, v)]
             if new:
                 self.vis[(w, v)] |= new
-                if len(self._fint(v)):
+                if len(self._row(v)):
                     self.nxt[(w, v)] = self.nxt.get((w, v), 0) | new
         return 0, len(self.nxt)
 
     def expand(self):
         nxt, self.nxt = self.nxt, {}
         for (w, v), mask in nxt.items():
-            self.out += [(w, int(u), mask) for u in self._fint(v)]
+            self.out += [(w, u, mask) for u in self._row(v)]
 
     def pull_emit(self):
         for i, (r, t) in enumerate(zip(self.roots, self.targets)):
-            if r == NONE or t == NONE or r >= self.Nx or not self._own(t):
+            if r == NONE or t == NONE or r >= self.Nx:
+                continue
+            if self.dir:  # backward: the root's owner asks whether u in fint(r) reaches t
+                if self._own(r):
+                    self.out += [(i, int(u), 0) for u in self._fint(r)]
+                continue
+            if not self._own(t):
                 continue
             row = [int(x) for x in self._rev(t)]
             if r in row:
