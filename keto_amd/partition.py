@@ -138,6 +138,7 @@ class PartitionedEngine:
             raise ValueError("direction must be auto, forward or backward")
         self.direction = {"forward": FORWARD, "backward": BACKWARD}.get(direction)
         self._trial = {}  # direction -> ns per request of its trial round
+        self._per = {FORWARD: 1 << 62, BACKWARD: 1 << 62}  # requests per round after overflow retries
         self.group = group
         if dist.is_available() and dist.is_initialized():
             self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
@@ -210,30 +211,46 @@ class PartitionedEngine:
         roots = np.ascontiguousarray(roots, dtype=np.uint32)
         targets = np.ascontiguousarray(targets, dtype=np.uint32)
         n = len(roots)
-        per = self._allreduce([self.local.round_words() * 64], dist.ReduceOp.MIN if self.world > 1 else None)[0]
+        top = self._allreduce([self.local.round_words() * 64], dist.ReduceOp.MIN if self.world > 1 else None)[0]
         out = np.zeros(n, dtype=bool)
         i = 0
         while i < n:
-            m = min(per, n - i)
+            if self.direction is None:
+                # auto: both directions run the SAME first round (equal work), timed (max over
+                # ranks, so every rank decides alike); the faster direction is kept
+                m = min(top, self._per[FORWARD], self._per[BACKWARD], n - i)
+                got = {}
+                for d in (FORWARD, BACKWARD):
+                    t0 = time.perf_counter()
+                    got[d] = self._round(roots[i:i + m], targets[i:i + m], d)
+                    ns = int((time.perf_counter() - t0) * 1e9 / max(m, 1))
+                    self._trial[d] = self._allreduce([ns], dist.ReduceOp.MAX if self.world > 1 else None)[0]
+                if got[FORWARD] is None or got[BACKWARD] is None:
+                    self._trial = {}
+                    for d in (FORWARD, BACKWARD):
+                        self._shrink(d, m)
+                    continue
+                if not np.array_equal(got[FORWARD], got[BACKWARD]):
+                    raise L.KetoError(L.EDEVICE, "partition: forward and backward rounds disagree")
+                self.direction = min(self._trial, key=lambda k: (self._trial[k], k))
+                out[i:i + m] = got[FORWARD]
+                i += m
+                continue
             d = self.direction
-            if d is None:  # auto: a trial round per direction, then the faster one
-                d = FORWARD if FORWARD not in self._trial else BACKWARD
-            t0 = time.perf_counter()
+            m = min(top, self._per[d], n - i)  # a round size that overflowed stays halved for later calls
             got = self._round(roots[i:i + m], targets[i:i + m], d)
-            if self.direction is None and got is not None:
-                ns = int((time.perf_counter() - t0) * 1e9 / max(m, 1))
-                self._trial[d] = self._allreduce([ns], dist.ReduceOp.MAX if self.world > 1 else None)[0]
-                if len(self._trial) == 2:
-                    self.direction = min(self._trial, key=lambda k: (self._trial[k], k))
             if got is None:
-                if m <= 64:
-                    raise L.KetoError(L.ENOMEM, "partition buffers overflow for a single 64-request word")
-                per = max(64, (m // 2) // 64 * 64)
-                self.retries += 1
+                self._shrink(d, m)
                 continue
             out[i:i + m] = got
             i += m
         return out
+
+    def _shrink(self, d, m):
+        if m <= 64:
+            raise L.KetoError(L.ENOMEM, "partition buffers overflow for a single 64-request word")
+        self._per[d] = max(64, (m // 2) // 64 * 64)
+        self.retries += 1
 
     def close(self):
         close = getattr(self.local, "close", None)
