@@ -258,42 +258,96 @@ __global__ __launch_bounds__(kPB) void part_scatter_kernel(const ketogpu_record 
     }
 }
 
-// received (word, u, mask): OR into the owned state, new bits enter the next frontier
+// received (word, u, mask): OR into the owned state, new bits enter the next frontier.
+// A block takes a tile of kPTile records (kPItems per thread) and makes ONE reservation
+// on the packed frontier counter (count << kCntShift | row-length prefix) and one on the
+// touch counter per tile: a reservation per wave serialised on the shared counter
+// (690 us per level of ~3M records on config #2).
 __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogpu_record *rec, uint64_t n,
                                                          uint64_t out_base, unsigned long long *out_ctr) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
-    bool app = false, touched = false;
-    uint64_t key = 0, deg = 0;
-    if (i < n) {
-        const ketogpu_record r = rec[i];
-        const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
-        if (l < P.Nil) {
+    __shared__ uint64_t s_wsum[kPB / 64][2];  // per wave: packed append total, touch count
+    __shared__ unsigned long long s_base[2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kPTile; t0 < n; t0 += (uint64_t)gridDim.x * kPTile) {
+        uint64_t key[kPItems], deg[kPItems];
+        uint32_t app = 0, touched = 0;  // bit it: item it appends / is a vis-only entry
+        uint64_t val = 0, tcnt = 0;
+#pragma unroll
+        for (int it = 0; it < kPItems; it++) {
+            const uint64_t i = t0 + (uint64_t)it * kPB + threadIdx.x;
+            key[it] = 0;
+            deg[it] = 0;
+            if (i >= n) continue;
+            const ketogpu_record r = rec[i];
+            const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
+            if (l >= P.Nil) {
+                atomicOr(P.overflow, 2u);  // not an interior node of this rank
+                continue;
+            }
             const size_t slot = (size_t)r.a * P.Nil + l;
             const uint64_t nw = r.m & ~P.vis[slot];
-            if (nw) {
-                const uint64_t old = atomicOr((unsigned long long *)&P.vis[slot], (unsigned long long)nw);
-                const uint64_t newly = nw & ~old;
-                if (newly) {
-                    key = ((uint64_t)r.a << 32) | l;
-                    const uint64_t d = P.dir ? P.lb_off[l + 1] - P.lb_off[l] : P.lf_off[l + 1] - P.lf_off[l];
-                    if (d) {
-                        const uint64_t o2 = atomicOr((unsigned long long *)&P.nxt[slot], (unsigned long long)newly);
-                        if (!o2) {
-                            app = true;
-                            deg = d;
-                        }
-                    } else if (!old) {
-                        touched = true;  // vis-only entry: recorded once for the reset
-                    }
+            if (!nw) continue;
+            const uint64_t old = atomicOr((unsigned long long *)&P.vis[slot], (unsigned long long)nw);
+            const uint64_t newly = nw & ~old;
+            if (!newly) continue;
+            key[it] = ((uint64_t)r.a << 32) | l;
+            const uint64_t d = P.dir ? P.lb_off[l + 1] - P.lb_off[l] : P.lf_off[l + 1] - P.lf_off[l];
+            if (d) {
+                const uint64_t o2 = atomicOr((unsigned long long *)&P.nxt[slot], (unsigned long long)newly);
+                if (!o2) {
+                    app |= 1u << it;
+                    deg[it] = d;
+                    val += (1ull << kCntShift) | d;
                 }
+            } else if (!old) {
+                touched |= 1u << it;  // vis-only entry: recorded once for the reset
+                tcnt++;
             }
-        } else {
-            atomicOr(P.overflow, 2u);  // not an interior node of this rank
         }
+        const uint64_t incl = wave_incl_scan(val, lane), tincl = wave_incl_scan(tcnt, lane);
+        if (lane == 63) {
+            s_wsum[wv][0] = incl;
+            s_wsum[wv][1] = tincl;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t tot = 0, ttot = 0;
+            for (int k = 0; k < kPB / 64; k++) tot += s_wsum[k][0], ttot += s_wsum[k][1];
+            unsigned long long b0 = 0, b1 = 0;
+            if (tot) {
+                b0 = atomicAdd(out_ctr, (unsigned long long)tot);
+                // a row-length prefix that carries into the count field corrupts both: flag it
+                if ((b0 & kPreMask) + (tot & kPreMask) > kPreMask) atomicOr(P.overflow, 1u);
+            }
+            if (ttot) b1 = atomicAdd(&P.ctr[2], (unsigned long long)ttot);
+            s_base[0] = b0;
+            s_base[1] = b1;
+        }
+        __syncthreads();
+        uint64_t pos = s_base[0] + incl - val, tpos = s_base[1] + tincl - tcnt;
+        for (int k = 0; k < wv; k++) pos += s_wsum[k][0], tpos += s_wsum[k][1];
+#pragma unroll
+        for (int it = 0; it < kPItems; it++) {
+            if ((app >> it) & 1u) {
+                const uint64_t idx = out_base + (pos >> kCntShift);
+                if (idx < P.fe_cap) {
+                    P.fe_key[idx] = key[it];
+                    P.fe_pre[idx] = pos & kPreMask;
+                } else {
+                    atomicOr(P.overflow, 1u);
+                }
+                pos += (1ull << kCntShift) | deg[it];
+            }
+            if ((touched >> it) & 1u) {
+                if (tpos < P.touch_cap)
+                    P.touch[tpos] = key[it];
+                else
+                    atomicOr(P.overflow, 1u);
+                tpos++;
+            }
+        }
+        __syncthreads();  // s_wsum / s_base are reused by the next tile
     }
-    wave_append(app, key, deg, lane, out_ctr, out_base, P.fe_cap, P.fe_key, P.fe_pre, nullptr, 0, P.overflow);
-    wave_touch(touched, key, lane, &P.ctr[2], P.touch, P.touch_cap, P.overflow);
 }
 
 // next level's masks: nxt -> entry list, nxt cleared
@@ -577,7 +631,10 @@ struct ketogpu_part {
             return KETOGPU_ENOMEM;
         }
         PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
-        if (n) {
+        if (n && world == 1) {  // one destination: the records are already grouped
+            counts[0] = n;
+            PHIP(hipMemcpyAsync(send, P.obuf, n * sizeof(ketogpu_record), hipMemcpyDeviceToDevice, stream));
+        } else if (n) {
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
             KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
             PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -606,7 +663,8 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(&P.ctr[nxt], 0, sizeof(unsigned long long), stream));
         const uint64_t base = lb + cnt;
         if (n)
-            KLAUNCH(part_apply_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n, base,
+            KLAUNCH(part_apply_kernel, dim3((unsigned)std::min<uint64_t>((n + kPTile - 1) / kPTile, 8192)), dim3(kPB), 0,
+                    stream, P, recv, n, base,
                                &P.ctr[nxt]);
         read_ctr();
         stats.records_received += n;
