@@ -552,7 +552,7 @@ struct ketogpu_part {
 
         size_t free_b = 0, total_b = 0;
         PHIP(hipMemGetInfo(&free_b, &total_b));
-        uint64_t budget = o.state_budget_bytes ? o.state_budget_bytes : std::min<uint64_t>(free_b / 4, 32ull << 30);
+        uint64_t budget = o.state_budget_bytes ? o.state_budget_bytes : std::min<uint64_t>(free_b / 4, 64ull << 30);
         budget = std::min<uint64_t>(budget, (uint64_t)free_b / 2);
         uint64_t lists = budget / 4;
         P.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 32, 1 << 16), kMaxListEntries);
