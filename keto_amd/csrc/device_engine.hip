@@ -2469,9 +2469,11 @@ struct ketogpu_engine {
                 HIP_CHECK(hipEventRecord(d, stream));
                 const size_t ns = stages.size() + 1;
                 KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 24, spill_count, ns * sizeof(unsigned int), hipMemcpyDeviceToHost,
-                                         stream));
+                // the spill counters sit 8 words after the reduced statistics (st.stats
+                // layout, kStatsLen): one copy brings both to h_ctr[16..21] and h_ctr + 24
+                static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
+                // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
                 HIP_CHECK(hipStreamSynchronize(stream));
                 unit_end = d;
                 unit_ev.push_back({a, b});
@@ -2735,10 +2737,20 @@ struct ketogpu_engine {
         // one launch zeroes results, flags, statistics and spill counters
         KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
                            q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen);
-        HIP_CHECK(hipEventRecord(t_begin, stream));
+        // A timing event costs ~5.6 us of GPU idle between the kernels it separates
+        // (kernel trace of config #2): with the bidi first stage the run starts at that
+        // stage's own start event, recorded right after this point.
+        const bool bidi_first = use_units && !wave_u && use_v2 && use_bidi && q.n;
+        if (!bidi_first) HIP_CHECK(hipEventRecord(t_begin, stream));
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
             uint64_t ns = run_units(q, rs, unit_ev);
+            if (bidi_first) {
+                if (!unit_ev.empty())
+                    t_begin = unit_ev.front().first;
+                else
+                    HIP_CHECK(hipEventRecord(t_begin, stream));
+            }
             rs.spilled_requests = ns;
             if (ns) {  // single requests whose closure exceeds an LDS table: global path
                 KLAUNCH(spill_gather_kernel, dim3(blocks_for(ns)), dim3(kBlock), 0, stream, spill_units, ns,
