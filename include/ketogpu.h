@@ -337,7 +337,10 @@ int ketogpu_part_begin(ketogpu_part *p, const uint32_t *roots, const uint32_t *t
 #define KETOGPU_PART_BACKWARD 1
 int ketogpu_part_begin_dir(ketogpu_part *p, const uint32_t *roots, const uint32_t *targets, size_t n,
                            int32_t direction);
-/* this step's outgoing records grouped by destination rank into send_dev; counts[world] */
+/* this step's outgoing records grouped by destination rank into send_dev; counts[world].
+   world > 1: send_dev is complete on return (any stream may read it).  world == 1: the copy
+   is ordered on the partition's stream only; pass send_dev straight to ketogpu_part_apply /
+   _pull_answer (which run on that stream) or call ketogpu_part_sync first. */
 int ketogpu_part_emit(ketogpu_part *p, ketogpu_record *send_dev, uint64_t capacity, uint64_t *counts);
 /* OR received records into the owned state; *frontier = owned entries of the next level */
 int ketogpu_part_apply(ketogpu_part *p, const ketogpu_record *recv_dev, uint64_t n, uint64_t *frontier);
@@ -349,6 +352,8 @@ int ketogpu_part_pull_answer(ketogpu_part *p, const ketogpu_record *recv_dev, ui
 /* this rank's hit bits of the round (ceil(n/64) host words) and state reset */
 int ketogpu_part_end(ketogpu_part *p, uint64_t *allowed_bits);
 int ketogpu_part_abort(ketogpu_part *p);
+/* wait for the partition's stream (world 1: makes the last emit's send_dev readable elsewhere) */
+int ketogpu_part_sync(ketogpu_part *p);
 int ketogpu_part_stats_get(const ketogpu_part *p, ketogpu_part_stats *out);
 
 /* ------------------------------------------------------------------ expand */

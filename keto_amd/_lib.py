@@ -171,6 +171,7 @@ SIGNATURES = {
     "ketogpu_part_pull_answer": (C.c_int, [vp, vp, C.c_uint64]),
     "ketogpu_part_end": (C.c_int, [vp, vp]),
     "ketogpu_part_abort": (C.c_int, [vp]),
+    "ketogpu_part_sync": (C.c_int, [vp]),
     "ketogpu_part_stats_get": (C.c_int, [vp, C.POINTER(PartStats)]),
 }
 

@@ -77,7 +77,7 @@ struct PartDev {
     uint64_t touch_cap;
     ketogpu_record *obuf;    // outgoing records of the current step (unordered)
     uint64_t ocap;
-    unsigned long long *ctr;  // [0..1] frontier counters (ping-pong), [2] touch, [3] obuf
+    unsigned long long *ctr;  // [0..1] frontier counters (ping-pong), [2] touch, [3] obuf, [4..5] overflow
     unsigned int *overflow;   // bit 0 list/buffer overflow, bit 1 misrouted record
     uint64_t *allowed;        // this rank's hit bits of the round
     const uint32_t *roots, *targets;
@@ -578,7 +578,7 @@ struct ketogpu_part {
         P.touch = own(palloc<uint64_t>(P.touch_cap));
         P.obuf = own(palloc<ketogpu_record>(P.ocap));
         P.ctr = own(palloc<unsigned long long>(8));
-        P.overflow = own(palloc<unsigned int>(4));
+        P.overflow = (unsigned int *)(P.ctr + 4);  // in the counter block: one copy reads both
         P.allowed = own(palloc<uint64_t>(W));
         d_roots = own(palloc<uint32_t>(W * 64));
         d_targets = own(palloc<uint32_t>(W * 64));
@@ -591,8 +591,8 @@ struct ketogpu_part {
     }
 
     void read_ctr() {
-        PHIP(hipMemcpyAsync(h, P.ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
-        PHIP(hipMemcpyAsync(h + 4, P.overflow, sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+        // ctr[0..3] and the overflow flags (ctr[4], low word) in one copy
+        PHIP(hipMemcpyAsync(h, P.ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
         PHIP(hipStreamSynchronize(stream));
     }
     uint32_t overflow_bits() const { return (uint32_t)h[4]; }
@@ -613,7 +613,6 @@ struct ketogpu_part {
             PHIP(hipMemcpyAsync(d_targets, targets, n * 4, hipMemcpyHostToDevice, stream));
         }
         PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
-        PHIP(hipMemsetAsync(P.overflow, 0, 4 * sizeof(unsigned int), stream));
         PHIP(hipMemsetAsync(P.allowed, 0, W * 8, stream));
         lb = cnt = edges = 0;
         cur = 0;
@@ -630,11 +629,11 @@ struct ketogpu_part {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
             return KETOGPU_ENOMEM;
         }
-        PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
         if (n && world == 1) {  // one destination: the records are already grouped
             counts[0] = n;
             PHIP(hipMemcpyAsync(send, P.obuf, n * sizeof(ketogpu_record), hipMemcpyDeviceToDevice, stream));
         } else if (n) {
+            PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
             KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
             PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -653,7 +652,9 @@ struct ketogpu_part {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
         }
         PHIP(hipMemsetAsync(&P.ctr[3], 0, sizeof(unsigned long long), stream));
-        PHIP(hipStreamSynchronize(stream));
+        // the exchange reads `send` on another stream (torch's, for RCCL); at world 1 the
+        // records go straight back into apply on this stream, in order, without a host wait
+        if (world > 1) PHIP(hipStreamSynchronize(stream));
         stats.records_sent += n;
         return KETOGPU_OK;
     }
@@ -682,7 +683,8 @@ struct ketogpu_part {
         *frontier = ncnt;
         stats.levels++;
         stats.frontier_entries += ncnt;
-        PHIP(hipStreamSynchronize(stream));
+        // no host wait for the gather: expand and the next emit's counter read follow it on
+        // this stream (each host synchronization left the GPU idle ~20 us per level)
         return KETOGPU_OK;
     }
 
@@ -694,7 +696,7 @@ struct ketogpu_part {
             PHIP(hipGetLastError());
             stats.forward_edges += edges;
         }
-        PHIP(hipStreamSynchronize(stream));
+        // no host wait: the next emit reads the record counter on this stream first
     }
 
     void pull_emit() {
@@ -726,7 +728,6 @@ struct ketogpu_part {
                                    ntouch);
         }
         PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
-        PHIP(hipMemsetAsync(P.overflow, 0, 4 * sizeof(unsigned int), stream));
         PHIP(hipStreamSynchronize(stream));
         lb = cnt = edges = 0;
         dirty = false;
@@ -865,6 +866,15 @@ int ketogpu_part_abort(ketogpu_part *p) {
     std::lock_guard<std::mutex> lk(p->mu);
     PHIP(hipSetDevice(p->device));
     p->reset(true);
+    PAPI_END
+}
+
+int ketogpu_part_sync(ketogpu_part *p) {
+    PAPI_BEGIN
+    if (!p) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    PHIP(hipStreamSynchronize(p->stream));
     PAPI_END
 }
 
