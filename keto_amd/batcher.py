@@ -118,26 +118,50 @@ class MicroBatcher:
                 else:
                     self._cv.wait()
 
+    @staticmethod
+    def _settle(f, result=None, exc=None):
+        """complete one request's future; a future its caller cancelled (Future.cancel) is
+        skipped, so no single request can raise InvalidStateError in the dispatcher"""
+        try:
+            if exc is not None:
+                f.set_exception(exc)
+            else:
+                f.set_result(result)
+        except Exception:  # cancelled or already settled: that caller is gone
+            pass
+
     def _run(self):
         while True:
             batch = self._take()
             if not batch:
                 return
-            live = []
-            for item in batch:
-                r, f, ctx, _ = item
-                if ctx is not None and ctx.done():  # dropped before it reaches the device
-                    f.set_exception(Canceled("context canceled before the batch was flushed"))
-                elif f.set_running_or_notify_cancel():
-                    live.append(item)
-            if not live:
-                continue
-            self.batches.append(len(live))
             try:
-                got = self.engine.check_many([r for r, _, _, _ in live])
-            except Exception as e:  # device failure: exactly this batch's requests fail
-                for _, f, _, _ in live:
-                    f.set_exception(e)
+                self._dispatch(batch)
+            except Exception as e:  # never let one batch end the dispatcher thread
+                for _, f, _, _ in batch:
+                    if not f.done():
+                        self._settle(f, exc=e)
+
+    def _dispatch(self, batch):
+        live = []
+        for item in batch:
+            r, f, ctx, _ = item
+            # claim the future first: set_running_or_notify_cancel() is False for a future the
+            # caller already cancelled, which then takes no outcome at all
+            if not f.set_running_or_notify_cancel():
                 continue
-            for (_, f, ctx, _), a in zip(live, got):
-                f.set_result(bool(a))
+            if ctx is not None and ctx.done():  # dropped before it reaches the device
+                self._settle(f, exc=Canceled("context canceled before the batch was flushed"))
+            else:
+                live.append(item)
+        if not live:
+            return
+        self.batches.append(len(live))
+        try:
+            got = self.engine.check_many([r for r, _, _, _ in live])
+        except Exception as e:  # device failure: exactly this batch's requests fail
+            for _, f, _, _ in live:
+                self._settle(f, exc=e)
+            return
+        for (_, f, _, _), a in zip(live, got):
+            self._settle(f, result=bool(a))

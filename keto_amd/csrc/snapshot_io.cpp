@@ -7,6 +7,7 @@
 // u32 sizeof(ketogpu_snapshot_stats) | then every field in a fixed order, vectors as
 // u64 count + raw elements, string pools as u64 count + u32 lengths + bytes.  The
 // derived hash maps (subject-set triples, subject-id index) are rebuilt on load.
+#include <algorithm>
 #include <cstdio>
 #include <memory>
 
@@ -22,8 +23,14 @@ constexpr uint32_t kFormat = 3;  // 3: row order flag
 struct File {
     FILE *f = nullptr;
     std::string path;
+    uint64_t size = 0, pos = 0;  // read mode: file size and bytes consumed
     File(const char *p, const char *mode) : f(fopen(p, mode)), path(p) {
         if (!f) throw Error(KETOGPU_EINVAL, "cannot open " + path);
+        if (mode[0] == 'r' && fseek(f, 0, SEEK_END) == 0) {
+            const long n = ftell(f);
+            size = n > 0 ? (uint64_t)n : 0;
+            fseek(f, 0, SEEK_SET);
+        }
     }
     ~File() {
         if (f) fclose(f);
@@ -33,6 +40,12 @@ struct File {
     }
     void read(void *p, size_t n) {
         if (n && fread(p, 1, n, f) != n) throw Error(KETOGPU_EINVAL, "truncated snapshot file " + path);
+        pos += n;
+    }
+    // a length field must fit in the rest of the file (a corrupt count must not allocate)
+    void need(uint64_t count, uint64_t elem) {
+        if (elem && count > (size - std::min(size, pos)) / elem)
+            throw Error(KETOGPU_EINVAL, "corrupt length field in snapshot file " + path);
     }
     template <class T>
     void put(const T &v) {
@@ -52,6 +65,7 @@ struct File {
     template <class T>
     void get_vec(std::vector<T> &v) {
         uint64_t n = get<uint64_t>();
+        need(n, sizeof(T));
         v.resize(n);
         read(v.data(), n * sizeof(T));
     }
@@ -60,7 +74,9 @@ struct File {
         write(s.data(), s.size());
     }
     std::string get_str() {
-        std::string s(get<uint32_t>(), '\0');
+        const uint32_t n = get<uint32_t>();
+        need(n, 1);
+        std::string s(n, '\0');
         read(s.data(), s.size());
         return s;
     }
@@ -70,6 +86,7 @@ struct File {
     }
     void get_pool(StrPool &p) {
         uint64_t n = get<uint64_t>();
+        need(n, sizeof(uint32_t));
         std::string s;
         for (uint64_t i = 0; i < n; i++) {
             s = get_str();
@@ -78,6 +95,52 @@ struct File {
         }
     }
 };
+
+// Every index a loaded snapshot holds must stay inside the arrays it indexes: the host
+// DFS, the resolver and the device kernels read them unchecked.  A file that passes the
+// magic trailer but is corrupt (or written by a buggy writer) is refused here.
+void validate(const Snapshot &s, const std::string &path) {
+    auto bad = [&](const char *what) { throw Error(KETOGPU_EINVAL, path + ": inconsistent snapshot (" + what + ")"); };
+    const uint64_t N = s.N, P = s.pool.size();
+    if (!(s.Ni <= s.Nx && s.Nx <= s.N)) bad("node ranges");
+    for (size_t n : {s.node_kind.size(), s.node_ns.size(), s.node_a.size(), s.node_b.size(), s.key_id.size(),
+                     s.ambiguous.size(), s.node_row.size()})
+        if (n != N) bad("per-node array size");
+    for (uint64_t v = 0; v < N; v++) {
+        if (s.node_kind[v] > 1 || s.node_a[v] >= P || (s.node_kind[v] == KETOGPU_SUBJECT_SET && s.node_b[v] >= P))
+            bad("node identity");
+        const RowRef &r = s.node_row[v];
+        if (r.off > s.row_col.size() || r.len > s.row_col.size() - r.off || r.len > r.full_len) bad("node rows");
+    }
+    for (uint32_t x : s.sid_node)
+        if (x != NONE && x >= N) bad("subject-id index");
+    for (uint32_t x : s.row_col)
+        if (x >= N) bad("row entries");
+    for (uint32_t x : s.group_col)
+        if (x >= N) bad("group entries");
+    for (const Group &g : s.groups) {
+        if (g.obj >= P || g.rel >= P || g.valid > g.full_len || g.begin > s.group_col.size() ||
+            g.valid > s.group_col.size() - g.begin)
+            bad("group rows");
+        if (g.first_bad >= 0 && ((uint64_t)g.first_bad >= g.full_len || g.tail > s.tail_rows.size() ||
+                                 g.full_len - (uint64_t)g.first_bad > s.tail_rows.size() - g.tail))
+            bad("group tail");
+    }
+    for (const TupleRow &t : s.tail_rows)
+        if (t.obj >= P || t.rel >= P || t.kind > 1 || (t.kind ? (t.ss_obj >= P || t.ss_rel >= P) : t.sid >= P))
+            bad("tail rows");
+    auto csr = [&](const std::vector<uint64_t> &off, const std::vector<uint32_t> &col, uint64_t rows, uint64_t lim,
+                   const char *what) {
+        if (off.size() != rows + 1 || off[0] != 0 || off.back() != col.size()) bad(what);
+        for (uint64_t i = 0; i < rows; i++)
+            if (off[i] > off[i + 1]) bad(what);
+        for (uint32_t x : col)
+            if (x >= lim) bad(what);
+    };
+    csr(s.fint_off, s.fint_col, s.Nx, s.Ni, "forward rows");
+    csr(s.rev_off, s.rev_col, N, s.Nx, "reverse rows");
+    if (s.has_ambiguous && s.row_amb.size() < ((uint64_t)s.Nx + 31) / 32) bad("ambiguous-row bitmap");
+}
 
 }  // namespace
 
@@ -188,8 +251,7 @@ int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out) {
         s->stats = f.get<ketogpu_snapshot_stats>();
         f.read(magic, sizeof magic);
         if (memcmp(magic, kMagic, sizeof magic)) throw Error(KETOGPU_EINVAL, std::string(path) + ": truncated snapshot");
-        if (s->node_kind.size() != s->N || s->fint_off.size() != (size_t)s->Nx + 1 || s->rev_off.size() != (size_t)s->N + 1)
-            throw Error(KETOGPU_EINVAL, std::string(path) + ": inconsistent snapshot");
+        validate(*s, path);
         for (uint32_t v = 0; v < s->N; v++)  // the subject-set index (sid_node is stored)
             if (s->node_kind[v] == KETOGPU_SUBJECT_SET) s->set_node.get_or_insert(s->node_ns[v], s->node_a[v], s->node_b[v], v);
         *out = reinterpret_cast<ketogpu_snapshot *>(s.release());

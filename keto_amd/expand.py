@@ -17,6 +17,13 @@ from .snapshot import Snapshot, subject_struct
 Union, Exclusion, Intersection, Leaf = "union", "exclusion", "intersection", "leaf"
 
 
+
+def _depth(d):
+    """restDepth for the int32 argument of ketogpu_expand: every depth <= 0 is the nil
+    tree and every depth beyond INT32_MAX exceeds any tree's height, so clamping keeps
+    BuildTree's answer (ctypes would silently truncate a wider Go int)"""
+    return max(-1, min(int(d), 2**31 - 1))
+
 class NotFound(LookupError):
     """herodot.ErrNotFound (HTTP 404)"""
 
@@ -55,7 +62,7 @@ class Engine:
         without Python objects (throughput measurements)"""
         h = C.c_void_p()
         subj = subject_struct(subject)
-        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), int(rest_depth), C.byref(h))
+        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), _depth(rest_depth), C.byref(h))
         if rc == L.ENOTFOUND:
             raise NotFound(self.L.ketogpu_last_error().decode("utf-8", "replace"))
         L.check(rc)
@@ -72,7 +79,7 @@ class Engine:
     def BuildTree(self, subject: Subject, rest_depth: int) -> Optional[Tree]:
         h = C.c_void_p()
         subj = subject_struct(subject)
-        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), int(rest_depth), C.byref(h))
+        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), _depth(rest_depth), C.byref(h))
         if rc == L.ENOTFOUND:
             raise NotFound(self.L.ketogpu_last_error().decode("utf-8", "replace"))
         L.check(rc)
@@ -103,7 +110,7 @@ class Engine:
         """the library's own MarshalJSON (ketogpu_tree_json)"""
         h = C.c_void_p()
         subj = subject_struct(subject)
-        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), int(rest_depth), C.byref(h))
+        rc = self.L.ketogpu_expand(self.snapshot.h, C.byref(subj), _depth(rest_depth), C.byref(h))
         if rc == L.ENOTFOUND:
             raise NotFound(self.L.ketogpu_last_error().decode("utf-8", "replace"))
         L.check(rc)

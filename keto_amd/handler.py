@@ -69,14 +69,90 @@ def tuple_from_url(q):
     return InternalRelationTuple(ns, obj, rel, subject)
 
 
+def _json_string(d, k):
+    """a string field of the JSON tuple: Go's decoder turns null into "" and rejects any
+    other non-string value (json.UnmarshalTypeError -> 400)"""
+    v = d.get(k)
+    if v is None:
+        return ""
+    if not isinstance(v, str):
+        raise BadRequest(f"json: cannot unmarshal {type(v).__name__} into field {k} of type string")
+    return v
+
+
 def tuple_from_json(d):
     """JSON body of POST /check: {namespace, object, relation, subject_id | subject_set}"""
     if not isinstance(d, dict):
         raise BadRequest("Unable to decode JSON payload: expected an object")
-    t = InternalRelationTuple.from_dict(d)
     if "subject_id" in d and "subject_set" in d:
         raise BadRequest("exactly one of subject_set or subject_id has to be provided")
-    return t
+    ns, obj, rel = (_json_string(d, k) for k in ("namespace", "object", "relation"))
+    subject = None
+    if d.get("subject_id") is not None:
+        subject = SubjectID(_json_string(d, "subject_id"))
+    elif d.get("subject_set") is not None:
+        ss = d["subject_set"]
+        if not isinstance(ss, dict):
+            raise BadRequest(f"json: cannot unmarshal {type(ss).__name__} into field subject_set of type object")
+        subject = SubjectSet(*(_json_string(ss, k) for k in ("namespace", "object", "relation")))
+    return InternalRelationTuple(ns, obj, rel, subject)
+
+
+def _underscore_ok(s):
+    """Go's strconv underscoreOK: '_' only between digits or after a base prefix"""
+    saw, i = "^", 0
+    if s[:1] in ("-", "+"):
+        s = s[1:]
+    hexa = False
+    if len(s) >= 2 and s[0] == "0" and s[1].lower() in "box":
+        i, saw, hexa = 2, "0", s[1].lower() == "x"
+    while i < len(s):
+        c = s[i]
+        if c.isdigit() and c.isascii() or hexa and c.lower() in "abcdef":
+            saw = "0"
+        elif c == "_":
+            if saw != "0":
+                return False
+            saw = "_"
+        else:
+            if saw == "_":
+                return False
+            saw = "!"
+        i += 1
+    return saw != "_"
+
+
+def go_parse_int(s):
+    """strconv.ParseInt(s, 0, 64), as getExpand parses max-depth (internal/expand/handler.go:79):
+    an optional sign, then 0b/0o/0x prefixes or a leading 0 for octal, '_' digit
+    separators, no whitespace; ValueError on bad syntax or a value outside int64"""
+    if not isinstance(s, str) or not s:
+        raise ValueError("invalid syntax")
+    neg = s[0] == "-"
+    body = s[1:] if s[0] in "+-" else s
+    if not body:
+        raise ValueError("invalid syntax")
+    base, digits = 10, body
+    if body[0] == "0":
+        p = body[1:2].lower()
+        if len(body) >= 3 and p in ("b", "o", "x"):
+            base, digits = {"b": 2, "o": 8, "x": 16}[p], body[2:]
+        else:
+            base, digits = 8, body[1:]
+    n, underscores = 0, False
+    for c in digits:
+        if c == "_":
+            underscores = True
+            continue
+        d = int(c, 16) if c.isascii() and c.lower() in "0123456789abcdef" else 99
+        if d >= base:
+            raise ValueError("invalid syntax")
+        n = n * base + d
+    if underscores and not _underscore_ok(s):
+        raise ValueError("invalid syntax")
+    if (not neg and n >= 1 << 63) or (neg and n > 1 << 63):
+        raise ValueError("value out of range")
+    return -n if neg else n
 
 
 class Handler:
@@ -115,10 +191,13 @@ class Handler:
 
     def get_expand(self, query):
         q = parse_qs(query, keep_blank_values=True) if isinstance(query, str) else query
+        raw = _get(q, "max-depth")
         try:
-            depth = int(_get(q, "max-depth"), 0)  # strconv.ParseInt(s, 0, 0)
-        except (TypeError, ValueError):
-            return self._error(400, 'strconv.ParseInt: parsing "max-depth": invalid syntax')
+            depth = go_parse_int(raw)  # strconv.ParseInt(s, 0, 0)
+        except ValueError as e:
+            return self._error(400, f'strconv.ParseInt: parsing "{raw}": {e}')
+        # ketogpu_expand takes an int32: every depth beyond any tree's height acts the same
+        depth = max(-1, min(depth, 2**31 - 1))
         subject = SubjectSet(_get(q, "namespace") or "", _get(q, "object") or "", _get(q, "relation") or "")
         try:
             tree = self.expand.BuildTree(subject, depth)

@@ -179,3 +179,25 @@ def test_batcher_on_gpu_engine(cases):
             t.join()
     assert got == want
     assert np.mean(b.batches) > 1
+
+
+def test_future_cancel_with_done_context_keeps_dispatcher(cases):
+    """a caller that cancels its Future and its context must not kill the
+    dispatcher (set_exception on a CANCELLED future raises InvalidStateError)"""
+    _, _, tuples, want = cases
+    gate = threading.Event()
+    eng = StubEngine(table_of(tuples, want), gate=gate)
+    with MicroBatcher(eng, max_batch=4, max_wait=1e-3) as b:
+        first = b.submit(tuples[0])  # holds the dispatcher inside the engine call
+        assert eng.entered.wait(5)
+        ctx = Context()
+        f = b.submit(tuples[1], ctx)
+        assert f.cancel()  # still queued: the caller's cancel succeeds
+        ctx.cancel()
+        g = b.submit(tuples[2], Context())
+        g.cancel()  # cancelled future, live context
+        gate.set()
+        assert first.result(5) == want[0]
+        # the dispatcher is still alive and answers later requests
+        assert b.SubjectIsAllowed(tuples[3]) == want[3]
+        assert f.cancelled() and g.cancelled()

@@ -8,7 +8,7 @@ import pytest
 from keto_amd import _lib as L
 from keto_amd import check, expand
 from keto_amd import relationtuple as rt
-from keto_amd.handler import BadRequest, Handler, relation_query_from_url, tuple_from_url
+from keto_amd.handler import BadRequest, Handler, go_parse_int, relation_query_from_url, tuple_from_json, tuple_from_url
 from keto_amd.snapshot import Snapshot
 
 
@@ -32,6 +32,35 @@ def test_url_query_parsing_matches_reference():
         tuple_from_url(q(namespace="n"))
 
 
+def test_json_tuple_rejects_non_string_fields():
+    """encoding/json into string fields: numbers, bools, lists are a 400, null is "" """
+    for bad in ({"namespace": "n", "object": 1, "relation": "r", "subject_id": "s"},
+                {"namespace": "n", "object": "o", "relation": "r", "subject_id": 7},
+                {"namespace": "n", "object": "o", "relation": "r", "subject_set": "n:o#r"},
+                {"namespace": "n", "object": "o", "relation": "r", "subject_set": {"namespace": ["x"]}},
+                {"namespace": True, "object": "o", "relation": "r", "subject_id": "s"}):
+        with pytest.raises(BadRequest, match="cannot unmarshal"):
+            tuple_from_json(bad)
+    t = tuple_from_json({"namespace": "n", "object": None, "relation": "r", "subject_set": {"namespace": "a"}})
+    assert t == rt.InternalRelationTuple("n", "", "r", rt.SubjectSet("a", "", ""))
+    h = Handler(None, None)  # both routes answer the type error before any engine call
+    assert h.post_check(b'{"namespace":"n","object":1,"relation":"r","subject_id":"s"}')[0] == 400
+    assert h.post_check(b'{"namespace":"n","object":"o","relation":"r","subject_set":5}')[0] == 400
+    code, body = h.post_check_batch(b'{"tuples":[{"namespace":"n","object":1,"relation":"r","subject_id":"s"}]}')
+    assert code == 200 and body["results"][0]["error"]["code"] == 400
+
+
+def test_max_depth_parses_like_strconv_parseint():
+    """strconv.ParseInt(s, 0, 0) of getExpand (internal/expand/handler.go:79)"""
+    ok = {"10": 10, "010": 8, "0x1F": 31, "0X1f": 31, "0o17": 15, "0b101": 5, "-3": -3, "+4": 4, "0": 0,
+          "1_000": 1000, "0x_1F": 31, "0_7": 7, "9223372036854775807": 2**63 - 1, "-9223372036854775808": -2**63}
+    for s, v in ok.items():
+        assert go_parse_int(s) == v, s
+    for s in ("", " 3", "3 ", "08", "0x", "1__0", "_1", "1_", "0b2", "+-1", "9223372036854775808", "1e3", "٣"):
+        with pytest.raises(ValueError):
+            go_parse_int(s)
+
+
 @pytest.fixture
 def expand_handler():
     ns = [("expand handler", 1)]
@@ -53,6 +82,12 @@ def test_expand_handler_matches_reference(expand_handler):
                     "children": [{"type": "leaf", "subject_id": "child0"}, {"type": "leaf", "subject_id": "child1"}]}
     code, body = h.get_expand("namespace=expand+handler&object=nothing&relation=x&max-depth=2")
     assert code == 200 and body is None  # a nil tree is JSON null (cmd/expand/root_test.go)
+    # Go base-0 syntax: "02" is octal 2; a depth above int32 is the full tree, not a truncation
+    full = h.get_expand("namespace=expand+handler&object=root&relation=parent+of&max-depth=2")[1]
+    assert h.get_expand("namespace=expand+handler&object=root&relation=parent+of&max-depth=02")[1] == full
+    assert h.get_expand("namespace=expand+handler&object=root&relation=parent+of&max-depth=4294967296")[1] == full
+    assert h.get_expand("max-depth=+%203")[0] == 400
+    assert h.get_expand("max-depth=99999999999999999999")[0] == 400
 
 
 @pytest.mark.gpu
