@@ -3,8 +3,12 @@
 Workload (BASELINE.json configs[1]): synthetic RBAC, 10M users, 100k
 nested groups, 50M tuples, 1M checks docs:d#viewer@u per GPU (half constructed
 positives), seed 0x4B45544F.  The graph is replicated on every GPU (it fits 288 GB many
-times over) and each rank checks its own 1M requests: no data-path collective, weak
-scaling.  A step = one ketogpu_queries_run over the rank's 1M HBM-resident requests.
+times over); the global batch of N x 1M requests is split into contiguous 64-request-word
+ranges, one per GPU: no data-path collective, weak scaling.  A step = one host-to-host
+ketogpu_check_ids over a GPU's range (requests H2D from pinned memory, traversal, result
+bits D2H), as SURVEY.md 8(d) times the batch call; the HBM-resident rate and the traversal
+kernel's roofline are measured beside it.  Under torchrun each rank drives its own GPU;
+`python bench.py --gpus N` in one process drives N GPUs through ketogpu_multi.
 
     python bench.py [--gpus N --steps K --warmup W] [--small] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -93,6 +97,25 @@ def cpu_model():
     return platform.processor()
 
 
+def kernel_source_hash():
+    from keto_amd.build import kernel_source_hash as h
+    return h()
+
+
+def host_cores():
+    """CPU threads this job may use: the scheduler affinity (= nproc), capped by a cgroup
+    CPU quota when one is set (a quota of 16 CPUs on 256 visible ones runs 16 at a time)"""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(nproc, quota) if quota else nproc), nproc, quota
+
+
 def main():
     a = parse()
     rank, world, local = dist_init(a.gpus)
@@ -102,113 +125,168 @@ def main():
     from keto_amd import check, synth
     from keto_amd.snapshot import Snapshot
 
+    # one process per GPU under torchrun (world = N), or one process driving N GPUs
+    # through the replicated multi-GPU engine (world = 1, --gpus N): either way the
+    # global batch of N x 1M requests is split into contiguous word ranges, one per GPU
+    procs_gpus = a.gpus if world == 1 else 1
+    n_gpus = world * procs_gpus
     scale = 100 if a.small else 1
+    per_gpu = 1_000_000 // (10 if a.small else 1)
     sizes = dict(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
-                 tuples=50_000_000 // scale, checks=1_000_000 // (10 if a.small else 1))
+                 tuples=50_000_000 // scale, checks=per_gpu * n_gpus)
     t0 = time.time()
-    # every rank builds the same graph (same seed) and draws its own 1M requests
-    w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1 + rank)
+    # every rank builds the same graph and the same global batch (same seeds)
+    w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1)
     t_gen = time.time() - t0
     log(f"generated {w.counts} in {t_gen:.1f}s")
     t0 = time.time()
     snap = Snapshot.from_columns(w.namespaces, w.columns)
     t_snap = time.time() - t0
     log(f"snapshot built in {t_snap:.1f}s")
-    roots, targets = w.resolve(snap)
-    eng = check.Engine(snap, device=local)
-    t0 = time.time()
-    q = eng.upload(roots, targets)
-    t_h2d = time.time() - t0
+    roots_all, targets_all = w.resolve(snap)
+    b, e = check.MultiEngine.ranges(len(roots_all), world)[rank]
+    roots, targets = roots_all[b:e], targets_all[b:e]
+    n = len(roots)
+    if procs_gpus > 1:
+        eng = check.MultiEngine(snap, list(range(procs_gpus)))
+        eng0 = eng.engine(0)
+    else:
+        eng = eng0 = check.Engine(snap, device=local)
+    # the batch lives in pinned host memory, as the cgo micro-batcher's buffer would
+    # (ketogpu_host_alloc); results come back into pinned words
+    pr, pt = check.pinned(roots), check.pinned(targets)
+    words = (n + 63) // 64
+    out = check.PinnedBuffer(words, np.uint64)
 
-    # plan selection (KETOGPU_UNITS=auto): the engine's first two large batches run
-    # both first stages and keep the faster; done here so the timed steps never do it
+    def step():
+        eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, n, out.array.ctypes.data)
+
+    # plan selection (KETOGPU_UNITS=auto): each engine's first two large batches run every
+    # candidate first stage and keep the fastest; done here so the timed steps never do it
     for _ in range(2):
-        q.run()
+        step()
     for _ in range(a.warmup):
-        q.run()
+        step()
     barrier(world)
+    calls = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        q.run()
+        c0 = time.perf_counter()
+        step()
+        calls.append(time.perf_counter() - c0)
     barrier(world)
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world)
     log(f"{a.steps} steps in {dt:.4f}s")
-    st = eng.last_stats()
-    allowed = q.download()
+    allowed = check.unpack_bits(out.array.copy(), n)
+    value = len(roots_all) * a.steps / dt
+    median_call = float(np.median(calls))
 
-    # PCIe-inclusive rate of one full host-to-host call (not `value`)
+    # the same batch from pageable numpy arrays (no pinned staging): reported, not `value`
+    c0 = time.perf_counter()
+    got_pageable = eng.check_ids(roots, targets)
+    t_pageable = time.perf_counter() - c0
+    assert np.array_equal(got_pageable, allowed)
+
+    # HBM-resident batch on one GPU: the traversal kernels alone (roofline source)
+    b0, e0 = (check.MultiEngine.ranges(n, procs_gpus)[0] if procs_gpus > 1 else (0, n))
+    q = eng0.upload(roots[b0:e0], targets[b0:e0])
+    for _ in range(a.warmup + 1):
+        q.run()
+    runs = []
     t0 = time.perf_counter()
-    eng.check_ids(roots, targets)
-    t_host = time.perf_counter() - t0
+    for _ in range(a.steps):
+        q.run()
+        runs.append(eng0.last_stats())
+    dt_res = time.perf_counter() - t0
+    assert np.array_equal(q.download(), allowed[b0:e0])
+    st = runs[-1]
 
-    n = len(roots)
-    value = n * world * a.steps / dt
-    out = None
+    out_line = None
     if rank == 0:
-        # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time
+        # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time over
+        # the timed HBM-resident runs
         plan = L.RunStats.PLANS.get(st["plan"], "unit")  # KETOGPU_UNITS=auto: the plan the engine kept
         main = {"bidi": "bidi_kernel<16>", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
+        tot = lambda k: sum(r[k] for r in runs)
         fam = {
-            main: (st["main_bytes"], st["main_ms"], 1 if st["main_ms"] > 0 else 0),
-            "spill stages (bidi w,q,s cascade or unit2 cascade)": (st["bytes_unit"] - st["main_bytes"], st["ms_unit"] - st["main_ms"],
-                                                    max(st["unit_launches"] - 1, 0)),
-            "expand_kernel": (st["bytes_push"], st["ms_push"], st["push_launches"] - st["unit_launches"]),
-            "pull_kernel": (st["bytes_pull"], st["ms_pull"], st["rounds"]),
+            main: (tot("main_bytes"), tot("main_ms"), sum(1 for r in runs if r["main_ms"] > 0)),
+            "spill stages (bidi w,q,s cascade or unit2 cascade)": (
+                tot("bytes_unit") - tot("main_bytes"), tot("ms_unit") - tot("main_ms"),
+                sum(max(r["unit_launches"] - 1, 0) for r in runs)),
+            "expand_kernel": (tot("bytes_push"), tot("ms_push"), sum(r["push_launches"] - r["unit_launches"]
+                                                                     for r in runs)),
+            "pull_kernel": (tot("bytes_pull"), tot("ms_pull"), tot("rounds")),
         }
-        gbps = {k: (b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0) for k, (b, ms, _) in fam.items()}
+        gbps = {k: (bb / (ms * 1e-3) / 1e9 if ms > 0 else 0.0) for k, (bb, ms, _) in fam.items()}
         dominant = max(fam, key=lambda k: fam[k][1])
         b_dom, ms_dom, n_launch = fam[dominant]
         achieved = gbps[dominant]
-        traffic = None
+        traffic, traffic_note = None, "no PMC summary"
         if os.path.exists(a.traffic):
             try:
                 tr = json.load(open(a.traffic))
-                if tr.get("workload") == ("config2_rbac" + ("_small" if a.small else "")):
+                src_ok = tr.get("source_hash") == kernel_source_hash()
+                if tr.get("workload") != ("config2_rbac" + ("_small" if a.small else "")):
+                    traffic_note = "PMC summary of another workload"
+                elif not src_ok:
+                    traffic_note = (f"stale: {os.path.relpath(a.traffic, ROOT)} was profiled at kernel sources "
+                                    f"{tr.get('source_hash')}, HEAD is {kernel_source_hash()}")
+                else:
                     traffic = tr.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
+                    traffic_note = f"{os.path.relpath(a.traffic, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
             except (OSError, ValueError):
-                traffic = None
+                traffic_note = "unreadable PMC summary"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": dominant,
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_note,
+                "kernel": dominant,
                 "bytes_per_launch": int(b_dom / max(n_launch, 1)), "ms_per_launch": round(ms_dom / max(n_launch, 1), 4),
-                "kernels": {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": b, "launches": n}
-                            for k, (b, ms, n) in fam.items() if ms > 0}}
+                "requests_per_launch": int(e0 - b0),
+                "kernels": {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": bb, "launches": nl}
+                            for k, (bb, ms, nl) in fam.items() if ms > 0}}
         stream = stream_copy_gbps(local)
         roof["stream_copy_GBps"] = round(stream, 1)  # measured device-copy bandwidth
         roof["frac_of_stream"] = round(achieved / stream, 4) if stream > 0 else None
         cpu = None
         parity = None
         sql = None
-        if not a.no_cpu_baseline and world == 1:
+        if not a.no_cpu_baseline and n_gpus == 1:
             cpu, parity = cpu_baseline(w, allowed, a.cpu_seconds, full=a.parity == "full")
             sql = sql_baseline(min(10.0, a.cpu_seconds))
         elif not a.no_cpu_baseline:
-            # N > 1: the CPU baseline is timed at N = 1 only; rank 0's batch still gets a
+            # N > 1: the CPU baseline is timed at N = 1 only; rank 0's range still gets a
             # bounded parity sample against the oracle
-            _, parity = cpu_baseline(w, allowed, 3.0, full=False)
-        pos = np.asarray(w.chk_pos, dtype=bool)
+            _, parity = cpu_baseline(w, allowed, 3.0, full=False, offset=b)
+        pos = np.asarray(w.chk_pos, dtype=bool)[b:e]
         parity = dict(parity or {}, constructed_positives=int(pos.sum()),
                       constructed_positives_denied=int((pos & ~allowed.astype(bool)).sum()))
-        out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "checks/s", "n_gpus": world, "steps": a.steps,
+        out_line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "checks/s", "n_gpus": n_gpus, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32 ids / u64 bitmasks (integer)",
             "data": "synthetic: config #2 RBAC generator (keto_amd/csrc/synth.cpp), seed 0x4B45544F",
             "config": {"workload": "config2_rbac" + ("_small" if a.small else ""), **sizes,
-                       "checks_per_gpu": n, "mode": "replicated graph, query batches sharded",
-                       "parallelism": f"query-shard x{world}"},
+                       "checks_per_gpu": per_gpu,
+                       "mode": "replicated graph, query batch split into contiguous word ranges",
+                       "parallelism": (f"query-shard x{n_gpus}" + (" (one process, ketogpu_multi)" if procs_gpus > 1
+                                                                 else " (one process per GPU)" if world > 1 else ""))},
+            "timing": ("host to host per step: ketogpu_check_ids over the GPU's range (requests H2D from pinned "
+                       "memory, traversal, result bits D2H); snapshot build excluded (SURVEY 8(d))"),
+            "median_call_checks_per_s": round(len(roots_all) / world / median_call, 1) if world == 1 else None,
+            "call_ms": [round(c * 1e3, 4) for c in calls],
+            "pageable_checks_per_s": round(n / t_pageable, 1),
+            "hbm_resident_checks_per_s": round((e0 - b0) * a.steps / dt_res, 1),
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
             "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)" if plan == "bidi" else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
                                           "hubs", "hub_build_ms")},
-            "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(n, 1), 2),
+            "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(e0 - b0, 1), 2),
             "allowed_fraction": round(float(allowed.mean()), 4),
-            "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2), "h2d_queries": round(t_h2d, 4)},
-            "pcie_inclusive_checks_per_s": round(n / t_host, 1),
+            "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2)},
             "snapshot": {k: v for k, v in snap.stats().items() if k.startswith("num_")},
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out_line), flush=True)
     barrier(world)
     if world > 1:
         import torch.distributed as dist
@@ -323,48 +401,51 @@ def stream_copy_gbps(device, nbytes=1 << 30, iters=10):
     return 2 * nbytes * iters / (ms * 1e-3) / 1e9
 
 
-def cpu_baseline(w, gpu_allowed, seconds, full=True):
-    """The oracle (exact restatement of the reference DFS) on host cores over a bounded
-    sample of the same requests; its answers double as a bit-exact parity sample, and with
-    `full` the rest of the batch is diffed too (every timed run is checked)."""
+def cpu_baseline(w, gpu_allowed, seconds, full=True, offset=0):
+    """The oracle (exact restatement of the reference DFS) on every host core this job may
+    use (host_cores) over a bounded sample of the same requests; its answers double as a
+    bit-exact parity sample, and with `full` the rest of the batch is diffed too (SURVEY
+    8(d): every timed run is checked).  gpu_allowed covers requests [offset, offset + len)."""
     from oracle import oracle as O
     from tests import randgraph
-    threads = min(16, os.cpu_count() or 1)
+    threads, nproc, quota = host_cores()
     t0 = time.time()
     orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
     t_build = time.time() - t0
     log(f"oracle store built in {t_build:.1f}s")
     rng = np.random.default_rng(1)
-    idx = rng.permutation(w.n_checks)
+    idx = rng.permutation(len(gpu_allowed))
     probe = idx[:2000]
     t0 = time.perf_counter()
-    ans = orc.check_batch(w.requests(probe), nthreads=threads)
+    ans = orc.check_batch(w.requests(probe + offset), nthreads=threads)
     tp = time.perf_counter() - t0
     rate = len(probe) / tp
     m = int(min(len(idx), max(len(probe), rate * seconds)))
     sample = idx[:m]
     t0 = time.perf_counter()
-    ans = orc.check_batch(w.requests(sample), nthreads=threads)
+    ans = orc.check_batch(w.requests(sample + offset), nthreads=threads)
     ts = time.perf_counter() - t0
     mism = int((ans != gpu_allowed[sample]).sum())
     checked = len(sample)
     if full and m < len(idx):
         rest = idx[m:]
         t0 = time.perf_counter()
-        ans_rest = orc.check_batch(w.requests(rest), nthreads=threads)
+        ans_rest = orc.check_batch(w.requests(rest + offset), nthreads=threads)
         log(f"parity: remaining {len(rest)} requests diffed in {time.perf_counter() - t0:.1f}s")
         mism += int((ans_rest != gpu_allowed[rest]).sum())
         checked += len(rest)
     one = idx[:max(200, m // threads)]  # the same work on one core
     t0 = time.perf_counter()
-    orc.check_batch(w.requests(one), nthreads=1)
+    orc.check_batch(w.requests(one + offset), nthreads=1)
     rate1 = len(one) / (time.perf_counter() - t0)
     del O
     return ({"value": round(len(sample) / ts, 1), "unit": "checks/s", "cores": threads, "kind": "port",
+             "nproc": nproc, "cgroup_cpu_quota": quota, "cpu_model": cpu_model(),
              "value_1_core": round(rate1, 1),
-             "sample": f"{len(sample)} of the {w.n_checks} config-2 requests (uniform sample), full 50M-tuple graph; "
-                       f"oracle/keto_oracle.c on {threads} threads of {cpu_model()}; store build {t_build:.1f}s"},
-            {"checked": checked, "of": int(w.n_checks), "mismatches": mism,
+             "sample": f"{len(sample)} of the {len(gpu_allowed)} config-2 requests (uniform sample), full 50M-tuple "
+                       f"graph; oracle/keto_oracle.c on {threads} threads (nproc {nproc}, cgroup quota {quota}) of "
+                       f"{cpu_model()}; store build {t_build:.1f}s"},
+            {"checked": checked, "of": int(len(gpu_allowed)), "mismatches": mism,
              "against": "oracle/keto_oracle.c (exact restatement of internal/check/engine.go)"})
 
 

@@ -33,19 +33,23 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 2 /* 2: ketogpu_run_stats gained hubs, hub_words, hub_build_ms, plan_unit */
+#define KETOGPU_ABI_VERSION 4 /* 4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
 
 #define KETOGPU_OK 0
 #define KETOGPU_ENOTFOUND 1 /* unknown namespace (herodot.ErrNotFound)              */
 #define KETOGPU_EINVAL 2    /* malformed input, nil subject, unsorted rows          */
 #define KETOGPU_EDEVICE 3   /* HIP runtime / device failure                          */
 #define KETOGPU_ENOMEM 4    /* host or device allocation failure                    */
+#define KETOGPU_ECOLLISION 5 /* partitioned loader: 64-bit node hash collision; reload
+                                with another ketogpu_shard_opts.salt                 */
 
 #define KETOGPU_SUBJECT_ID 0
 #define KETOGPU_SUBJECT_SET 1
 #define KETOGPU_SUBJECT_NIL (-1)
 
 #define KETOGPU_NODE_NONE 0xFFFFFFFFu /* no such node / root with no tuples      */
+#define KETOGPU_NODE_NOT_OWNED 0xFFFFFFFEu /* ketogpu_shard_resolve_batch: another rank
+                                              owns this node and resolves it          */
 
 /* builder flags */
 #define KETOGPU_BUILD_SORT 1u /* rows are NOT in ORDER BY order: sort them with the
@@ -234,9 +238,42 @@ int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n
  * ceil(n/64) words, bit i%64 of word i/64 for request i.  A flagged request touched a
  * node whose Subject.String() key is shared with another node (R4 in DESIGN.md): its bit
  * is only exact after re-evaluation with the sequential semantics (ketogpu_check does
- * that itself).  flagged_bits may be NULL. */
+ * that itself).  flagged_bits may be NULL.  Host to host: the requests are copied to HBM
+ * in chunks that overlap the traversal of the chunks before them, ids are validated on
+ * the device (an id outside the snapshot fails the call with KETOGPU_EINVAL), and the
+ * result bits come back with the run's one host synchronization.  This is the batch
+ * call SURVEY.md 8(d) times. */
 int ketogpu_check_ids(ketogpu_engine *e, const uint32_t *roots, const uint32_t *targets, size_t n,
                       uint64_t *allowed_bits, uint64_t *flagged_bits);
+
+/* Pinned host memory (hipHostMalloc) for request and result arrays.  A batch whose
+ * roots/targets live here is copied by DMA at full PCIe rate; the cgo micro-batcher
+ *  fills such a buffer in place instead of a Go slice, which it has to
+ * copy into C memory anyway (cgo pointer rules).  Any host memory works with
+ * ketogpu_check_ids; pageable memory is staged by the HIP runtime. */
+int ketogpu_host_alloc(size_t bytes, void **out);
+void ketogpu_host_free(void *p);
+
+/* ------------------------------------------------------ replicated multi-GPU */
+/* One engine per listed device over the same snapshot (the graph replicated in every
+ * GPU's HBM, SURVEY.md 8(e) "Replicated"); replaces scaling out by more Keto processes
+ * (internal/driver/daemon.go:87-159) with one PermissionEngine per process
+ * (internal/driver/registry_default.go:158-163) that drives the whole node.
+ * ketogpu_multi_check_ids splits the batch into ketogpu_multi_size() contiguous ranges of
+ * whole 64-request words (ketogpu_multi_range), runs ketogpu_check_ids on every device
+ * concurrently from one host thread per device and writes each range's bits at its
+ * offset of allowed_bits / flagged_bits.  No communication between devices. */
+typedef struct ketogpu_multi ketogpu_multi;
+int ketogpu_multi_new(const ketogpu_snapshot *s, const int32_t *devices, size_t num_devices,
+                      const ketogpu_engine_opts *opts, ketogpu_multi **out);
+void ketogpu_multi_free(ketogpu_multi *m);
+size_t ketogpu_multi_size(const ketogpu_multi *m);
+/* the engine of device slot i (statistics); owned by m */
+ketogpu_engine *ketogpu_multi_engine(ketogpu_multi *m, size_t i);
+int ketogpu_multi_check_ids(ketogpu_multi *m, const uint32_t *roots, const uint32_t *targets, size_t n,
+                            uint64_t *allowed_bits, uint64_t *flagged_bits);
+/* requests [*begin, *end) of part i when n requests are split into `parts` ranges */
+void ketogpu_multi_range(size_t n, size_t parts, size_t i, size_t *begin, size_t *end);
 
 /* device-resident query sets: upload once, run many times (results stay in HBM) */
 int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint32_t *targets,
@@ -290,12 +327,94 @@ typedef struct {
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 
+/* ----------------------------------------------- partition-aware loader */
+/* BASELINE config #5 (SURVEY.md 8(e) "Partitioned"): a graph that fits neither one GPU nor
+ * one host.  Every rank streams the same ordered row read the single-GPU loader takes
+ * (ketogpu_builder_*; internal/persistence/sql/relationtuples.go:203-258 with the ORDER
+ * BY of :215, one nid, persister.go:94-96) and keeps only what it owns: node v (a typed
+ * subject, internal/relationtuple/definitions.go:253-267) belongs to rank
+ * hash(v, salt) % world; a rank keeps the rows of the groups it owns (forward rows) and
+ * the rows whose subject it owns (reverse rows), after the reference's page poisoning
+ * (R7), so no rank interns or holds the whole graph.  Owners number their nodes; the ids
+ * of referenced nodes owned elsewhere come from one exchange the caller carries out
+ * (keto_amd/partition.py: torch.distributed all_to_all / all_gather):
+ *   builder_new/append.../finish -> counts -> [all_gather] -> set_layout
+ *   -> queries -> [all_to_all] -> answer -> [all_to_all] -> apply
+ *   -> claims -> [all_to_all] -> check_claims -> [all_reduce: any ambiguous key -> refuse]
+ * Graphs the partitioned engine does not evaluate are refused on every rank alike:
+ * wildcard subject sets (R5) and rows out of ORDER BY order with KETOGPU_EINVAL, shared
+ * Subject.String() keys (R4) by check_claims' count.  Node ids: within each class (interior,
+ * other expandable, never expanded) ids interleave the ranks, so owner and local index are
+ * arithmetic (partition.hip); interior ids stay the smallest. */
+typedef struct ketogpu_shard_builder ketogpu_shard_builder;
+typedef struct ketogpu_shard ketogpu_shard;
+typedef struct {
+    int32_t page_size; /* GetRelationTuples page size; 0 -> 100                        */
+    uint32_t flags;    /* KETOGPU_ORDER_* (rows must arrive in ORDER BY order)          */
+    int32_t rank, world; /* world <= 64                                                 */
+    uint64_t salt;     /* node hash salt; retry another after KETOGPU_ECOLLISION       */
+} ketogpu_shard_opts;
+typedef struct {
+    uint64_t rows, bad_rows;             /* rows streamed; rows with unknown namespaces */
+    uint64_t owned_nodes, owned_interior, owned_expandable;
+    uint64_t forward_edges;              /* kept forward row entries (before dedup)     */
+    uint64_t interior_forward_edges;     /* device forward rows (interior, deduplicated) */
+    uint64_t reverse_edges;              /* reverse row entries                         */
+    uint64_t queries;                    /* distinct referenced nodes (id exchange)     */
+    uint64_t ambiguous_keys;             /* check_claims: shared String() keys found    */
+    uint64_t num_interior, num_expandable, num_nodes; /* global id layout (Ni, Nx, N)   */
+    uint64_t host_bytes;                 /* peak bytes of the loader's own arrays       */
+    double seconds;                      /* streaming time                              */
+} ketogpu_shard_stats;
+int ketogpu_shard_builder_new(const ketogpu_namespace *namespaces, size_t num_namespaces,
+                              const ketogpu_shard_opts *opts, ketogpu_shard_builder **out);
+int ketogpu_shard_builder_append(ketogpu_shard_builder *b, const ketogpu_row_batch *rows);
+/* consumes b (also on failure) */
+int ketogpu_shard_builder_finish(ketogpu_shard_builder *b, ketogpu_shard **out);
+void ketogpu_shard_builder_free(ketogpu_shard_builder *b);
+void ketogpu_shard_free(ketogpu_shard *s);
+/* this rank's node counts per class; every rank's (world x 3, rank order) to set_layout */
+int ketogpu_shard_counts(const ketogpu_shard *s, uint64_t counts[3]);
+int ketogpu_shard_set_layout(ketogpu_shard *s, const uint64_t *all_counts);
+/* distinct node hashes this rank references, grouped by owner (counts[world]) */
+uint64_t ketogpu_shard_query_count(const ketogpu_shard *s);
+int ketogpu_shard_queries(const ketogpu_shard *s, uint64_t *hashes, uint64_t capacity, uint64_t *counts);
+/* owner side: the global ids of received hashes (all owned by this rank) */
+int ketogpu_shard_answer(const ketogpu_shard *s, const uint64_t *hashes, uint64_t n, uint32_t *ids);
+/* the answers, in the order of ketogpu_shard_queries: builds the device rows */
+int ketogpu_shard_apply(ketogpu_shard *s, const uint32_t *ids, uint64_t n);
+/* R4: (String() key hash, node hash) pairs of owned nodes whose key another node could
+ * share, grouped by the key hash's owner; the receiver counts keys held by >= 2 nodes */
+uint64_t ketogpu_shard_claim_count(const ketogpu_shard *s);
+int ketogpu_shard_claims(const ketogpu_shard *s, uint64_t *pairs, uint64_t capacity, uint64_t *counts);
+int ketogpu_shard_check_claims(ketogpu_shard *s, const uint64_t *pairs, uint64_t n, uint64_t *ambiguous);
+/* ketogpu_resolve_batch for a shard: ids of the requests' roots and targets this rank owns,
+ * KETOGPU_NODE_NOT_OWNED for the others (the owner's answer is the one that counts);
+ * status ENOTFOUND for wildcard roots (not evaluated partitioned), EINVAL nil subjects */
+int ketogpu_shard_resolve_batch(const ketogpu_shard *s, const ketogpu_request_batch *reqs, uint32_t *roots,
+                                uint32_t *targets, int32_t *status);
+int ketogpu_shard_stats_get(const ketogpu_shard *s, ketogpu_shard_stats *out);
+/* read-only view of the rank's device rows (tools, tests); global node ids */
+typedef struct {
+    uint32_t rank, world;
+    uint32_t num_interior, num_expandable, num_nodes;       /* Ni, Nx, N (global)      */
+    uint32_t owned_interior, owned_expandable, owned_nodes; /* local class bounds      */
+    const uint64_t *lf_off; /* owned_expandable + 1: interior successors               */
+    const uint32_t *lf_col;
+    const uint64_t *lr_off; /* owned_nodes + 1: expandable predecessors, sorted          */
+    const uint32_t *lr_col;
+    const uint64_t *lb_off; /* owned_interior + 1: interior predecessors                */
+    const uint32_t *lb_col;
+} ketogpu_shard_graph;
+int ketogpu_shard_view(const ketogpu_shard *s, ketogpu_shard_graph *out);
+
 /* ------------------------------------------------------- partitioned mode */
 /* Hash-partitioned traversal for graphs that do not fit one GPU (BASELINE config #5,
  * SURVEY.md 8(e)); replaces the same SubjectIsAllowed recursion as ketogpu_check_ids
- * (internal/check/engine.go:33-95), spread over ranks.  Node v is owned by rank
- * ketogpu_part_owner(v, world) = mix64(v) % world; a rank holds the forward interior rows
- * and traversal state of its expandable nodes and the reverse rows of its nodes.  These
+ * (internal/check/engine.go:33-95), spread over ranks.  A rank's partition is its loaded
+ * shard (ketogpu_shard_*): it holds the forward interior rows and traversal state of its
+ * expandable nodes and the reverse rows of its nodes; ketogpu_part_owner(v) names the
+ * rank that owns global node id v.  These
  * calls are one rank's device steps of a round; the caller moves the records between
  * ranks (keto_amd/partition.py: torch.distributed all_to_all over RCCL):
  *   begin -> { emit -> [all-to-all] -> apply -> [all-reduce frontier; stop at 0] -> expand }
@@ -322,8 +441,9 @@ typedef struct {
     uint64_t rounds, levels, frontier_entries, forward_edges;
     uint64_t records_sent, records_received, queries_answered;
 } ketogpu_part_stats;
-uint32_t ketogpu_part_owner(uint32_t node, int32_t world);
-int ketogpu_part_new(const ketogpu_snapshot *s, const ketogpu_part_opts *opts, ketogpu_part **out);
+/* opts->rank / world must match the shard's */
+int ketogpu_part_new(const ketogpu_shard *s, const ketogpu_part_opts *opts, ketogpu_part **out);
+uint32_t ketogpu_part_owner(const ketogpu_part *p, uint32_t node);
 void ketogpu_part_free(ketogpu_part *p);
 /* 64-request words one round holds */
 uint64_t ketogpu_part_round_words(const ketogpu_part *p);

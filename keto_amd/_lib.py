@@ -158,6 +158,14 @@ SIGNATURES = {
     "ketogpu_abi_version": (C.c_int, []),
     "ketogpu_free": (None, [vp]),
     "ketogpu_device_count": (C.c_int, []),
+    "ketogpu_host_alloc": (C.c_int, [sz, C.POINTER(vp)]),
+    "ketogpu_host_free": (None, [vp]),
+    "ketogpu_multi_new": (C.c_int, [vp, vp, sz, C.POINTER(EngineOpts), C.POINTER(vp)]),
+    "ketogpu_multi_free": (None, [vp]),
+    "ketogpu_multi_size": (sz, [vp]),
+    "ketogpu_multi_engine": (vp, [vp, sz]),
+    "ketogpu_multi_check_ids": (C.c_int, [vp, vp, vp, sz, vp, vp]),
+    "ketogpu_multi_range": (None, [sz, sz, sz, C.POINTER(sz), C.POINTER(sz)]),
     "ketogpu_part_owner": (C.c_uint32, [u32, i32]),
     "ketogpu_part_new": (C.c_int, [vp, C.POINTER(PartOpts), C.POINTER(vp)]),
     "ketogpu_part_free": (None, [vp]),

@@ -14,8 +14,20 @@ SYNTH_LIB = os.path.join(HERE, "libketosynth.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
 
-SOURCES = ["snapshot.cpp", "snapshot_io.cpp", "host_engine.cpp", "device_engine.hip", "partition.hip"]
+SOURCES = ["snapshot.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "device_engine.hip", "partition.hip"]
 HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
+
+
+def kernel_source_hash():
+    """hash of the traversal kernels' sources.  A PMC traffic summary records the hash it
+    was profiled at (tools/pmc_traffic.py); bench.py reports its traffic only while the
+    hash still matches, so a stale figure never passes as current."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("device_engine.hip", "device_util.hpp"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _stale(out, deps):

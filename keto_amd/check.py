@@ -23,10 +23,19 @@ class Engine:
         h = C.c_void_p()
         L.check(self.L.ketogpu_engine_new(snapshot.h, C.byref(opts), C.byref(h)))
         self.h = h
+        self.owned = True
+
+    @classmethod
+    def borrowed(cls, handle, snapshot, owner):
+        """a view of an engine owned by something else (MultiEngine.engine(i))"""
+        e = cls.__new__(cls)
+        e.L, e.snapshot, e.h, e.owned, e._owner = L.lib(), snapshot, C.c_void_p(handle), False, owner
+        return e
 
     def close(self):
         if getattr(self, "h", None):
-            self.L.ketogpu_engine_free(self.h)
+            if getattr(self, "owned", True):
+                self.L.ketogpu_engine_free(self.h)
             self.h = None
 
     def __del__(self):
@@ -64,6 +73,10 @@ class Engine:
         allowed = unpack_bits(ab, n)
         return (allowed, unpack_bits(fb, n)) if with_flags else allowed
 
+    def check_ids_raw(self, roots_ptr, targets_ptr, n, allowed_ptr, flagged_ptr=None):
+        """the C call on caller-owned (e.g. pinned) buffers, no conversions (benchmarks)"""
+        L.check(self.L.ketogpu_check_ids(self.h, roots_ptr, targets_ptr, n, allowed_ptr, flagged_ptr))
+
     def upload(self, roots, targets):
         return DeviceQueries(self, roots, targets)
 
@@ -71,6 +84,97 @@ class Engine:
         st = L.RunStats()
         L.check(self.L.ketogpu_engine_last_stats(self.h, C.byref(st)))
         return st.as_dict()
+
+
+class PinnedBuffer:
+    """pinned host memory (ketogpu_host_alloc) viewed as a numpy array: a request batch
+    written here is copied to HBM by DMA at full PCIe rate by check_ids"""
+
+    def __init__(self, n, dtype=np.uint32):
+        self.L = L.lib()
+        dt = np.dtype(dtype)
+        p = C.c_void_p()
+        L.check(self.L.ketogpu_host_alloc(max(n, 1) * dt.itemsize, C.byref(p)))
+        self.p = p
+        buf = (C.c_char * (max(n, 1) * dt.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dt)[:n]
+
+    def close(self):
+        if getattr(self, "p", None):
+            self.array = None
+            self.L.ketogpu_host_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        self.close()
+
+
+def pinned(values, dtype=np.uint32):
+    """a PinnedBuffer holding a copy of `values` (keep the buffer alive while it is used)"""
+    values = np.asarray(values, dtype=dtype)
+    b = PinnedBuffer(len(values), dtype)
+    b.array[:] = values
+    return b
+
+
+class MultiEngine:
+    """One engine per device over the same snapshot (ketogpu_multi_*): check_ids splits a
+    batch into contiguous 64-request-word ranges, one per device, run concurrently; the
+    answers are exactly Engine.check_ids's (SURVEY.md 8(e) "Replicated")."""
+
+    def __init__(self, snapshot: Snapshot, devices, max_words_per_round=0, state_budget_bytes=0):
+        self.L = L.lib()
+        self.snapshot = snapshot
+        self.devices = [int(d) for d in devices]
+        dev = (C.c_int32 * max(len(self.devices), 1))(*self.devices)
+        opts = L.EngineOpts(0, max_words_per_round, state_budget_bytes)
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_multi_new(snapshot.h, dev, len(self.devices), C.byref(opts), C.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def ranges(n, parts):
+        lib = L.lib()
+        out = []
+        for i in range(parts):
+            b, e = C.c_size_t(), C.c_size_t()
+            lib.ketogpu_multi_range(n, parts, i, C.byref(b), C.byref(e))
+            out.append((b.value, e.value))
+        return out
+
+    def check_ids(self, roots, targets, with_flags=False):
+        roots = np.ascontiguousarray(roots, dtype=np.uint32)
+        targets = np.ascontiguousarray(targets, dtype=np.uint32)
+        n = len(roots)
+        words = max((n + 63) // 64, 1)
+        ab = np.zeros(words, dtype=np.uint64)
+        fb = np.zeros(words, dtype=np.uint64)
+        L.check(self.L.ketogpu_multi_check_ids(self.h, roots.ctypes.data, targets.ctypes.data, n, ab.ctypes.data,
+                                               fb.ctypes.data))
+        allowed = unpack_bits(ab, n)
+        return (allowed, unpack_bits(fb, n)) if with_flags else allowed
+
+    def check_ids_raw(self, roots_ptr, targets_ptr, n, allowed_ptr, flagged_ptr=None):
+        """the C call on caller-owned (e.g. pinned) buffers, no conversions (benchmarks)"""
+        L.check(self.L.ketogpu_multi_check_ids(self.h, roots_ptr, targets_ptr, n, allowed_ptr, flagged_ptr))
+
+    def last_stats(self, i=0):
+        return self.engine(i).last_stats()
+
+    def engine(self, i):
+        """the engine of device slot i (a borrowed view: statistics, HBM-resident queries)"""
+        h = self.L.ketogpu_multi_engine(self.h, i)
+        if not h:
+            raise IndexError(i)
+        return Engine.borrowed(h, self.snapshot, self)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ketogpu_multi_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def unpack_bits(words, n):

@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1517,26 +1518,30 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     }
 }
 
-// Stage kernel.  in_count == nullptr: workgroup b runs unit parents ? parents[b] : b.
+// Stage kernel.  in_count == nullptr: workgroup b runs unit parents ? parents[b] : unit0 + b.
 // Otherwise persistent: the workgroups stride over the *in_count units listed in
 // parents (the previous stage's spills), so the stage is launched without the host
 // reading that count first.
 // WPE > 1 asks the compiler for at least WPE waves per SIMD (VGPR budget 512 / WPE): with
 // 5 KB of LDS, 8-request units could run 32 per CU at WPE 8
-template <int U, int HLOG, int F, int BT, int LF, int WPE = 1>
+// CHUNKED = 1: the same kernel for the pipelined host-to-host first stage (check_host),
+// one launch per chunk; a separate symbol keeps its launches apart in kernel traces.
+template <int U, int HLOG, int F, int BT, int LF, int WPE = 1, int CHUNKED = 0>
 __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(WPE)))
 void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                   const uint32_t *roots, const uint32_t *targets, uint64_t n,
                                                   uint64_t *allowed, const uint32_t *parents,
                                                   const unsigned int *in_count, uint32_t fan, uint32_t *spill_out,
                                                   unsigned int *spill_count, unsigned long long *stats,
-                                                  unsigned long long *stamps) {
+                                                  unsigned long long *stamps, uint64_t unit0) {
     __shared__ BidiShared<U, HLOG, F, BT, LF> S;
     const uint64_t units = (n + U - 1) / U;
     if (!in_count) {
         unsigned long long *stamp =
             (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
-        const uint64_t unit = parents ? parents[blockIdx.x] : blockIdx.x;
+        // unit0: a pipelined batch launches its units chunk by chunk, as each chunk of
+        // requests arrives in HBM (ketogpu_engine::check_host)
+        const uint64_t unit = parents ? parents[blockIdx.x] : unit0 + blockIdx.x;
         uint32_t r, t;
         bidi_load_rt<U>(unit, units, roots, targets, n, r, t);
         bidi_unit<U, HLOG, F, BT, LF>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out,
@@ -1565,6 +1570,21 @@ __global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t *a, uint64_t na,
             b[i - na] = 0;
         else
             c[i - na - nb] = 0;
+    }
+}
+
+// Device-side request validation (no host pass over the batch): an id outside the
+// snapshot becomes NONE before any traversal kernel reads it, and the smallest such
+// request index is recorded; the call then fails with KETOGPU_EINVAL.
+__global__ __launch_bounds__(kBlock) void validate_kernel(uint32_t *roots, uint32_t *targets, uint64_t n, uint32_t Nx,
+                                                          uint32_t N, uint64_t base, unsigned long long *first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = roots[i], t = targets[i];
+    if ((r != KETOGPU_NODE_NONE && r >= Nx) || (t != KETOGPU_NODE_NONE && t >= N)) {
+        roots[i] = KETOGPU_NODE_NONE;
+        targets[i] = KETOGPU_NODE_NONE;
+        atomicMin(first_bad, (unsigned long long)(base + i));
     }
 }
 
@@ -1913,6 +1933,11 @@ struct Batch {
     bool has_dyn = false;
 };
 
+// host arrays of a batch that check_host copies in chunk by chunk
+struct HostSrc {
+    const uint32_t *roots, *targets;
+};
+
 struct ketogpu_queries {
     uint64_t n = 0;
     uint32_t *d_roots = nullptr, *d_targets = nullptr;
@@ -1990,11 +2015,17 @@ struct ketogpu_engine {
 
     void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
-                     unsigned long long *stp) {
+                     unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
+        if (!stream) stream = this->stream;
+        if (chunked && c == BidiCfg{9, 64, 128, 7, 16, 1}) {  // the default shape's chunk instantiation
+            KLAUNCH((bidi_kernel<16, 9, 128, 64, 7, 1, 1>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
+                    q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp, unit0);
+            return;
+        }
 #define KETO_BIDI_U(U, HL, F, BT, LF, WPE)                                                                        \
     if (c == BidiCfg{HL, BT, F, LF, U, WPE}) {                                                                   \
         KLAUNCH((bidi_kernel<U, HL, F, BT, LF, WPE>), dim3(grid), dim3(BT), pad, stream, g, frec, brec,          \
-                q.roots, q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp);          \
+                q.roots, q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp, unit0);   \
         return;                                                                                                  \
     }
 #define KETO_BIDI(HL, F, BT, LF) KETO_BIDI_U(16, HL, F, BT, LF, 1)
@@ -2033,23 +2064,23 @@ struct ketogpu_engine {
         switch (sg.kind) {
         case 'w':
             KLAUNCH((bidi_kernel<16, 11, 384, 256, 6>), dim3(1024), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'q':
             KLAUNCH((bidi_kernel<4, 12, 512, 256, 7>), dim3(512), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'h':
             KLAUNCH((bidi_kernel<16, 10, 256, 64, 6>), dim3(2048), dim3(64), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'r':
             KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(1280), dim3(64), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         default:
             KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(256), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr);
+                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         }
     }
@@ -2099,6 +2130,13 @@ struct ketogpu_engine {
     uint64_t *hub_mask = nullptr;
     double hub_build_ms = 0;
     hipEvent_t unit_end = nullptr;  // last event of the bidi cascade (already complete after its sync)
+    // host-to-host batches (check_host): persistent request/result buffers in HBM, a copy
+    // stream for the chunked request upload and a second compute stream
+    ketogpu_queries *io = nullptr;
+    uint64_t io_cap = 0;
+    hipStream_t copy_stream = nullptr, stream2 = nullptr;
+    unsigned long long *d_bad = nullptr;  // smallest request index with an id outside the snapshot
+    uint64_t pipe_chunk = 1 << 18;        // requests per pipelined chunk (KETOGPU_PIPE_CHUNK)
 
     hipEvent_t ev() {
         if (ev_used == ev_pool.size()) {
@@ -2120,6 +2158,9 @@ struct ketogpu_engine {
                         (void *)spill_flags})
             if (p) (void)hipFree(p);
         if (h_ctr) (void)hipHostFree(h_ctr);
+        delete io;
+        for (hipStream_t x : {copy_stream, stream2})
+            if (x) (void)hipStreamDestroy(x);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -2131,6 +2172,10 @@ struct ketogpu_engine {
         if (device < 0 || device >= ndev) throw Error(KETOGPU_EDEVICE, "no such HIP device");
         HIP_CHECK(hipSetDevice(device));
         HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+        if (const char *pc = getenv("KETOGPU_PIPE_CHUNK"))  // requests per chunk, rounded to 64
+            pipe_chunk = std::max<uint64_t>(64, (uint64_t)atoll(pc) / 64 * 64);
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
@@ -2266,6 +2311,8 @@ struct ketogpu_engine {
         spill_count = (unsigned int *)(st.stats + 8 + 8 * kStatSlots + 8);
         for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats}) owned.push_back(p);  // spill_count lives in st.stats
         HIP_CHECK(hipHostMalloc((void **)&h_ctr, 64 * sizeof(uint64_t), hipHostMallocDefault));
+        d_bad = dalloc<unsigned long long>(1);
+        owned.push_back(d_bad);
         HIP_CHECK(hipStreamSynchronize(stream));
         build_hubs(s);
     }
@@ -2392,10 +2439,65 @@ struct ketogpu_engine {
         return (uint32_t)h_ctr[12];
     }
 
+    // After a bidi first stage over the whole batch q (its spilled units in list[0],
+    // counted in spill_count[0]; events a -> b around it): the spill stages of `cascade`
+    // (persistent over the previous stage's spilled units, counts read on the device),
+    // the statistics reduction and ONE host synchronization.  `before_sync` enqueues
+    // more work (result copies) ahead of that synchronization.  Returns the number of
+    // single requests left in spill_units[0..) for the global path.
+    uint64_t bidi_tail(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &unit_ev,
+                       hipEvent_t a, hipEvent_t b, uint64_t bunits, const std::function<void()> &before_sync = {}) {
+        uint32_t *list[2] = {spill_units, spill_units + spill_cap};
+        hipEvent_t d = ev();
+        // spill stages of no more requests per unit than the stage before (an 8-request
+        // first stage skips the 16-request stage w)
+        std::vector<SpillStage> stages;
+        for (const SpillStage &sg : cascade)
+            if (sg.u <= (stages.empty() ? bidi_cfg.u : stages.back().u)) stages.push_back(sg);
+        int cur = 0, u_prev = bidi_cfg.u;
+        for (size_t k = 0; k < stages.size(); k++) {
+            const SpillStage sg = stages[k];
+            launch_stage(sg, q, list[cur], &spill_count[k], (uint32_t)(u_prev / sg.u), list[cur ^ 1],
+                         &spill_count[k + 1], st.stats + 4 * kStatSlots);
+            cur ^= 1;
+            u_prev = sg.u;
+        }
+        HIP_CHECK(hipEventRecord(d, stream));
+        const size_t ns = stages.size() + 1;
+        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
+        // the spill counters sit 8 words after the reduced statistics (st.stats
+        // layout, kStatsLen): one copy brings both to h_ctr[16..21] and h_ctr + 24
+        static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
+        // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        if (before_sync) before_sync();
+        HIP_CHECK(hipStreamSynchronize(stream));
+        unit_end = d;
+        unit_ev.push_back({a, b});
+        unit_ev.push_back({b, d});
+        const uint64_t *t = (const uint64_t *)h_ctr + 16;
+        rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
+        const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
+        if (cascade_log) {
+            fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)bunits);
+            for (size_t k = 0; k < ns; k++) fprintf(stderr, " %u", cnt[k]);
+            fprintf(stderr, "\n");
+        }
+        for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
+        rs.push_launches += ns;
+        rs.unit_launches += ns;
+        const uint64_t left = cnt[ns - 1];
+        if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
+        if (left && cur != 0)  // single requests for the global path, read from list[0]
+            HIP_CHECK(hipMemcpyAsync(list[0], list[cur], left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+        return left;
+    }
+
     // The LDS cascade: 16-request units, then 4-request and 1-request units for what
     // spilled.  Returns the number of single requests left in spill_units[0..) for the
     // global path.
-    uint64_t run_units(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &unit_ev) {
+    uint64_t run_units(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &unit_ev,
+                       const HostSrc *src = nullptr, const std::function<void()> &before_sync = {}) {
         ensure_spill(q.n);
         uint32_t *list[2] = {spill_units, spill_units + spill_cap};
         if (wave_u) {
@@ -2447,54 +2549,41 @@ struct ketogpu_engine {
                 // `cascade` (persistent over the previous stage's spilled units, counts read
                 // on the device), then the global path for single requests that exceed the
                 // last table; one host synchronization for counts and statistics
-                hipEvent_t a = ev(), b = ev(), d = ev();
+                hipEvent_t a = ev(), b = ev();
                 HIP_CHECK(hipEventRecord(a, stream));
                 const uint64_t bunits = (q.n + bidi_cfg.u - 1) / bidi_cfg.u;
-                launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
-                            st.stats, stamps);
+                if (!src) {
+                    launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
+                                st.stats, stamps);
+                } else {
+                    // Host-to-host batch (check_host): the requests arrive in chunks on the
+                    // copy stream; each chunk is validated and its units launched as soon as
+                    // it lands, alternating two streams so one chunk's tail overlaps the next
+                    // chunk's start.  All chunks append spilled units to the one list, so the
+                    // spill stages below run once for the whole batch.
+                    HIP_CHECK(hipStreamWaitEvent(stream2, a, 0));  // after the clear
+                    const uint64_t U = (uint64_t)bidi_cfg.u, chunk = pipe_chunk;
+                    for (uint64_t c0 = 0, k = 0; c0 < q.n; c0 += chunk, k++) {
+                        const uint64_t m = std::min<uint64_t>(chunk, q.n - c0);
+                        HIP_CHECK(hipMemcpyAsync(io->d_roots + c0, src->roots + c0, m * 4, hipMemcpyHostToDevice,
+                                                 copy_stream));
+                        HIP_CHECK(hipMemcpyAsync(io->d_targets + c0, src->targets + c0, m * 4, hipMemcpyHostToDevice,
+                                                 copy_stream));
+                        hipEvent_t h = ev();
+                        HIP_CHECK(hipEventRecord(h, copy_stream));
+                        hipStream_t cs = (k & 1) ? stream2 : stream;
+                        HIP_CHECK(hipStreamWaitEvent(cs, h, 0));
+                        KLAUNCH(validate_kernel, dim3(blocks_for(m)), dim3(kBlock), 0, cs, io->d_roots + c0,
+                                io->d_targets + c0, m, g.Nx, g.N, c0, d_bad);
+                        launch_bidi(bidi_cfg, (unsigned)((m + U - 1) / U), lds_pad, q, nullptr, nullptr, list[0],
+                                    &spill_count[0], st.stats, nullptr, c0 / U, cs, true);
+                    }
+                    hipEvent_t j = ev();
+                    HIP_CHECK(hipEventRecord(j, stream2));
+                    HIP_CHECK(hipStreamWaitEvent(stream, j, 0));
+                }
                 HIP_CHECK(hipEventRecord(b, stream));
-                // spill stages of no more requests per unit than the stage before (an 8-request
-                // first stage skips the 16-request stage w)
-                std::vector<SpillStage> stages;
-                for (const SpillStage &sg : cascade)
-                    if (sg.u <= (stages.empty() ? bidi_cfg.u : stages.back().u)) stages.push_back(sg);
-                int cur = 0, u_prev = bidi_cfg.u;
-                for (size_t k = 0; k < stages.size(); k++) {
-                    const SpillStage sg = stages[k];
-                    launch_stage(sg, q, list[cur], &spill_count[k], (uint32_t)(u_prev / sg.u), list[cur ^ 1],
-                                 &spill_count[k + 1], st.stats + 4 * kStatSlots);
-                    cur ^= 1;
-                    u_prev = sg.u;
-                }
-                HIP_CHECK(hipEventRecord(d, stream));
-                const size_t ns = stages.size() + 1;
-                KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
-                // the spill counters sit 8 words after the reduced statistics (st.stats
-                // layout, kStatsLen): one copy brings both to h_ctr[16..21] and h_ctr + 24
-                static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
-                // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
-                HIP_CHECK(hipStreamSynchronize(stream));
-                unit_end = d;
-                unit_ev.push_back({a, b});
-                unit_ev.push_back({b, d});
-                const uint64_t *t = (const uint64_t *)h_ctr + 16;
-                rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
-                const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
-                if (cascade_log) {
-                    fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)bunits);
-                    for (size_t k = 0; k < ns; k++) fprintf(stderr, " %u", cnt[k]);
-                    fprintf(stderr, "\n");
-                }
-                for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
-                rs.push_launches += ns;
-                rs.unit_launches += ns;
-                left = cnt[ns - 1];
-                if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
-                if (left && cur != 0)  // single requests for the global path, read from list[0]
-                    HIP_CHECK(hipMemcpyAsync(list[0], list[cur], left * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                                             stream));
-                return left;
+                return bidi_tail(q, rs, unit_ev, a, b, bunits, before_sync);
             }
             uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
             struct Stage {
@@ -2720,7 +2809,9 @@ struct ketogpu_engine {
         run_once(qq);
     }
 
-    void run_once(ketogpu_queries &qq) {
+    // src: the requests are still on the host (check_host's pipelined first stage copies
+    // them in); before_sync: copies enqueued ahead of the first-stage synchronization
+    void run_once(ketogpu_queries &qq, const HostSrc *src = nullptr, const std::function<void()> &before_sync = {}) {
         Batch q = qq.batch();
         ketogpu_run_stats rs{};
         rs.checks = q.n;
@@ -2744,7 +2835,7 @@ struct ketogpu_engine {
         if (!bidi_first) HIP_CHECK(hipEventRecord(t_begin, stream));
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
-            uint64_t ns = run_units(q, rs, unit_ev);
+            uint64_t ns = run_units(q, rs, unit_ev, src, before_sync);
             if (bidi_first) {
                 if (!unit_ev.empty())
                     t_begin = unit_ev.front().first;
@@ -2819,7 +2910,69 @@ struct ketogpu_engine {
         if (stamps && use_units && !wave_u) report_stamps();
     }
 
-    ketogpu_queries *upload(const uint32_t *roots, const uint32_t *targets, uint64_t n) {
+    void ensure_io(uint64_t n) {
+        if (io && n <= io_cap) return;
+        delete io;
+        io = nullptr;
+        io_cap = std::max<uint64_t>((n + 63) / 64 * 64, 1 << 16);
+        auto q = std::make_unique<ketogpu_queries>();
+        q->d_roots = dalloc<uint32_t>(io_cap);
+        q->d_targets = dalloc<uint32_t>(io_cap);
+        q->d_allowed = dalloc<uint64_t>(io_cap / 64);
+        q->d_flags = dalloc<uint64_t>(io_cap / 64);
+        io = q.release();
+    }
+
+    void check_bad(uint64_t first_bad) {
+        if (first_bad != ~0ull)
+            throw Error(KETOGPU_EINVAL, "request " + std::to_string(first_bad) + " has a node id outside the snapshot");
+    }
+
+    // SubjectIsAllowed over a batch held in host memory (SURVEY 8(d) "throughput timing":
+    // requests H2D, traversal, result bits D2H).  Persistent HBM buffers, ids validated on
+    // the device, and with the bidi plan a pipelined first stage (run_units, HostSrc): the
+    // chunks' uploads overlap the traversal of the chunks before them, and the result copy
+    // is enqueued ahead of the run's one host synchronization.  Host arrays allocated
+    // with ketogpu_host_alloc (pinned) are copied by DMA at full PCIe rate.
+    void check_host(const uint32_t *roots, const uint32_t *targets, uint64_t n, uint64_t *allowed, uint64_t *flagged) {
+        HIP_CHECK(hipSetDevice(device));
+        ensure_io(n);
+        ketogpu_queries &q = *io;
+        q.n = n;
+        const uint64_t words = (n + 63) / 64;
+        HIP_CHECK(hipMemsetAsync(d_bad, 0xFF, sizeof(unsigned long long), stream));
+        const bool pipe = n >= 2 * pipe_chunk && use_units && !wave_u && use_v2 && use_bidi &&
+                          !(trials_left && n >= kTrialMin);
+        if (!pipe) {
+            if (n) {
+                HIP_CHECK(hipMemcpyAsync(q.d_roots, roots, n * 4, hipMemcpyHostToDevice, stream));
+                HIP_CHECK(hipMemcpyAsync(q.d_targets, targets, n * 4, hipMemcpyHostToDevice, stream));
+                KLAUNCH(validate_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, q.d_roots, q.d_targets, n, g.Nx,
+                        g.N, 0ull, d_bad);
+            }
+            run(q);
+        } else {
+            const HostSrc src{roots, targets};
+            run_once(q, &src, [&] {
+                if (words && allowed)
+                    HIP_CHECK(hipMemcpyAsync(allowed, q.d_allowed, words * 8, hipMemcpyDeviceToHost, stream));
+                if (words && flagged)
+                    HIP_CHECK(hipMemcpyAsync(flagged, q.d_flags, words * 8, hipMemcpyDeviceToHost, stream));
+                HIP_CHECK(hipMemcpyAsync(h_ctr + 40, d_bad, 8, hipMemcpyDeviceToHost, stream));
+            });
+            // the copies above were final unless requests went on to the global path
+            if (!last.spilled_requests) {
+                check_bad(h_ctr[40]);
+                return;
+            }
+        }
+        HIP_CHECK(hipMemcpyAsync(h_ctr + 40, d_bad, 8, hipMemcpyDeviceToHost, stream));
+        download(q, allowed, flagged);  // synchronizes
+        check_bad(h_ctr[40]);
+    }
+
+    // validate = false: ids built by the library itself (ketogpu_check, dynamic roots)
+    ketogpu_queries *upload(const uint32_t *roots, const uint32_t *targets, uint64_t n, bool validate = true) {
         HIP_CHECK(hipSetDevice(device));
         auto q = std::make_unique<ketogpu_queries>();
         q->n = n;
@@ -2833,7 +2986,14 @@ struct ketogpu_engine {
             HIP_CHECK(hipMemcpyAsync(q->d_targets, targets, n * 4, hipMemcpyHostToDevice, stream));
         }
         HIP_CHECK(hipMemsetAsync(q->d_allowed, 0, words * 8, stream));
+        if (validate && n) {  // never launch on ids the graph does not have
+            HIP_CHECK(hipMemsetAsync(d_bad, 0xFF, sizeof(unsigned long long), stream));
+            KLAUNCH(validate_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, stream, q->d_roots, q->d_targets, n, g.Nx,
+                    g.N, 0ull, d_bad);
+            HIP_CHECK(hipMemcpyAsync(h_ctr + 40, d_bad, 8, hipMemcpyDeviceToHost, stream));
+        }
         HIP_CHECK(hipStreamSynchronize(stream));
+        if (validate && n) check_bad(h_ctr[40]);
         return q.release();
     }
 
@@ -2887,11 +3047,7 @@ int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint3
     API_BEGIN
     if (!e || !out || (n && (!roots || !targets))) throw Error(KETOGPU_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
-    const Snapshot &s = *e->snap;
-    for (size_t i = 0; i < n; i++)  // never launch on ids the graph does not have
-        if ((roots[i] != NONE && roots[i] >= s.Nx) || (targets[i] != NONE && targets[i] >= s.N))
-            throw Error(KETOGPU_EINVAL, "request " + std::to_string(i) + " has a node id outside the snapshot");
-    *out = e->upload(roots, targets, n);
+    *out = e->upload(roots, targets, n);  // ids are validated on the device
     API_END
 }
 
@@ -2916,12 +3072,23 @@ void ketogpu_queries_free(ketogpu_queries *q) { delete q; }
 
 int ketogpu_check_ids(ketogpu_engine *e, const uint32_t *roots, const uint32_t *targets, size_t n,
                       uint64_t *allowed_bits, uint64_t *flagged_bits) {
-    ketogpu_queries *q = nullptr;
-    int rc = ketogpu_queries_upload(e, roots, targets, n, &q);
-    if (rc) return rc;
-    std::unique_ptr<ketogpu_queries> owned(q);
-    if ((rc = ketogpu_queries_run(e, q))) return rc;
-    return ketogpu_queries_download(e, q, allowed_bits, flagged_bits);
+    API_BEGIN
+    if (!e || (n && (!roots || !targets || !allowed_bits))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->check_host(roots, targets, n, allowed_bits, flagged_bits);
+    API_END
+}
+
+int ketogpu_host_alloc(size_t bytes, void **out) {
+    API_BEGIN
+    if (!out) throw Error(KETOGPU_EINVAL, "null argument");
+    *out = nullptr;
+    HIP_CHECK(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    API_END
+}
+
+void ketogpu_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n, uint8_t *allowed, int32_t *status) {
@@ -2971,7 +3138,7 @@ int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n
             dfo.push_back(dfull.size());
         }
     }
-    std::unique_ptr<ketogpu_queries> q(e->upload(roots.data(), targets.data(), n));
+    std::unique_ptr<ketogpu_queries> q(e->upload(roots.data(), targets.data(), n, false));
     if (dio.size() > 1) {
         q->has_dyn = true;
         q->d_dyn_int_off = dupload(dio);

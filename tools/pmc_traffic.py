@@ -22,6 +22,9 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [
+    # the pipelined host-to-host first stage is its own instantiation (last template
+    # argument 1), so a launch per chunk never mixes into the full-batch launch's figures
+    ("bidi_kernel<16> (pipelined chunks)", r"bidi_kernel<16, 9, .*, 1>"),
     ("bidi_kernel<16>", r"bidi_kernel<16, 9, "),
     ("bidi spill stage w (16 requests, 2048 slots)", r"bidi_kernel<16, 11, "),
     ("bidi spill stage h (16 requests, 1024 slots)", r"bidi_kernel<16, 10, "),
@@ -53,7 +56,11 @@ def read_csv(path):
 
 
 def summarise(src, workload):
-    out = {"workload": workload, "source": src, "kernels": {}}
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from keto_amd.build import kernel_source_hash
+    # the kernel sources this profile was taken at: bench.py reports the traffic only
+    # while they are unchanged
+    out = {"workload": workload, "source": src, "source_hash": kernel_source_hash(), "kernels": {}}
     dur = defaultdict(list)
     res = {}
     for tr in glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True):
