@@ -10,9 +10,10 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KETOGPU_LIB") or os.path.join(HERE, "libketogpu.so")  # override: A/B builds
 
-OK, ENOTFOUND, EINVAL, EDEVICE, ENOMEM = 0, 1, 2, 3, 4
+OK, ENOTFOUND, EINVAL, EDEVICE, ENOMEM, ECOLLISION = 0, 1, 2, 3, 4, 5
 SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
 NODE_NONE = 0xFFFFFFFF
+NODE_NOT_OWNED = 0xFFFFFFFE
 BUILD_SORT = 1
 ORDER_NULLS_LAST = 2  # Postgres row order (include/ketogpu.h KETOGPU_ORDER_NULLS_LAST)
 ORDERS = {"sqlite": 0, "mysql-bin": 0, "cockroach": 0, "postgres": ORDER_NULLS_LAST}
@@ -22,7 +23,7 @@ NODE_UNION, NODE_LEAF = 0, 1
 class KetoError(Exception):
     """A failing libketogpu call; .code is the KETOGPU_E* code."""
 
-    NAMES = {ENOTFOUND: "not_found", EINVAL: "invalid", EDEVICE: "device", ENOMEM: "nomem"}
+    NAMES = {ENOTFOUND: "not_found", EINVAL: "invalid", EDEVICE: "device", ENOMEM: "nomem", ECOLLISION: "collision"}
 
     def __init__(self, code, msg=""):
         super().__init__(f"{self.NAMES.get(code, code)}: {msg}")
@@ -98,6 +99,23 @@ class RequestBatch(C.Structure):
         "ss_ns_data", "ss_ns_off", "ss_obj_data", "ss_obj_off", "ss_rel_data", "ss_rel_off")]
 
 
+def request_batch(cols):
+    """a RequestBatch over persistence.request_columns() arrays (keep cols alive while used)"""
+    ptr = lambda k: cols[k].ctypes.data
+    return RequestBatch(cols["n"], ptr("ns_data"), ptr("ns_off"), ptr("obj_data"), ptr("obj_off"), ptr("rel_data"),
+                        ptr("rel_off"), ptr("subject_kind"), ptr("sid_data"), ptr("sid_off"), ptr("ss_ns_data"),
+                        ptr("ss_ns_off"), ptr("ss_obj_data"), ptr("ss_obj_off"), ptr("ss_rel_data"), ptr("ss_rel_off"))
+
+
+def row_batch(cols):
+    """a RowBatch over persistence.columnar()-style arrays (keep cols alive while used)"""
+    ptr = lambda k: None if cols.get(k) is None else cols[k].ctypes.data
+    return RowBatch(len(cols["namespace_id"]), ptr("namespace_id"), ptr("object_data"), ptr("object_off"),
+                    ptr("relation_data"), ptr("relation_off"), ptr("subject_kind"), ptr("subject_id_data"),
+                    ptr("subject_id_off"), ptr("ss_namespace_id"), ptr("ss_object_data"), ptr("ss_object_off"),
+                    ptr("ss_relation_data"), ptr("ss_relation_off"))
+
+
 class GraphView(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_expandable", C.c_uint32), ("num_interior", C.c_uint32),
                 ("fint_off", C.POINTER(C.c_uint64)), ("fint_col", C.POINTER(C.c_uint32)),
@@ -115,6 +133,29 @@ class Record(C.Structure):
 class PartOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("record_capacity", C.c_uint64),
                 ("max_words_per_round", C.c_uint32), ("state_budget_bytes", C.c_uint64)]
+
+
+class ShardOpts(C.Structure):
+    _fields_ = [("page_size", C.c_int32), ("flags", C.c_uint32), ("rank", C.c_int32), ("world", C.c_int32),
+                ("salt", C.c_uint64)]
+
+
+class ShardStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "rows", "bad_rows", "owned_nodes", "owned_interior", "owned_expandable", "forward_edges",
+        "interior_forward_edges", "reverse_edges", "queries", "ambiguous_keys", "num_interior", "num_expandable",
+        "num_nodes", "host_bytes")] + [("seconds", C.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class ShardGraph(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("rank", "world", "num_interior", "num_expandable", "num_nodes",
+                                          "owned_interior", "owned_expandable", "owned_nodes")] + [
+        ("lf_off", C.POINTER(C.c_uint64)), ("lf_col", C.POINTER(C.c_uint32)),
+        ("lr_off", C.POINTER(C.c_uint64)), ("lr_col", C.POINTER(C.c_uint32)),
+        ("lb_off", C.POINTER(C.c_uint64)), ("lb_col", C.POINTER(C.c_uint32))]
 
 
 class PartStats(C.Structure):
@@ -166,7 +207,24 @@ SIGNATURES = {
     "ketogpu_multi_engine": (vp, [vp, sz]),
     "ketogpu_multi_check_ids": (C.c_int, [vp, vp, vp, sz, vp, vp]),
     "ketogpu_multi_range": (None, [sz, sz, sz, C.POINTER(sz), C.POINTER(sz)]),
-    "ketogpu_part_owner": (C.c_uint32, [u32, i32]),
+    "ketogpu_shard_builder_new": (C.c_int, [C.POINTER(Namespace), sz, C.POINTER(ShardOpts), C.POINTER(vp)]),
+    "ketogpu_shard_builder_append": (C.c_int, [vp, C.POINTER(RowBatch)]),
+    "ketogpu_shard_builder_finish": (C.c_int, [vp, C.POINTER(vp)]),
+    "ketogpu_shard_builder_free": (None, [vp]),
+    "ketogpu_shard_free": (None, [vp]),
+    "ketogpu_shard_counts": (C.c_int, [vp, vp]),
+    "ketogpu_shard_set_layout": (C.c_int, [vp, vp]),
+    "ketogpu_shard_query_count": (C.c_uint64, [vp]),
+    "ketogpu_shard_queries": (C.c_int, [vp, vp, C.c_uint64, vp]),
+    "ketogpu_shard_answer": (C.c_int, [vp, vp, C.c_uint64, vp]),
+    "ketogpu_shard_apply": (C.c_int, [vp, vp, C.c_uint64]),
+    "ketogpu_shard_claim_count": (C.c_uint64, [vp]),
+    "ketogpu_shard_claims": (C.c_int, [vp, vp, C.c_uint64, vp]),
+    "ketogpu_shard_check_claims": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "ketogpu_shard_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
+    "ketogpu_shard_stats_get": (C.c_int, [vp, C.POINTER(ShardStats)]),
+    "ketogpu_shard_view": (C.c_int, [vp, C.POINTER(ShardGraph)]),
+    "ketogpu_part_owner": (C.c_uint32, [vp, u32]),
     "ketogpu_part_new": (C.c_int, [vp, C.POINTER(PartOpts), C.POINTER(vp)]),
     "ketogpu_part_free": (None, [vp]),
     "ketogpu_part_round_words": (C.c_uint64, [vp]),

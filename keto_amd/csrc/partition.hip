@@ -1,9 +1,12 @@
 // partition.hip — hash-partitioned traversal for graphs that do not fit one GPU
 // (BASELINE.json config #5).
 //
-// Node v is owned by rank owner(v) = mix64(v) mod world.  A rank holds, for the nodes
-// it owns: the forward interior rows and the 64-request traversal state of its
-// expandable nodes, and the reverse rows of its nodes.  One round checks up to 64*W
+// A rank's partition is its shard (shard.cpp, loaded from the one ordered row stream by
+// every rank): node v is owned by rank part_owner(v) (ids interleave the ranks inside the
+// interior / expandable / other ranges, so owner and local index are arithmetic and no
+// rank holds a per-node table of the whole graph).  A rank holds, for the nodes it owns:
+// the forward interior rows and the 64-request traversal state of its expandable nodes,
+// and the reverse rows of its nodes.  One round checks up to 64*W
 // requests (W words of the multi-source bitmask BFS of SURVEY.md 8(a)):
 //   begin      owned roots r seed (word, u, bit) for u in fint(r)
 //   emit       outgoing records grouped by owner(u) into the caller's send buffer
@@ -26,14 +29,15 @@
 //              fint(r) from the roots' owners: u in B(t) <=> r reaches t in >= 2 edges.
 // Which side is cheaper depends on the graph (RBAC: documents fan out to many groups, a
 // user reaches few); keto_amd/partition.py times both and keeps the faster.
-// Snapshots with ambiguous Subject.String() keys (R4) are refused: their exact
-// re-evaluation needs the whole graph on one host.
+// Graphs with ambiguous Subject.String() keys (R4) are refused (the shard loader counts
+// them): their exact re-evaluation needs the whole graph on one host.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "device_util.hpp"
@@ -49,23 +53,20 @@ constexpr int kPItems = 4;
 constexpr int kPTile = kPB * kPItems;
 constexpr uint32_t kMaxWorld = 64;
 
-__host__ __device__ __forceinline__ uint32_t part_owner(uint32_t v, uint32_t world) {
-    uint64_t x = v;
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    x ^= x >> 31;
-    return (uint32_t)(x % world);
+// Owner of global node id v (the shard layout, shard.cpp): inside each class range —
+// interior [0, Ni), other expandable [Ni, Nx), never expanded [Nx, N) — ids interleave
+// the ranks.
+__host__ __device__ __forceinline__ uint32_t part_owner(uint32_t v, uint32_t Ni, uint32_t Nx, uint32_t world) {
+    const uint32_t base = v < Ni ? 0u : v < Nx ? Ni : Nx;
+    return (v - base) % world;
 }
 
 struct PartDev {
-    uint32_t world, Ni, Nx, N, Nil;
-    const uint32_t *lx;      // [Nx] local id of an owned expandable node (interior first) or NONE
+    uint32_t world, rank, Ni, Nx, N;  // global layout
+    uint32_t Nil, Nxl, Nl;            // this rank's class bounds: owned interior | expandable | all
     const uint64_t *lf_off;  // [Nxl + 1] forward interior rows of owned expandable nodes
     const uint32_t *lf_col;  //           (global node ids)
-    const uint32_t *lt;      // [N] local reverse row of an owned node or NONE
-    const uint64_t *lr_off;  // [Ntl + 1] reverse rows of owned nodes (global ids, sorted)
+    const uint64_t *lr_off;  // [Nl + 1] reverse rows of owned nodes (global ids, sorted)
     const uint32_t *lr_col;
     const uint64_t *lb_off;  // [Nil + 1] interior predecessors of owned interior nodes (backward rows)
     const uint32_t *lb_col;
@@ -83,6 +84,26 @@ struct PartDev {
     const uint32_t *roots, *targets;
     uint64_t n;
 };
+
+__device__ __forceinline__ uint32_t p_owner(const PartDev &P, uint32_t v) { return part_owner(v, P.Ni, P.Nx, P.world); }
+
+// local index of node v if this rank owns it (NONE otherwise, and for ids of the layout's
+// unused slots)
+__device__ __forceinline__ uint32_t p_local(const PartDev &P, uint32_t v) {
+    if (v >= P.N || p_owner(P, v) != P.rank) return KETOGPU_NODE_NONE;
+    uint32_t l, lim;
+    if (v < P.Ni) {
+        l = v / P.world;
+        lim = P.Nil;
+    } else if (v < P.Nx) {
+        l = P.Nil + (v - P.Ni) / P.world;
+        lim = P.Nxl;
+    } else {
+        l = P.Nxl + (v - P.Nx) / P.world;
+        lim = P.Nl;
+    }
+    return l < lim ? l : KETOGPU_NODE_NONE;
+}
 
 // Records are appended to obuf through one shared counter.  One atomic per wave and loop
 // iteration (a ballot-compacted append) measured seed 1.0 ms and pull_emit 1.4 ms per
@@ -128,7 +149,7 @@ __global__ __launch_bounds__(kPB) void part_seed_kernel(PartDev P) {
             const uint32_t t = P.targets[i];
             r = P.roots[i];
             if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
-                const uint32_t lt = P.lt[t];
+                const uint32_t lt = p_local(P, t);
                 if (lt != KETOGPU_NODE_NONE) {
                     b = P.lr_off[lt];
                     e = P.lr_off[lt + 1];
@@ -153,7 +174,7 @@ __global__ __launch_bounds__(kPB) void part_seed_kernel(PartDev P) {
     if (i < P.n) {
         uint32_t r = P.roots[i], t = P.targets[i];
         if (r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE && r < P.Nx) {
-            uint32_t l = P.lx[r];
+            uint32_t l = p_local(P, r);
             if (l != KETOGPU_NODE_NONE) {
                 b = P.lf_off[l];
                 e = P.lf_off[l + 1];
@@ -220,21 +241,22 @@ __global__ __launch_bounds__(kPB) void part_expand_kernel(PartDev P, uint64_t en
 }
 
 // per-destination record counts (LDS histogram, one global atomic per rank per block)
-__global__ __launch_bounds__(kPB) void part_count_kernel(const ketogpu_record *rec, uint64_t n, uint32_t world,
+__global__ __launch_bounds__(kPB) void part_count_kernel(PartDev P, const ketogpu_record *rec, uint64_t n,
                                                          unsigned long long *counts) {
     __shared__ uint32_t h[kMaxWorld];
     if (threadIdx.x < kMaxWorld) h[threadIdx.x] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kPB)
-        atomicAdd(&h[part_owner(rec[i].b, world)], 1u);
+        atomicAdd(&h[p_owner(P, rec[i].b)], 1u);
     __syncthreads();
-    if (threadIdx.x < world && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+    if (threadIdx.x < P.world && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
 // records -> out grouped by destination (cursor[g] starts at the group's offset); each
 // block reserves its share of every group once per 256-record tile
-__global__ __launch_bounds__(kPB) void part_scatter_kernel(const ketogpu_record *rec, uint64_t n, uint32_t world,
+__global__ __launch_bounds__(kPB) void part_scatter_kernel(PartDev P, const ketogpu_record *rec, uint64_t n,
                                                            unsigned long long *cursor, ketogpu_record *out) {
+    const uint32_t world = P.world;
     __shared__ uint32_t h[kMaxWorld];
     __shared__ unsigned long long base[kMaxWorld];
     for (uint64_t t0 = (uint64_t)blockIdx.x * kPB; t0 < n; t0 += (uint64_t)gridDim.x * kPB) {
@@ -246,7 +268,7 @@ __global__ __launch_bounds__(kPB) void part_scatter_kernel(const ketogpu_record 
         uint32_t o = 0, pos = 0;
         if (have) {
             r = rec[i];
-            o = part_owner(r.b, world);
+            o = p_owner(P, r.b);
             pos = atomicAdd(&h[o], 1u);
         }
         __syncthreads();
@@ -279,7 +301,7 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
             deg[it] = 0;
             if (i >= n) continue;
             const ketogpu_record r = rec[i];
-            const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
+            const uint32_t l = p_local(P, r.b);
             if (l >= P.Nil) {
                 atomicOr(P.overflow, 2u);  // not an interior node of this rank
                 continue;
@@ -371,7 +393,7 @@ __global__ __launch_bounds__(kPB) void part_pull_emit_kernel(PartDev P) {
             const uint32_t t = P.targets[i];
             r = P.roots[i];
             if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
-                const uint32_t l = P.lx[r];
+                const uint32_t l = p_local(P, r);
                 if (l != KETOGPU_NODE_NONE) {
                     b = P.lf_off[l];
                     e = P.lf_off[l + 1];
@@ -386,7 +408,7 @@ __global__ __launch_bounds__(kPB) void part_pull_emit_kernel(PartDev P) {
         const uint32_t t = P.targets[i];
         r = P.roots[i];
         if (t != KETOGPU_NODE_NONE && r != KETOGPU_NODE_NONE && r < P.Nx && t < P.N) {
-            const uint32_t lt = P.lt[t];
+            const uint32_t lt = p_local(P, t);
             if (lt != KETOGPU_NODE_NONE) {
                 b = P.lr_off[lt];
                 e = P.lr_off[lt + 1];
@@ -408,7 +430,7 @@ __global__ __launch_bounds__(kPB) void part_pull_answer_kernel(PartDev P, const 
     const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
     if (i >= n) return;
     const ketogpu_record r = rec[i];
-    const uint32_t l = r.b < P.Nx ? P.lx[r.b] : KETOGPU_NODE_NONE;
+    const uint32_t l = p_local(P, r.b);
     if (l >= P.Nil || r.a >= P.n) {
         atomicOr(P.overflow, 2u);
         return;
@@ -487,11 +509,19 @@ struct ketogpu_part {
         return p;
     }
 
-    void init(const Snapshot &s, const ketogpu_part_opts &o) {
+    void init(const ketogpu_shard *sh, const ketogpu_part_opts &o) {
+        ketogpu_shard_graph v{};
+        {
+            const int rc = ketogpu_shard_view(sh, &v);
+            if (rc) throw Error(rc, ketogpu_last_error());
+        }
         if (o.world < 1 || (uint32_t)o.world > kMaxWorld || o.rank < 0 || o.rank >= o.world)
             throw Error(KETOGPU_EINVAL, "partition: need 0 <= rank < world <= 64");
-        if (s.has_ambiguous)
-            throw Error(KETOGPU_EINVAL, "partition: snapshots with ambiguous Subject.String() keys (R4) are not supported");
+        if ((uint32_t)o.rank != v.rank || (uint32_t)o.world != v.world)
+            throw Error(KETOGPU_EINVAL, "partition: rank/world differ from the shard's");
+        ketogpu_shard_stats ss{};
+        if (ketogpu_shard_stats_get(sh, &ss) == KETOGPU_OK && ss.ambiguous_keys)
+            throw Error(KETOGPU_EINVAL, "partition: the graph has ambiguous Subject.String() keys (R4)");
         device = o.device;
         rank = (uint32_t)o.rank;
         world = (uint32_t)o.world;
@@ -500,55 +530,29 @@ struct ketogpu_part {
         if (device < 0 || device >= ndev) throw Error(KETOGPU_EDEVICE, "no such HIP device");
         PHIP(hipSetDevice(device));
         PHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        // local numbering: owned interior nodes [0, Nil), then owned sources
-        std::vector<uint32_t> lx(s.Nx, NONE);
-        std::vector<uint32_t> order;
-        for (uint32_t v = 0; v < s.Ni; v++)
-            if (part_owner(v, world) == rank) lx[v] = (uint32_t)order.size(), order.push_back(v);
-        const uint32_t Nil = (uint32_t)order.size();
-        for (uint32_t v = s.Ni; v < s.Nx; v++)
-            if (part_owner(v, world) == rank) lx[v] = (uint32_t)order.size(), order.push_back(v);
-        std::vector<uint64_t> lf_off{0};
-        std::vector<uint32_t> lf_col;
-        for (uint32_t v : order) {
-            lf_col.insert(lf_col.end(), s.fint_col.begin() + s.fint_off[v], s.fint_col.begin() + s.fint_off[v + 1]);
-            lf_off.push_back(lf_col.size());
-        }
-        // backward rows: interior predecessors of owned interior nodes = the prefix of
-        // their (sorted) reverse rows below Ni
-        std::vector<uint64_t> lb_off{0};
-        std::vector<uint32_t> lb_col;
-        for (uint32_t l = 0; l < Nil; l++) {
-            const uint32_t *b = s.rev_col.data() + s.rev_off[order[l]], *e = s.rev_col.data() + s.rev_off[order[l] + 1];
-            lb_col.insert(lb_col.end(), b, std::lower_bound(b, e, s.Ni));
-            lb_off.push_back(lb_col.size());
-        }
-        std::vector<uint32_t> lt(s.N, NONE);
-        std::vector<uint64_t> lr_off{0};
-        std::vector<uint32_t> lr_col;
-        for (uint32_t t = 0; t < s.N; t++) {
-            if (part_owner(t, world) != rank || s.rev_off[t + 1] == s.rev_off[t]) continue;
-            lt[t] = (uint32_t)(lr_off.size() - 1);
-            lr_col.insert(lr_col.end(), s.rev_col.begin() + s.rev_off[t], s.rev_col.begin() + s.rev_off[t + 1]);
-            lr_off.push_back(lr_col.size());
-        }
+        auto upv = [&](const auto *p, size_t n) {
+            using T = std::remove_const_t<std::remove_pointer_t<decltype(p)>>;
+            return upload(std::vector<T>(p, p + n));
+        };
         P.world = world;
-        P.Ni = s.Ni;
-        P.Nx = s.Nx;
-        P.N = s.N;
-        P.Nil = Nil;
-        P.lx = upload(lx);
-        P.lf_off = upload(lf_off);
-        P.lf_col = upload(lf_col);
-        P.lt = upload(lt);
-        P.lr_off = upload(lr_off);
-        P.lr_col = upload(lr_col);
-        P.lb_off = upload(lb_off);
-        P.lb_col = upload(lb_col);
-        stats.owned_interior = Nil;
-        stats.owned_expandable = order.size();
-        stats.owned_forward_edges = lf_col.size();
-        stats.owned_reverse_edges = lr_col.size();
+        P.rank = rank;
+        P.Ni = v.num_interior;
+        P.Nx = v.num_expandable;
+        P.N = v.num_nodes;
+        P.Nil = v.owned_interior;
+        P.Nxl = v.owned_expandable;
+        P.Nl = v.owned_nodes;
+        P.lf_off = upv(v.lf_off, (size_t)v.owned_expandable + 1);
+        P.lf_col = upv(v.lf_col, (size_t)v.lf_off[v.owned_expandable]);
+        P.lr_off = upv(v.lr_off, (size_t)v.owned_nodes + 1);
+        P.lr_col = upv(v.lr_col, (size_t)v.lr_off[v.owned_nodes]);
+        P.lb_off = upv(v.lb_off, (size_t)v.owned_interior + 1);
+        P.lb_col = upv(v.lb_col, (size_t)v.lb_off[v.owned_interior]);
+        stats.owned_interior = v.owned_interior;
+        stats.owned_expandable = v.owned_expandable;
+        stats.owned_forward_edges = v.lf_off[v.owned_expandable];
+        stats.owned_reverse_edges = v.lr_off[v.owned_nodes];
+        const uint32_t Nil = v.owned_interior;
 
         size_t free_b = 0, total_b = 0;
         PHIP(hipMemGetInfo(&free_b, &total_b));
@@ -635,7 +639,7 @@ struct ketogpu_part {
         } else if (n) {
             PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
-            KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_counts);
+            KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_counts);
             PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             PHIP(hipStreamSynchronize(stream));
             unsigned long long off = 0;
@@ -646,7 +650,7 @@ struct ketogpu_part {
             }
             PHIP(hipMemcpyAsync(d_cursor, h + 16 + kMaxWorld, world * sizeof(unsigned long long),
                                 hipMemcpyHostToDevice, stream));
-            KLAUNCH(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P.obuf, n, world, d_cursor, send);
+            KLAUNCH(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_cursor, send);
             PHIP(hipGetLastError());
         } else {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
@@ -757,14 +761,16 @@ struct ketogpu_part {
 
 extern "C" {
 
-uint32_t ketogpu_part_owner(uint32_t node, int32_t world) { return world > 0 ? part_owner(node, (uint32_t)world) : 0; }
+uint32_t ketogpu_part_owner(const ketogpu_part *p, uint32_t node) {
+    return p ? part_owner(node, p->P.Ni, p->P.Nx, p->P.world) : 0;
+}
 
-int ketogpu_part_new(const ketogpu_snapshot *s, const ketogpu_part_opts *opts, ketogpu_part **out) {
+int ketogpu_part_new(const ketogpu_shard *s, const ketogpu_part_opts *opts, ketogpu_part **out) {
     PAPI_BEGIN
     if (!s || !opts || !out) throw Error(KETOGPU_EINVAL, "null argument");
     *out = nullptr;
     auto p = std::make_unique<ketogpu_part>();
-    p->init(*reinterpret_cast<const Snapshot *>(s), *opts);
+    p->init(s, *opts);
     *out = p.release();
     PAPI_END
 }

@@ -36,6 +36,7 @@
 // _check_claims): the partitioned engine refuses such graphs as before.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -82,7 +83,18 @@ inline void key_id(std::string &k, std::string_view sid) {
     k.push_back('\0');
     k.append(sid.data(), sid.size());
 }
-inline uint64_t key_hash(uint64_t salt, const std::string &k) { return absorb(mix64(salt ^ 0x4b45544f53484152ull), k.data(), k.size()); }
+// KETOGPU_SHARD_HASH_BITS (tests only) narrows node hashes so collisions actually happen
+inline uint64_t hash_mask() {
+    static const uint64_t m = [] {
+        const char *e = getenv("KETOGPU_SHARD_HASH_BITS");
+        const int b = e ? atoi(e) : 64;
+        return b >= 64 || b <= 0 ? ~0ull : (1ull << b) - 1;
+    }();
+    return m;
+}
+inline uint64_t key_hash(uint64_t salt, const std::string &k) {
+    return absorb(mix64(salt ^ 0x4b45544f53484152ull), k.data(), k.size()) & hash_mask();
+}
 
 // hash -> u32 (open addressing; hash 0 is remapped so 0 can mark empty slots)
 class HashIndex {
@@ -91,7 +103,7 @@ class HashIndex {
     static uint64_t fix(uint64_t h) { return h ? h : 1; }
     uint32_t get(uint64_t h) const {
         h = fix(h);
-        for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+        for (size_t i = slot(h);; i = (i + 1) & mask_) {
             if (keys_[i] == h) return vals_[i];
             if (!keys_[i]) return NONE;
         }
@@ -100,7 +112,7 @@ class HashIndex {
     uint32_t get_or_insert(uint64_t h, uint32_t v, bool &fresh) {
         if ((n_ + 1) * 4 > keys_.size() * 3) rehash(keys_.size() * 2);
         h = fix(h);
-        for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+        for (size_t i = slot(h);; i = (i + 1) & mask_) {
             if (keys_[i] == h) {
                 fresh = false;
                 return vals_[i];
@@ -128,6 +140,9 @@ class HashIndex {
     }
 
   private:
+    // the slot from the hash's high bits: an owner keeps hashes with equal h % world, so
+    // their low bits are alike (Fibonacci hashing spreads them)
+    size_t slot(uint64_t h) const { return (size_t)((h * 0x9e3779b97f4a7c15ull) >> (64 - bits_)); }
     void rehash(size_t cap) {
         std::vector<uint64_t> ok;
         std::vector<uint32_t> ov;
@@ -136,10 +151,12 @@ class HashIndex {
         keys_.assign(cap, 0);
         vals_.assign(cap, NONE);
         mask_ = cap - 1;
+        bits_ = 0;
+        while ((size_t(1) << bits_) < cap) bits_++;
         n_ = 0;
         for (size_t i = 0; i < ok.size(); i++)
             if (ok[i]) {
-                size_t j = ok[i] & mask_;
+                size_t j = slot(ok[i]);
                 while (keys_[j]) j = (j + 1) & mask_;
                 keys_[j] = ok[i];
                 vals_[j] = ov[i];
@@ -149,6 +166,7 @@ class HashIndex {
     std::vector<uint64_t> keys_;
     std::vector<uint32_t> vals_;
     size_t n_ = 0, mask_ = 0;
+    int bits_ = 0;
 };
 
 template <class T>
@@ -156,7 +174,7 @@ size_t vbytes(const std::vector<T> &v) {
     return v.capacity() * sizeof(T);
 }
 
-constexpr uint8_t kExp = 1, kSub = 2, kSet = 4;
+constexpr uint8_t kExp = 1, kSub = 2, kSet = 4, kClosed = 8;  // kClosed: an owned group's rows ended
 
 }  // namespace
 
@@ -257,7 +275,6 @@ struct ketogpu_shard_builder {
     std::vector<uint8_t> r_flags;  // kSet for subject-set subjects, 0x80 owned
     std::vector<uint64_t> r_key_off;
     std::string r_keys;
-    HashIndex owned_groups;  // groups of this rank already closed (contiguity check)
     std::string key, skey;
     uint64_t rows = 0, bad_rows = 0;
 
@@ -293,13 +310,13 @@ struct ketogpu_shard_builder {
         const uint64_t len = first_bad < 0 ? r_h.size() : std::min<uint64_t>(r_h.size(), (uint64_t)first_bad / ps * ps);
         uint32_t gi = NONE;
         if (g_owned) {
-            bool fresh = false;
-            owned_groups.get_or_insert(g_h, 1, fresh);
-            if (!fresh)
-                throw Error(KETOGPU_EINVAL, "rows are not in ORDER BY order: a group (namespace_id, object, relation) "
-                                            "appears twice in the stream");
             key_set(key, g_ns, g_obj, g_rel);
             gi = S.reg(g_h, key, string_key_set(g_ns, g_obj, g_rel), (uint8_t)(kSet | (len ? kExp : 0)));
+            // the same group closed before (the key matched: not a hash collision)
+            if (S.node_flags[gi] & kClosed)
+                throw Error(KETOGPU_EINVAL, "rows are not in ORDER BY order: a group (namespace_id, object, relation) "
+                                            "appears twice in the stream");
+            S.node_flags[gi] |= kClosed;
             if (len) {
                 S.frow_node.push_back(gi);
                 S.frow_begin.push_back(S.fcol.size());

@@ -163,3 +163,21 @@ def rows_from_tuples(namespaces, tuples):
             s = t.subject
             out.append((nsid(t.namespace), t.object, t.relation, None, nsid(s.namespace), s.object, s.relation))
     return out
+
+
+def request_columns(requests):
+    """check requests [(namespace, object, relation, subject)] -> ketogpu_request_batch
+    columns (subject: SubjectID, SubjectSet, None for nil, or their dict forms)"""
+    subs = [rt.subject_from_dict(q[3]) if isinstance(q[3], dict) else q[3] for q in requests]
+    cols = {"n": len(requests)}
+    cols["ns_data"], cols["ns_off"] = _strcol([q[0] for q in requests])
+    cols["obj_data"], cols["obj_off"] = _strcol([q[1] for q in requests])
+    cols["rel_data"], cols["rel_off"] = _strcol([q[2] for q in requests])
+    cols["subject_kind"] = np.array([255 if s is None else 0 if isinstance(s, rt.SubjectID) else 1 for s in subs],
+                                    dtype=np.uint8)
+    cols["sid_data"], cols["sid_off"] = _strcol([s.id if isinstance(s, rt.SubjectID) else "" for s in subs])
+    ss = [s if isinstance(s, rt.SubjectSet) else rt.SubjectSet() for s in subs]
+    cols["ss_ns_data"], cols["ss_ns_off"] = _strcol([x.namespace for x in ss])
+    cols["ss_obj_data"], cols["ss_obj_off"] = _strcol([x.object for x in ss])
+    cols["ss_rel_data"], cols["ss_rel_off"] = _strcol([x.relation for x in ss])
+    return cols

@@ -1,9 +1,12 @@
-"""Partitioned mode (BASELINE config #5): the multi-rank exchange
-protocol of keto_amd.partition.PartitionedEngine against the oracle.
+"""Partitioned mode (BASELINE config #5): the partition-aware loader
+(ketogpu_shard_*) and the multi-rank exchange protocol of keto_amd.partition against the
+oracle.
 
-CPU tests run the protocol for real over gloo with world_size 2 and 3, with each rank's
-device steps played by tests/part_cpu.py; the GPU tests run the HIP steps
-(partition.hip) with world_size 1 and with two ranks sharing the box's GPU over gloo."""
+CPU tests load real shards (the C++ loader) with world_size 1, 2 and 3 over gloo and run
+the check protocol with each rank's device steps played by tests/part_cpu.py; they also
+pin the refusals (wildcard subject sets, rows out of order, shared String() keys, hash
+collisions) and that a rank holds about 1/world of the graph.  The GPU tests run the HIP
+steps (partition.hip) with world_size 1 and with two ranks sharing the box's GPU."""
 import os
 import tempfile
 
@@ -12,31 +15,45 @@ import pytest
 import torch.multiprocessing as mp
 
 from keto_amd import _lib as L
-from keto_amd import relationtuple as rt
+from keto_amd import persistence
 from keto_amd.snapshot import Snapshot
 from tests import randgraph
-from tests.part_cpu import owner
+
+NS_SMALL = None
 
 
 def _case(seed, n_rows=900, n_req=700):
-    namespaces, rows = randgraph.make_graph(seed, n_rows=n_rows, n_obj=40, n_users=60, poison=True)
+    """a random network without wildcard subject sets (the partitioned engine refuses them)
+    in the backend's row order, with poisoned pages"""
+    namespaces, rows = randgraph.make_graph(seed, n_rows=n_rows, n_obj=40, n_users=60, poison=True, wildcard=False)
+    rows = randgraph.backend_sorted(rows)
     reqs = randgraph.make_requests(seed, namespaces, rows, n=n_req, wildcard=False)
     return namespaces, rows, reqs
 
 
-def _ids(snap, reqs):
-    return snap.resolve_many([(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs])
+def _batches(rows, size=97):
+    """the ordered read in batches (groups cross batch boundaries)"""
+    return lambda: (persistence.columnar(rows[i:i + size]) for i in range(0, max(len(rows), 1), size))
 
 
 def _want(namespaces, rows, reqs):
     return randgraph.oracle_store(namespaces, rows).check_batch(reqs).astype(bool)
 
 
-def test_owner_matches_library():
-    lib = L.lib()
-    vs = np.array([0, 1, 2, 3, 1000, 123456, 0x7FFFFFFF, 0xFFFFFFFE], dtype=np.uint64)
-    for world in (1, 2, 3, 8, 64):
-        assert owner(vs, world).tolist() == [lib.ketogpu_part_owner(int(v), world) for v in vs]
+def _load(namespaces, rows, **kw):
+    from keto_amd.partition import Shard
+    return Shard.load(namespaces, _batches(rows), **kw)
+
+
+def test_single_rank_shard_matches_whole_graph_snapshot():
+    namespaces, rows, _ = _case(60)
+    sh = _load(namespaces, rows)
+    snap = Snapshot.from_rows(namespaces, rows, sort=False).stats()
+    st = sh.stats()
+    assert st["num_interior"] == snap["num_interior"] and st["num_expandable"] == snap["num_expandable"]
+    assert st["interior_forward_edges"] == snap["num_interior_edges"]
+    assert st["reverse_edges"] == snap["num_rev_edges"]
+    assert st["rows"] == len(rows) and st["bad_rows"] == snap["num_bad_rows"]
 
 
 @pytest.mark.parametrize("direction", ["forward", "backward", "auto"])
@@ -44,15 +61,71 @@ def test_protocol_single_rank_cpu(direction):
     from keto_amd.partition import PartitionedEngine
     from tests.part_cpu import CpuPartition
     namespaces, rows, reqs = _case(61)
-    snap = Snapshot.from_rows(namespaces, rows, sort=True)
-    roots, targets = _ids(snap, reqs)
-    eng = PartitionedEngine(snap, local=CpuPartition(snap.graph(), 0, 1, words=3), direction=direction)
-    np.testing.assert_array_equal(eng.check_ids(roots, targets), _want(namespaces, rows, reqs))
+    sh = _load(namespaces, rows)
+    eng = PartitionedEngine(sh, local=CpuPartition(sh.view(), words=3), direction=direction)
+    got = eng.check_requests(persistence.request_columns(reqs))
+    np.testing.assert_array_equal(got, _want(namespaces, rows, reqs))
     if direction == "auto":  # both directions ran a trial round, then one was kept
         assert set(eng._trial) == {0, 1} and eng.direction in (0, 1)
 
 
+def test_refusals_single_rank():
+    from keto_amd.partition import Shard
+    ns = [("a", 1), ("a:b", 2)]
+    ok = [(1, "o", "r", "u", None, None, None)]
+    # a wildcard subject set (R5)
+    with pytest.raises(L.KetoError, match="wildcard") as e:
+        _load(ns, ok + [(1, "p", "r", None, 1, "", "r")])
+    assert e.value.code == L.EINVAL
+    # rows out of ORDER BY order: a group appears twice
+    rows = [(1, "o", "r", "u1", None, None, None), (1, "p", "r", "u2", None, None, None),
+            (1, "o", "r", "u3", None, None, None)]
+    with pytest.raises(L.KetoError, match="ORDER BY"):
+        Shard.load(ns, lambda: iter([persistence.columnar(rows)]))
+    # R4: the subject id "a:b#c" and the subject set a:b#c share a String() key; so do the
+    # sets (a, "b:x", r) and (a:b, "x", r)
+    for extra in ([(1, "o", "r", "a:b#c", None, None, None), (1, "q", "r", None, 1, "b", "c")],
+                  [(1, "q", "r", None, 1, "b:x", "r"), (1, "q", "s", None, 2, "x", "r")]):
+        with pytest.raises(L.KetoError, match="String"):
+            _load(ns, randgraph.backend_sorted(ok + extra))
+    # ':' and '#' alone are not ambiguous
+    _load(ns, randgraph.backend_sorted(ok + [(1, "q", "r", "x:y#z", None, None, None),
+                                             (1, "q", "s", None, 1, "b:x", "r")]))
+
+
+def test_hash_collisions_are_detected_and_retried(monkeypatch):
+    """node hashes narrowed to 16 bits (test knob): collisions happen, every one is caught
+    (the typed keys differ) and the load is retried with another salt until one is free;
+    at 4 bits no salt is, and the load fails with KETOGPU_ECOLLISION"""
+    from keto_amd.partition import PartitionedEngine, Shard
+    from tests.part_cpu import CpuPartition
+    namespaces, rows, reqs = _case(65, n_rows=600)
+    monkeypatch.setenv("KETOGPU_SHARD_HASH_BITS", "16")
+    _reload_lib(monkeypatch)
+    sh = Shard.load(namespaces, _batches(rows), tries=40)
+    eng = PartitionedEngine(sh, local=CpuPartition(sh.view(), words=4), direction="forward")
+    np.testing.assert_array_equal(eng.check_requests(persistence.request_columns(reqs)),
+                                  _want(namespaces, rows, reqs))
+    monkeypatch.setenv("KETOGPU_SHARD_HASH_BITS", "4")
+    _reload_lib(monkeypatch)
+    with pytest.raises(L.KetoError) as e:
+        Shard.load(namespaces, _batches(rows), tries=3)
+    assert e.value.code == L.ECOLLISION
+
+
+def _reload_lib(monkeypatch):
+    """the hash-width knob is read once per process: load a private copy of the library"""
+    import shutil
+    d = tempfile.mkdtemp()
+    p = os.path.join(d, "libketogpu.so")
+    shutil.copy(L.LIB_PATH, p)
+    monkeypatch.setattr(L, "LIB_PATH", p)
+    monkeypatch.setattr(L, "_lib", None)
+
+
 def _worker(rank, world, port, seed, out_dir, device_steps, direction="auto"):
+    import resource
+
     import torch.distributed as dist
     from keto_amd.partition import PartitionedEngine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -60,16 +133,18 @@ def _worker(rank, world, port, seed, out_dir, device_steps, direction="auto"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         namespaces, rows, reqs = _case(seed)
-        snap = Snapshot.from_rows(namespaces, rows, sort=True)
-        roots, targets = _ids(snap, reqs)
+        sh = _load(namespaces, rows)
         if device_steps:
-            eng = PartitionedEngine(snap, device=0, record_capacity=4096, max_words_per_round=4, direction=direction)
+            eng = PartitionedEngine(sh, device=0, record_capacity=4096, max_words_per_round=4, direction=direction)
         else:
             from tests.part_cpu import CpuPartition
-            eng = PartitionedEngine(snap, local=CpuPartition(snap.graph(), rank, world, words=4), direction=direction)
-        got = eng.check_ids(roots, targets)
+            eng = PartitionedEngine(sh, local=CpuPartition(sh.view(), words=4), direction=direction)
+        got = eng.check_requests(persistence.request_columns(reqs))
+        st = sh.stats()
         np.save(os.path.join(out_dir, f"rank{rank}.npy"), got)
-        np.save(os.path.join(out_dir, f"records{rank}.npy"), np.array([eng.records, eng.levels]))
+        np.save(os.path.join(out_dir, f"records{rank}.npy"),
+                np.array([eng.records, eng.levels, st["owned_nodes"], st["forward_edges"], st["reverse_edges"],
+                          st["host_bytes"], resource.getrusage(resource.RUSAGE_SELF).ru_maxrss]))
         eng.close()
     finally:
         dist.destroy_process_group()
@@ -94,6 +169,12 @@ def test_protocol_multi_rank_gloo(world, seed, direction):
         np.testing.assert_array_equal(g, want)
     assert all(r[0] > 0 for r in rec)  # records really crossed ranks
     assert want.any() and not want.all()
+    # each rank owns a share of the nodes and rows, together the whole graph once
+    single = _load(namespaces, rows).stats()
+    assert sum(int(r[2]) for r in rec) == single["owned_nodes"]
+    assert sum(int(r[3]) for r in rec) == single["forward_edges"]
+    assert sum(int(r[4]) for r in rec) == single["reverse_edges"]
+    assert max(int(r[2]) for r in rec) < single["owned_nodes"] * 0.75
 
 
 # --------------------------------------------------------------------- GPU
@@ -105,36 +186,38 @@ def test_partition_device_single_rank(seed, direction):
     if L.lib().ketogpu_device_count() < 1:
         pytest.fail("no HIP device visible")
     namespaces, rows, reqs = _case(seed, n_rows=1500, n_req=3000)
-    snap = Snapshot.from_rows(namespaces, rows, sort=True)
-    roots, targets = _ids(snap, reqs)
+    sh = _load(namespaces, rows)
     want = _want(namespaces, rows, reqs)
-    eng = PartitionedEngine(snap, device=0, max_words_per_round=8, direction=direction)
-    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    cols = persistence.request_columns(reqs)
+    eng = PartitionedEngine(sh, device=0, max_words_per_round=8, direction=direction)
+    np.testing.assert_array_equal(eng.check_requests(cols), want)
     st = eng.local.stats()
     assert st["rounds"] >= 6 and st["levels"] > 0 and st["records_sent"] > 0
     # tiny buffers: rounds overflow and are retried with fewer words, same answers
-    small = PartitionedEngine(snap, device=0, record_capacity=2048, max_words_per_round=8, direction=direction)
-    np.testing.assert_array_equal(small.check_ids(roots, targets), want)
+    small = PartitionedEngine(sh, device=0, record_capacity=2048, max_words_per_round=8, direction=direction)
+    np.testing.assert_array_equal(small.check_requests(cols), want)
     assert small.retries > 0
 
 
 @pytest.mark.gpu
-def test_partition_device_rbac_matches_single_gpu_engine():
+def test_partition_device_rbac_matches_oracle():
     from keto_amd import check, synth
-    from keto_amd.partition import PartitionedEngine
+    from keto_amd.partition import PartitionedEngine, Shard
     w = synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=20000, seed=9)
-    snap = Snapshot.from_columns(w.namespaces, w.columns)
-    roots, targets = w.resolve(snap)
-    want = check.Engine(snap).check_ids(roots, targets)
+    sh = Shard.load(w.namespaces, lambda: iter([w.columns]))
+    roots, targets, status = sh.resolve_batch(w.request_batch())
+    assert not status.any()
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
+        w.requests(range(w.n_checks)), nthreads=8).astype(bool)
     for direction in ("forward", "backward"):
-        np.testing.assert_array_equal(PartitionedEngine(snap, device=0, direction=direction).check_ids(roots, targets),
+        np.testing.assert_array_equal(PartitionedEngine(sh, device=0, direction=direction).check_ids(roots, targets),
                                       want)
-    eng = PartitionedEngine(snap, device=0, max_words_per_round=32)  # auto: trial rounds, then one direction
-    got = eng.check_ids(roots, targets)
-    np.testing.assert_array_equal(got, want)
+    eng = PartitionedEngine(sh, device=0, max_words_per_round=32)  # auto: trial rounds, then one direction
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     assert set(eng._trial) == {0, 1}
-    orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
-    np.testing.assert_array_equal(got[:3000], orc.check_batch(w.requests(range(3000)), nthreads=8).astype(bool))
+    # the whole-graph engine agrees
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    np.testing.assert_array_equal(check.Engine(snap).check_ids(*w.resolve(snap)), want)
 
 
 @pytest.mark.gpu
