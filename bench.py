@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
                    help="replicated: graph on every GPU, request batches sharded (the metric's line); "
                         "partitioned: hash-partitioned graph, per-level all-to-all (config #5 path)")
+    p.add_argument("--scale", type=float, default=0.02,
+                   help="partitioned: config #5 size as a fraction of its 5B tuples (1.0 = full)")
     return p.parse_args()
 
 
@@ -293,23 +295,36 @@ def main():
         dist.destroy_process_group()
 
 
+def max_rss_gb():
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6  # KB -> GB
+
+
 def main_partitioned(a, rank, world, local):
-    """Config #5's path on config #2's graph: the snapshot is hash-partitioned over the
-    ranks (keto_amd/partition.py, partition.hip) and every level exchanges records with
-    all_to_all over RCCL.  Every rank holds the same global batch of 1M * world requests
-    (weak scaling); value = that batch / the slowest rank's time."""
-    from keto_amd import check, synth
-    from keto_amd.partition import PartitionedEngine
-    from keto_amd.snapshot import Snapshot
-    scale = 100 if a.small else 1
-    n_req = (1_000_000 // (10 if a.small else 1)) * world
-    sizes = dict(users=10_000_000 // scale, groups=100_000 // scale, docs=2_000_000 // scale,
-                 tuples=50_000_000 // scale, checks=n_req)
-    w = synth.rbac(**sizes, seed=synth.SEED, check_seed=synth.SEED + 1)
-    snap = Snapshot.from_columns(w.namespaces, w.columns)
-    roots, targets = w.resolve(snap)
-    eng = PartitionedEngine(snap, device=local, record_capacity=1 << 26)
-    for _ in range(a.warmup):
+    """Config #5's path (BASELINE.json configs[4]): the RBAC shape at `--scale` x 5B tuples,
+    generated as a stream (synth.config5) that every rank reads in ORDER BY order while
+    the partition-aware loader keeps only what the rank owns (keto_amd/partition.py Shard);
+    then per-level all_to_all over RCCL.  Every rank holds the same global batch of
+    1M x world requests (weak scaling); value = that batch / the slowest rank's time."""
+    from keto_amd import synth
+    from keto_amd.partition import PartitionedEngine, Shard
+    f = a.scale
+    sizes = dict(users=max(1000, int(500_000_000 * f)), groups=max(100, int(10_000_000 * f)),
+                 docs=max(100, int(200_000_000 * f)), tuples=max(10_000, int(5_000_000_000 * f)))
+    per_gpu = 1_000_000 // (10 if a.small else 1)
+    n_req = per_gpu * world
+    w = synth.config5(**sizes, checks=n_req, check_seed=synth.SEED + 1)
+    rss0 = max_rss_gb()
+    t0 = time.time()
+    sh = Shard.load(w.namespaces, lambda: w.batches(1 << 20))
+    t_load = time.time() - t0
+    rss_load = max_rss_gb()
+    sst = sh.stats()
+    log(f"shard loaded in {t_load:.1f}s: {sst['rows']} rows streamed, {sst['owned_nodes']} nodes owned, "
+        f"host arrays {sst['host_bytes'] / 1e9:.2f} GB, peak RSS {rss_load:.2f} GB")
+    roots, targets, status = sh.resolve_batch(w.request_batch())
+    eng = PartitionedEngine(sh, device=local, record_capacity=1 << 26)
+    for _ in range(max(a.warmup, 1)):  # the first call also picks the direction (auto)
         got = eng.check_ids(roots, targets)
     barrier(world)
     t0 = time.perf_counter()
@@ -317,30 +332,107 @@ def main_partitioned(a, rank, world, local):
         got = eng.check_ids(roots, targets)
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    st = eng.local.stats()
+    # measurement pass: the same step with every kernel launch bracketed by hipEvents
+    before = eng.local.stats()["kernels"]
+    eng.local.set_timing(True)
+    t0 = time.perf_counter()
+    eng.check_ids(roots, targets)
+    t_timed = time.perf_counter() - t0
+    eng.local.set_timing(False)
+    after = eng.local.stats()
+    fam = {k: {kk: after["kernels"][k][kk] - before[k][kk] for kk in ("bytes", "ms", "launches")}
+           for k in after["kernels"]}
+    rss = [max_rss_gb()]
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([rss[0], rss_load, float(sst["host_bytes"])], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        out_t = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out_t, t)
+        per_rank = [o.tolist() for o in out_t]
+    else:
+        per_rank = [[rss[0], rss_load, float(sst["host_bytes"])]]
     out = None
     if rank == 0:
-        # parity: the single-GPU engine on this rank's GPU holds the whole graph here
-        ref = check.Engine(snap, device=local).check_ids(roots, targets)
+        dominant = max(fam, key=lambda k: fam[k]["ms"])
+        d = fam[dominant]
+        achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "traffic_source": "no PMC summary for this workload", "kernel": dominant,
+                "bytes_per_launch": int(d["bytes"] / max(d["launches"], 1)),
+                "ms_per_launch": round(d["ms"] / max(d["launches"], 1), 4),
+                "measured": "one extra step with hipEvents around every launch (ketogpu_part_set_timing)",
+                "kernels": {k: {"GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
+                                "ms": round(v["ms"], 4), "bytes": v["bytes"], "launches": v["launches"]}
+                            for k, v in fam.items() if v["launches"]}}
+        cpu, parity = None, None
+        if not a.no_cpu_baseline:
+            cpu, parity = cpu_baseline_stream(w, got, a.cpu_seconds, world)
+        pos = np.asarray(w.chk_pos, dtype=bool)
+        parity = dict(parity or {}, constructed_positives=int(pos.sum()),
+                      constructed_positives_denied=int((pos & ~got.astype(bool)).sum()))
+        st = eng.local.stats()
         out = {"metric": METRIC, "value": round(n_req * a.steps / dt, 1), "unit": "checks/s", "n_gpus": world,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "u32 ids / u64 bitmasks (integer)",
-               "data": "synthetic: config #2 RBAC generator, seed 0x4B45544F; graph hash-partitioned",
-               "config": {"workload": "config2_rbac_partitioned" + ("_small" if a.small else ""), **sizes,
-                          "mode": "hash-partitioned graph, per-level all-to-all", "parallelism": f"partition x{world}"},
-               "roofline": None, "cpu_baseline": None,
-               "parity": {"sample": int(n_req), "mismatches": int((got != ref).sum()),
-                          "against": "single-GPU engine"},
-               "partition": {k: int(v) for k, v in st.items()},
+               "data": "synthetic: config #5 RBAC-shape stream generator (keto_amd/csrc/synth.cpp ks_c5), seed 0x4B45544F",
+               "config": {"workload": f"config5_partitioned_x{f:g}", **sizes, "checks": n_req,
+                          "mode": "hash-partitioned graph (partition-aware loader), per-level all-to-all",
+                          "parallelism": f"partition x{world}"},
+               "roofline": roof, "cpu_baseline": cpu, "parity": parity,
+               "load": {"seconds": round(t_load, 1), "rows": sst["rows"], "rows_per_s": round(sst["rows"] / t_load, 1),
+                        "rss_gb_before_load": round(rss0, 2),
+                        "per_rank_peak_rss_gb": [round(r[0], 2) for r in per_rank],
+                        "per_rank_rss_after_load_gb": [round(r[1], 2) for r in per_rank],
+                        "per_rank_loader_array_gb": [round(r[2] / 1e9, 3) for r in per_rank],
+                        "shard": sst},
+               "partition": {k: v for k, v in st.items() if k != "kernels"},
                "direction": {0: "forward", 1: "backward"}.get(eng.direction, "undecided"),
                "direction_trials_ns_per_check": {{0: "forward", 1: "backward"}[k]: v for k, v in eng._trial.items()},
-               "exchange": {"records": int(eng.records), "levels": int(eng.levels), "retries": int(eng.retries)}}
+               "exchange": {"records": int(eng.records), "levels": int(eng.levels), "retries": int(eng.retries)},
+               "timed_pass_s": round(t_timed, 4)}
         print(json.dumps(out), flush=True)
     barrier(world)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def cpu_baseline_stream(w, got, seconds, world):
+    """the oracle over the streamed graph (it holds every row: only at scales one host
+    holds) on the job's cores, a bounded sample of the same requests, timed at N = 1;
+    its answers are the parity sample"""
+    threads, nproc, quota = host_cores()
+    t0 = time.time()
+    from oracle import oracle as O
+    st = O.Store(w.namespaces, 100)
+    for cols in w.batches(1 << 20):
+        st.add_columnar(cols)
+    orc = st.finalize(presorted=True)
+    t_build = time.time() - t0
+    log(f"oracle store built in {t_build:.1f}s")
+    rng = np.random.default_rng(1)
+    idx = rng.permutation(len(got))
+    probe = idx[:2000]
+    t0 = time.perf_counter()
+    orc.check_batch(w.requests(probe), nthreads=threads)
+    rate = len(probe) / (time.perf_counter() - t0)
+    m = int(min(len(idx), max(len(probe), rate * seconds)))
+    sample = idx[:m]
+    t0 = time.perf_counter()
+    ans = orc.check_batch(w.requests(sample), nthreads=threads)
+    ts = time.perf_counter() - t0
+    mism = int((ans.astype(bool) != got[sample]).sum())
+    cpu = None
+    if world == 1:
+        cpu = {"value": round(m / ts, 1), "unit": "checks/s", "cores": threads, "kind": "port", "nproc": nproc,
+               "cgroup_cpu_quota": quota, "cpu_model": cpu_model(),
+               "sample": f"{m} of the {len(got)} requests (uniform sample); oracle/keto_oracle.c over the whole "
+                         f"streamed graph on {threads} threads; store build {t_build:.1f}s"}
+    return cpu, {"checked": m, "of": int(len(got)), "mismatches": mism,
+                 "against": "oracle/keto_oracle.c (exact restatement of internal/check/engine.go)"}
 
 
 def sql_baseline(seconds):

@@ -436,10 +436,24 @@ typedef struct {
     uint32_t max_words_per_round; /* 0 = auto (state budget)                           */
     uint64_t state_budget_bytes;  /* 0 = auto                                          */
 } ketogpu_part_opts;
+/* kernel families of ketogpu_part_stats.ms / bytes / launches */
+#define KETOGPU_PART_K_SEED 0
+#define KETOGPU_PART_K_EXPAND 1
+#define KETOGPU_PART_K_PACK 2        /* count + scatter by destination (world 1: a copy) */
+#define KETOGPU_PART_K_APPLY 3
+#define KETOGPU_PART_K_GATHER 4
+#define KETOGPU_PART_K_PULL_EMIT 5
+#define KETOGPU_PART_K_PULL_ANSWER 6
+#define KETOGPU_PART_K_RESET 7
 typedef struct {
     uint64_t owned_interior, owned_expandable, owned_forward_edges, owned_reverse_edges;
     uint64_t rounds, levels, frontier_entries, forward_edges;
     uint64_t records_sent, records_received, queries_answered;
+    /* per kernel family: algorithmic HBM bytes (always counted) and, while timing is on
+     * (ketogpu_part_set_timing), summed hipEvent device time and timed launches */
+    uint64_t bytes[8];
+    double ms[8];
+    uint64_t launches[8];
 } ketogpu_part_stats;
 /* opts->rank / world must match the shard's */
 int ketogpu_part_new(const ketogpu_shard *s, const ketogpu_part_opts *opts, ketogpu_part **out);
@@ -475,6 +489,9 @@ int ketogpu_part_abort(ketogpu_part *p);
 /* wait for the partition's stream (world 1: makes the last emit's send_dev readable elsewhere) */
 int ketogpu_part_sync(ketogpu_part *p);
 int ketogpu_part_stats_get(const ketogpu_part *p, ketogpu_part_stats *out);
+/* on: every kernel launch of the partition is bracketed by hipEvents on its stream (a
+ * measurement pass; each event costs a few microseconds of GPU idle) */
+int ketogpu_part_set_timing(ketogpu_part *p, int32_t on);
 
 /* ------------------------------------------------------------------ expand */
 /* BuildTree(subject, rest_depth).  *out = NULL is the nil tree (JSON null).

@@ -161,10 +161,17 @@ class ShardGraph(C.Structure):
 class PartStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "owned_interior", "owned_expandable", "owned_forward_edges", "owned_reverse_edges", "rounds", "levels",
-        "frontier_entries", "forward_edges", "records_sent", "records_received", "queries_answered")]
+        "frontier_entries", "forward_edges", "records_sent", "records_received", "queries_answered")] + [
+        ("bytes", C.c_uint64 * 8), ("ms", C.c_double * 8), ("launches", C.c_uint64 * 8)]
+
+    KERNELS = ["part_seed_kernel", "part_expand_kernel", "part_count+scatter_kernel", "part_apply_kernel",
+               "part_gather_kernel", "part_pull_emit_kernel", "part_pull_answer_kernel", "part_reset_kernel"]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        d = {n: getattr(self, n) for n, _ in self._fields_[:11]}
+        d["kernels"] = {k: {"bytes": int(self.bytes[i]), "ms": float(self.ms[i]), "launches": int(self.launches[i])}
+                        for i, k in enumerate(self.KERNELS)}
+        return d
 
 
 # every symbol declared in include/ketogpu.h, with its ctypes signature
@@ -239,6 +246,7 @@ SIGNATURES = {
     "ketogpu_part_abort": (C.c_int, [vp]),
     "ketogpu_part_sync": (C.c_int, [vp]),
     "ketogpu_part_stats_get": (C.c_int, [vp, C.POINTER(PartStats)]),
+    "ketogpu_part_set_timing": (C.c_int, [vp, C.c_int32]),
 }
 
 _lib = None

@@ -486,12 +486,57 @@ struct ketogpu_part {
     int cur = 0;
     bool dirty = false;  // state may hold bits a sparse reset does not know about
     ketogpu_part_stats stats{};
+    // measurement pass (ketogpu_part_set_timing): event pairs per launch, resolved at the
+    // next host synchronization
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    struct Pending {
+        int fam;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pend;
+
+    hipEvent_t ev() {
+        if (ev_used == ev_pool.size()) {
+            hipEvent_t e;
+            PHIP(hipEventCreate(&e));
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_used++];
+    }
+    // bracket one launch (fam: KETOGPU_PART_K_*) with events while timing; bytes always
+    template <class F>
+    void timed(int fam, uint64_t bytes, F &&launch) {
+        stats.bytes[fam] += bytes;
+        if (!timing) {
+            launch();
+            return;
+        }
+        hipEvent_t a = ev(), b = ev();
+        PHIP(hipEventRecord(a, stream));
+        launch();
+        PHIP(hipEventRecord(b, stream));
+        pend.push_back({fam, a, b});
+    }
+    // after a stream synchronization: fold the completed launches' times into the stats
+    void resolve_timing() {
+        for (const Pending &x : pend) {
+            float ms = 0;
+            PHIP(hipEventElapsedTime(&ms, x.a, x.b));
+            stats.ms[x.fam] += ms;
+            stats.launches[x.fam]++;
+        }
+        pend.clear();
+        ev_used = 0;
+    }
 
     ~ketogpu_part() {
         if (stream) {
             (void)hipSetDevice(device);
             (void)hipStreamSynchronize(stream);
         }
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
         for (void *p : owned) (void)hipFree(p);
         if (h) (void)hipHostFree(h);
         if (stream) (void)hipStreamDestroy(stream);
@@ -598,6 +643,7 @@ struct ketogpu_part {
         // ctr[0..3] and the overflow flags (ctr[4], low word) in one copy
         PHIP(hipMemcpyAsync(h, P.ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
         PHIP(hipStreamSynchronize(stream));
+        if (timing) resolve_timing();
     }
     uint32_t overflow_bits() const { return (uint32_t)h[4]; }
 
@@ -620,7 +666,7 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(P.allowed, 0, W * 8, stream));
         lb = cnt = edges = 0;
         cur = 0;
-        KLAUNCH(part_seed_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P);
+        timed(KETOGPU_PART_K_SEED, 16 * n, [&] { KLAUNCH(part_seed_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P); });
         PHIP(hipGetLastError());
         stats.rounds++;
     }
@@ -635,11 +681,14 @@ struct ketogpu_part {
         }
         if (n && world == 1) {  // one destination: the records are already grouped
             counts[0] = n;
-            PHIP(hipMemcpyAsync(send, P.obuf, n * sizeof(ketogpu_record), hipMemcpyDeviceToDevice, stream));
+            timed(KETOGPU_PART_K_PACK, 32 * n, [&] {
+                PHIP(hipMemcpyAsync(send, P.obuf, n * sizeof(ketogpu_record), hipMemcpyDeviceToDevice, stream));
+            });
         } else if (n) {
             PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
-            KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_counts);
+            timed(KETOGPU_PART_K_PACK, 16 * n,
+                  [&] { KLAUNCH(part_count_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_counts); });
             PHIP(hipMemcpyAsync(h + 16, d_counts, world * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             PHIP(hipStreamSynchronize(stream));
             unsigned long long off = 0;
@@ -650,7 +699,8 @@ struct ketogpu_part {
             }
             PHIP(hipMemcpyAsync(d_cursor, h + 16 + kMaxWorld, world * sizeof(unsigned long long),
                                 hipMemcpyHostToDevice, stream));
-            KLAUNCH(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_cursor, send);
+            timed(KETOGPU_PART_K_PACK, 32 * n,
+                  [&] { KLAUNCH(part_scatter_kernel, dim3(grid), dim3(kPB), 0, stream, P, P.obuf, n, d_cursor, send); });
             PHIP(hipGetLastError());
         } else {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
@@ -668,9 +718,10 @@ struct ketogpu_part {
         PHIP(hipMemsetAsync(&P.ctr[nxt], 0, sizeof(unsigned long long), stream));
         const uint64_t base = lb + cnt;
         if (n)
-            KLAUNCH(part_apply_kernel, dim3((unsigned)std::min<uint64_t>((n + kPTile - 1) / kPTile, 8192)), dim3(kPB), 0,
-                    stream, P, recv, n, base,
-                               &P.ctr[nxt]);
+            timed(KETOGPU_PART_K_APPLY, 32 * n, [&] {
+                KLAUNCH(part_apply_kernel, dim3((unsigned)std::min<uint64_t>((n + kPTile - 1) / kPTile, 8192)),
+                        dim3(kPB), 0, stream, P, recv, n, base, &P.ctr[nxt]);
+            });
         read_ctr();
         stats.records_received += n;
         if (overflow_bits()) {
@@ -678,8 +729,11 @@ struct ketogpu_part {
             return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_ENOMEM;
         }
         const uint64_t ncnt = h[nxt] >> kCntShift, nedges = h[nxt] & kPreMask;
+        stats.bytes[KETOGPU_PART_K_APPLY] += 16 * ncnt;  // appended (key, prefix) entries
         if (ncnt)
-            KLAUNCH(part_gather_kernel, dim3(pblocks(ncnt)), dim3(kPB), 0, stream, P, base, base + ncnt);
+            timed(KETOGPU_PART_K_GATHER, 32 * ncnt, [&] {
+                KLAUNCH(part_gather_kernel, dim3(pblocks(ncnt)), dim3(kPB), 0, stream, P, base, base + ncnt);
+            });
         lb = base;
         cnt = ncnt;
         edges = nedges;
@@ -696,7 +750,8 @@ struct ketogpu_part {
         if (cnt && edges) {
             uint64_t tiles = (edges + kPTile - 1) / kPTile;
             unsigned grid = (unsigned)std::min<uint64_t>(tiles, 256ull * 16);
-            KLAUNCH(part_expand_kernel, dim3(grid), dim3(kPB), 0, stream, P, lb, cnt, edges);
+            timed(KETOGPU_PART_K_EXPAND, 40 * cnt + 20 * edges,
+                  [&] { KLAUNCH(part_expand_kernel, dim3(grid), dim3(kPB), 0, stream, P, lb, cnt, edges); });
             PHIP(hipGetLastError());
             stats.forward_edges += edges;
         }
@@ -704,12 +759,15 @@ struct ketogpu_part {
     }
 
     void pull_emit() {
-        KLAUNCH(part_pull_emit_kernel, dim3(pblocks(P.n)), dim3(kPB), 0, stream, P);
+        timed(KETOGPU_PART_K_PULL_EMIT, 16 * P.n,
+              [&] { KLAUNCH(part_pull_emit_kernel, dim3(pblocks(P.n)), dim3(kPB), 0, stream, P); });
         PHIP(hipGetLastError());
     }
 
     int pull_answer(const ketogpu_record *recv, uint64_t n) {
-        if (n) KLAUNCH(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n);
+        if (n)
+            timed(KETOGPU_PART_K_PULL_ANSWER, 24 * n,
+                  [&] { KLAUNCH(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n); });
         read_ctr();
         stats.queries_answered += n;
         return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_OK;
@@ -725,14 +783,18 @@ struct ketogpu_part {
         } else {
             const uint64_t ents = lb + cnt, ntouch = h[2];
             if (ents)
-                KLAUNCH(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key,
-                                   ents);
+                timed(KETOGPU_PART_K_RESET, 16 * ents, [&] {
+                    KLAUNCH(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key, ents);
+                });
             if (ntouch)
-                KLAUNCH(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
-                                   ntouch);
+                timed(KETOGPU_PART_K_RESET, 16 * ntouch, [&] {
+                    KLAUNCH(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
+                            ntouch);
+                });
         }
         PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
         PHIP(hipStreamSynchronize(stream));
+        if (timing) resolve_timing();
         lb = cnt = edges = 0;
         dirty = false;
     }
@@ -881,6 +943,17 @@ int ketogpu_part_sync(ketogpu_part *p) {
     std::lock_guard<std::mutex> lk(p->mu);
     PHIP(hipSetDevice(p->device));
     PHIP(hipStreamSynchronize(p->stream));
+    PAPI_END
+}
+
+int ketogpu_part_set_timing(ketogpu_part *p, int32_t on) {
+    PAPI_BEGIN
+    if (!p) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    PHIP(hipSetDevice(p->device));
+    PHIP(hipStreamSynchronize(p->stream));
+    if (p->timing) p->resolve_timing();
+    p->timing = on != 0;
     PAPI_END
 }
 

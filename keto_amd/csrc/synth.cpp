@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <numeric>
+#include <cstdio>
 #include <random>
 #include <string>
 #include <vector>
@@ -537,6 +538,286 @@ ks_rbac *ks_social_generate(const ks_social_params *p) {
     }
     return w;
 }
+
+// ---------------------------------------------------------------------------------
+// Config #5 (BASELINE.json configs[4]): the config #2 RBAC shape at 5B tuples, for the
+// hash-partitioned mode.  Too large to materialize (the rows alone are ~150 GB), so the
+// graph is defined node by node by counter-based random draws — the k-th child of group
+// j, the k-th member of leaf group j, the k-th grant of doc d are pure functions of
+// (seed, node, k) — and STREAMED in the reference's ORDER BY order (SQLite semantics),
+// batch by batch, without holding more than one group's rows.  Every rank of the
+// partitioned loader runs the same stream.  Shape: groups in 4 levels (1/4/15/80 %);
+// a group of level l < 3 has floor(lambda + u) children drawn from level l + 1
+// (lambda = 1.5 |L_{l+1}| / |L_l|); leaf group j has floor(M w(j) + u) members, w = Zipf(s)
+// over a fixed permutation of the leaves, M = users * member_mean; doc d has
+// floor(lambda_g + u) grants, 80 % to a group, 20 % to a user, lambda_g filling the
+// tuple budget.  Checks docs:d#viewer@u: half constructed positives (a grant path walked
+// down by random access), half uniform pairs.
+typedef struct {
+    uint64_t users, groups, docs, tuples, seed;
+    double zipf_s, member_mean;
+} ks_c5_params;
+
+namespace {
+
+inline uint64_t cmix(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// decimal-string order of numbers < 10^10: n * 10^(10 - digits) with the digit count as
+// tie-break (a prefix sorts first)
+inline uint64_t lex_key(uint64_t n) {
+    int d = 1;
+    uint64_t p = 10;
+    while (n >= p && d < 10) d++, p *= 10;
+    uint64_t k = n;
+    for (int i = d; i < 10; i++) k *= 10;
+    return k * 16 + (uint64_t)d;
+}
+
+// numbers 0..n-1 in the order of their decimal strings, without a table
+struct LexIter {
+    uint64_t n = 0, cur = 0;
+    bool started = false, done = false;
+    void reset(uint64_t n_) {
+        n = n_;
+        cur = 0;
+        started = false;
+        done = n == 0;
+    }
+    bool next(uint64_t &out) {
+        if (done) return false;
+        if (!started) {
+            started = true;
+            cur = 0;
+            out = 0;
+            if (n <= 1) done = true;
+            return true;
+        }
+        if (cur == 0) {
+            cur = 1;
+        } else if (cur * 10 < n) {
+            cur *= 10;
+        } else {
+            while (cur % 10 == 9 || cur + 1 >= n) {
+                cur /= 10;
+                if (cur == 0) {
+                    done = true;
+                    return false;
+                }
+            }
+            cur += 1;
+        }
+        out = cur;
+        return true;
+    }
+};
+
+}  // namespace
+
+struct ks_c5 {
+    ks_c5_params p{};
+    uint64_t base[5] = {0, 0, 0, 0, 0}, lv[4] = {0, 0, 0, 0};
+    double lam_child[3] = {0, 0, 0}, lam_grant = 0, zipf_h = 0, members = 0;
+    uint64_t perm_a = 1, perm_b = 0;
+    // stream state
+    int phase = 0;  // 0 groups, 1 docs, 2 done
+    LexIter it;
+    std::vector<uint64_t> cur_sets, cur_users;  // lex keys of the current node's subjects
+    uint64_t cur_obj = 0, cur_pos = 0;
+    bool cur_open = false;
+    ks_rbac batch;  // the last batch's columns (and the checks)
+    uint64_t rows_out = 0;
+
+    uint64_t draw(uint64_t node_tag, uint64_t stream, uint64_t k) const {
+        return cmix(p.seed ^ cmix(node_tag * 0x9e3779b97f4a7c15ull + stream) ^ (k * 0xd1b54a32d192ed03ull));
+    }
+    double unit(uint64_t x) const { return (x >> 11) * (1.0 / 9007199254740992.0); }
+    int level(uint64_t g) const { return g < base[1] ? 0 : g < base[2] ? 1 : g < base[3] ? 2 : 3; }
+    uint64_t count(uint64_t tag, double lam) const { return (uint64_t)(lam + unit(draw(tag, 0, 0))); }
+    // group j: children (groups of the next level) and members (users, leaves only)
+    uint64_t n_children(uint64_t g) const {
+        const int l = level(g);
+        return l < 3 ? count(g * 4 + 1, lam_child[l]) : 0;
+    }
+    uint64_t child(uint64_t g, uint64_t k) const {
+        const int l = level(g);
+        return base[l + 1] + draw(g * 4 + 1, 1, k) % lv[l + 1];
+    }
+    uint64_t n_members(uint64_t g) const {
+        if (level(g) != 3) return 0;
+        const uint64_t rank = (perm_a * (g - base[3]) + perm_b) % lv[3];
+        const double w = 1.0 / std::pow((double)(rank + 1), p.zipf_s) / zipf_h;
+        return count(g * 4 + 2, members * w);
+    }
+    uint64_t member(uint64_t g, uint64_t k) const { return draw(g * 4 + 2, 2, k) % p.users; }
+    // doc d: grants, 80 % to a group
+    uint64_t n_grants(uint64_t d) const { return count(d * 4 + 3, lam_grant); }
+    bool grant_group(uint64_t d, uint64_t k) const { return unit(draw(d * 4 + 3, 3, k)) < 0.8; }
+    uint64_t grant_target(uint64_t d, uint64_t k) const {
+        return draw(d * 4 + 3, 4, k) % (grant_group(d, k) ? p.groups : p.users);
+    }
+
+    void init(const ks_c5_params &q) {
+        p = q;
+        const uint64_t G = std::max<uint64_t>(p.groups, 4), U = std::max<uint64_t>(p.users, 1);
+        p.groups = G;
+        p.users = U;
+        p.docs = std::max<uint64_t>(p.docs, 1);
+        lv[0] = std::max<uint64_t>(1, G / 100);
+        lv[1] = std::max<uint64_t>(1, G * 4 / 100);
+        lv[2] = std::max<uint64_t>(1, G * 15 / 100);
+        lv[3] = G - lv[0] - lv[1] - lv[2];
+        for (int l = 0; l < 4; l++) base[l + 1] = base[l] + lv[l];
+        for (int l = 0; l < 3; l++) lam_child[l] = 1.5 * (double)lv[l + 1] / (double)lv[l];
+        for (uint64_t k = 0; k < lv[3]; k++) zipf_h += 1.0 / std::pow((double)(k + 1), p.zipf_s);
+        members = (double)U * p.member_mean;
+        perm_a = (cmix(p.seed) | 1) % lv[3];
+        while (std::gcd(perm_a, lv[3]) != 1) perm_a++;
+        perm_b = cmix(p.seed + 1) % lv[3];
+        double used = members;
+        for (int l = 0; l < 3; l++) used += lam_child[l] * (double)lv[l];
+        lam_grant = std::max(0.0, ((double)p.tuples - used) / (double)p.docs);
+        rewind();
+    }
+    void rewind() {
+        phase = 0;
+        it.reset(p.groups);
+        cur_open = false;
+        rows_out = 0;
+    }
+    // the next node's rows, sorted as the ORDER BY sorts them (subject sets first)
+    bool open_next() {
+        uint64_t o;
+        while (phase < 2) {
+            if (it.next(o)) {
+                cur_obj = o;
+                cur_sets.clear();
+                cur_users.clear();
+                if (phase == 0) {
+                    for (uint64_t k = 0, n = n_children(o); k < n; k++) cur_sets.push_back(lex_key(child(o, k)));
+                    for (uint64_t k = 0, n = n_members(o); k < n; k++) cur_users.push_back(lex_key(member(o, k)));
+                } else {
+                    for (uint64_t k = 0, n = n_grants(o); k < n; k++)
+                        (grant_group(o, k) ? cur_sets : cur_users).push_back(lex_key(grant_target(o, k)));
+                }
+                if (cur_sets.empty() && cur_users.empty()) continue;
+                std::sort(cur_sets.begin(), cur_sets.end());
+                std::sort(cur_users.begin(), cur_users.end());
+                cur_pos = 0;
+                cur_open = true;
+                return true;
+            }
+            phase++;
+            if (phase == 1) it.reset(p.docs);
+        }
+        return false;
+    }
+    static uint64_t unkey(uint64_t k) {
+        const int d = (int)(k & 15);
+        k >>= 4;
+        for (int i = d; i < 10; i++) k /= 10;
+        return k;
+    }
+    uint64_t next_batch(uint64_t max_rows) {
+        ks_rbac &w = batch;
+        w.ns.clear();
+        w.ss_ns.clear();
+        w.kind.clear();
+        for (Col *c : {&w.obj, &w.rel, &w.sid, &w.ss_obj, &w.ss_rel}) {
+            c->data.clear();
+            c->off.assign(1, 0);
+        }
+        uint64_t n = 0;
+        while (n < max_rows) {
+            if (!cur_open && !open_next()) break;
+            const bool doc = phase == 1;
+            const uint64_t ns_sets = cur_sets.size(), total = ns_sets + cur_users.size();
+            for (; cur_pos < total && n < max_rows; cur_pos++, n++) {
+                w.ns.push_back(doc ? 2 : 1);
+                w.obj.put_num(doc ? 'd' : 'g', cur_obj);
+                if (doc)
+                    w.rel.put("viewer", 6);
+                else
+                    w.rel.put("member", 6);
+                if (cur_pos < ns_sets) {
+                    w.kind.push_back(1);
+                    w.ss_ns.push_back(1);
+                    w.sid.empty();
+                    w.ss_obj.put_num('g', unkey(cur_sets[cur_pos]));
+                    w.ss_rel.put("member", 6);
+                } else {
+                    w.kind.push_back(0);
+                    w.ss_ns.push_back(0);
+                    w.sid.put_num('u', unkey(cur_users[cur_pos - ns_sets]));
+                    w.ss_obj.empty();
+                    w.ss_rel.empty();
+                }
+            }
+            if (cur_pos == total) cur_open = false;
+        }
+        rows_out += n;
+        return n;
+    }
+    void checks(uint64_t C, uint64_t check_seed) {
+        ks_rbac &w = batch;
+        Rng rng(check_seed ? check_seed : p.seed + 1);
+        w.chk_doc.resize(C);
+        w.chk_user.resize(C);
+        w.chk_pos.resize(C);
+        w.rq_ns = w.rq_obj = w.rq_rel = w.rq_sid = Col();
+        for (uint64_t i = 0; i < C; i++) {
+            uint64_t d = rng.below(p.docs), u = rng.below(p.users);
+            bool pos = false;
+            if (rng.unit() < 0.5) {
+                for (int tries = 0; tries < 64 && !pos; tries++) {  // a grant path, walked down
+                    const uint64_t dd = rng.below(p.docs), ng = n_grants(dd);
+                    if (!ng) continue;
+                    const uint64_t k = rng.below(ng);
+                    if (!grant_group(dd, k)) {
+                        d = dd, u = grant_target(dd, k), pos = true;
+                        break;
+                    }
+                    uint64_t g = grant_target(dd, k);
+                    for (int hop = 0; hop < 8; hop++) {
+                        const uint64_t nc = n_children(g), nm = n_members(g);
+                        if (!nc && !nm) break;
+                        const uint64_t j = rng.below(nc + nm);
+                        if (j >= nc) {
+                            d = dd, u = member(g, j - nc), pos = true;
+                            break;
+                        }
+                        g = child(g, j);
+                    }
+                }
+            }
+            w.chk_doc[i] = (uint32_t)d;
+            w.chk_user[i] = (uint32_t)u;
+            w.chk_pos[i] = pos;
+            w.rq_ns.put("docs", 4);
+            w.rq_obj.put_num('d', d);
+            w.rq_rel.put("viewer", 6);
+            w.rq_sid.put_num('u', u);
+        }
+    }
+};
+
+ks_c5 *ks_c5_new(const ks_c5_params *p) {
+    auto *g = new ks_c5();
+    g->init(*p);
+    return g;
+}
+void ks_c5_rewind(ks_c5 *g) { g->rewind(); }
+// the next batch of at most max_rows rows into the generator's column buffers (valid until
+// the next call); 0 at the end of the stream
+uint64_t ks_c5_next(ks_c5 *g, uint64_t max_rows) { return g->next_batch(max_rows); }
+void ks_c5_checks(ks_c5 *g, uint64_t checks, uint64_t check_seed) { g->checks(checks, check_seed); }
+ks_rbac *ks_c5_buffers(ks_c5 *g) { return &g->batch; }
+void ks_c5_free(ks_c5 *g) { delete g; }
 
 void ks_rbac_view_get(const ks_rbac *w, ks_rbac_view *v) {
     v->n = w->ns.size();

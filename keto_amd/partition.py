@@ -347,6 +347,10 @@ class DevicePartition:
         L.check(self.L.ketogpu_part_stats_get(self.h, C.byref(st)))
         return st.as_dict()
 
+    def set_timing(self, on):
+        """bracket every kernel launch with hipEvents (a measurement pass)"""
+        L.check(self.L.ketogpu_part_set_timing(self.h, 1 if on else 0))
+
     def close(self):
         if getattr(self, "h", None):
             self.L.ketogpu_part_free(self.h)

@@ -36,6 +36,11 @@ class SocialParams(C.Structure):
         ("check_seed", C.c_uint64)]
 
 
+class C5Params(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("users", "groups", "docs", "tuples", "seed")] + [
+        ("zipf_s", C.c_double), ("member_mean", C.c_double)]
+
+
 class View(C.Structure):
     _fields_ = [("n", C.c_uint64)] + [(n, C.c_void_p) for n in (
         "namespace_id", "object_data", "object_off", "relation_data", "relation_off", "subject_kind",
@@ -59,6 +64,15 @@ def slib():
         _slib.ks_social_generate.restype = C.c_void_p
         _slib.ks_social_generate.argtypes = [C.POINTER(SocialParams)]
         _slib.ks_rbac_view_get.argtypes = [C.c_void_p, C.POINTER(View)]
+        _slib.ks_c5_new.restype = C.c_void_p
+        _slib.ks_c5_new.argtypes = [C.POINTER(C5Params)]
+        _slib.ks_c5_rewind.argtypes = [C.c_void_p]
+        _slib.ks_c5_next.restype = C.c_uint64
+        _slib.ks_c5_next.argtypes = [C.c_void_p, C.c_uint64]
+        _slib.ks_c5_checks.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        _slib.ks_c5_buffers.restype = C.c_void_p
+        _slib.ks_c5_buffers.argtypes = [C.c_void_p]
+        _slib.ks_c5_free.argtypes = [C.c_void_p]
         _slib.ks_rbac_free.argtypes = [C.c_void_p]
     return _slib
 
@@ -151,3 +165,73 @@ def social(users=100_000_000, groups=10_000_000, tuples=1_000_000_000, checks=1_
     """config #4: power-law social/group graph (Zipf popularity, acyclic nesting)"""
     return Workload(SocialParams(users, groups, tuples, checks, seed, zipf_s, member_mean, nest_per_group,
                                  check_seed), "social")
+
+
+def _columns(v, n):
+    off = lambda p: _arr(p, n + 1, np.uint64)
+    data = lambda p, o: _arr(p, int(o[-1]), np.uint8) if int(o[-1]) else np.zeros(1, np.uint8)
+    cols = {"namespace_id": _arr(v.namespace_id, n, np.int32), "subject_kind": _arr(v.subject_kind, n, np.uint8),
+            "ss_namespace_id": _arr(v.ss_namespace_id, n, np.int32)}
+    for c in ("object", "relation", "subject_id", "ss_object", "ss_relation"):
+        o = off(getattr(v, c + "_off"))
+        cols[c + "_off"] = o
+        cols[c + "_data"] = data(getattr(v, c + "_data"), o)
+    cols["commit_time"] = None
+    return cols
+
+
+class StreamWorkload:
+    """config #5: the RBAC shape at billions of tuples, defined node by node and streamed in
+    ORDER BY order (keto_amd/csrc/synth.cpp ks_c5_*): `batches()` is the one ordered read
+    every rank of the partitioned loader takes; no process holds all rows.  Requests as
+    Workload's (docs:d#viewer@u, half constructed positives)."""
+
+    namespaces = [("groups", 1), ("docs", 2)]
+    request_shape = ("docs", "d", "viewer")
+    kind = "config5"
+
+    def __init__(self, params, checks, check_seed=0):
+        self.params = params
+        self.h = slib().ks_c5_new(C.byref(params))
+        slib().ks_c5_checks(self.h, checks, check_seed)
+        v = View()
+        slib().ks_rbac_view_get(slib().ks_c5_buffers(self.h), C.byref(v))
+        self.n_checks = v.n_checks
+        self.chk_doc = _arr(v.chk_doc, v.n_checks, np.uint32).copy()
+        self.chk_user = _arr(v.chk_user, v.n_checks, np.uint32).copy()
+        self.chk_pos = _arr(v.chk_pos, v.n_checks, np.uint8).copy()
+        self._rq = v  # request columns stay valid: batches only rewrite the row columns
+
+    def batches(self, batch_rows=1 << 20):
+        """the ordered row stream, as column dicts valid until the next batch"""
+        lib = slib()
+        lib.ks_c5_rewind(self.h)
+        done = 0
+        while True:
+            n = lib.ks_c5_next(self.h, batch_rows)
+            if not n:
+                return
+            v = View()
+            lib.ks_rbac_view_get(lib.ks_c5_buffers(self.h), C.byref(v))
+            cols = _columns(v, n)
+            cols["commit_time"] = np.arange(done, done + n, dtype=np.int64)  # insertion order across batches
+            done += n
+            yield cols
+
+    def request_batch(self):
+        v, m = self._rq, self.n_checks
+        return L.RequestBatch(m, v.rq_ns_data, v.rq_ns_off, v.rq_obj_data, v.rq_obj_off, v.rq_rel_data, v.rq_rel_off,
+                              None, v.rq_sid_data, v.rq_sid_off, None, None, None, None, None, None)
+
+    requests = Workload.requests
+
+    def __del__(self):
+        if getattr(self, "h", None) and _slib is not None:
+            _slib.ks_c5_free(self.h)
+            self.h = None
+
+
+def config5(users=500_000_000, groups=10_000_000, docs=200_000_000, tuples=5_000_000_000, checks=1_000_000,
+            seed=SEED, zipf_s=1.1, member_mean=3.0, check_seed=0):
+    """config #5 (BASELINE.json configs[4]): the RBAC shape at 5B tuples, streamed"""
+    return StreamWorkload(C5Params(users, groups, docs, tuples, seed, zipf_s, member_mean), checks, check_seed)

@@ -177,6 +177,49 @@ def test_protocol_multi_rank_gloo(world, seed, direction):
     assert max(int(r[2]) for r in rec) < single["owned_nodes"] * 0.75
 
 
+def _c5_worker(rank, world, port, out_dir):
+    import resource
+
+    import torch.distributed as dist
+    from keto_amd import synth
+    from keto_amd.partition import PartitionedEngine, Shard
+    from tests.part_cpu import CpuPartition
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = synth.config5(users=30000, groups=3000, docs=6000, tuples=150000, checks=1500, seed=17)
+        sh = Shard.load(w.namespaces, lambda: w.batches(4093))
+        roots, targets, st = sh.resolve_batch(w.request_batch())
+        eng = PartitionedEngine(sh, local=CpuPartition(sh.view(), words=8), direction="backward")
+        np.save(os.path.join(out_dir, f"rank{rank}.npy"), eng.check_ids(roots, targets))
+        np.save(os.path.join(out_dir, f"stats{rank}.npy"),
+                np.array([sh.stats()["owned_nodes"], sh.stats()["host_bytes"],
+                          resource.getrusage(resource.RUSAGE_SELF).ru_maxrss]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_stream_two_ranks_match_oracle():
+    """the config #5 stream generator read by two ranks of the partition-aware loader, the
+    check protocol over gloo, every answer against the oracle over the same stream"""
+    from keto_amd import synth
+    w = synth.config5(users=30000, groups=3000, docs=6000, tuples=150000, checks=1500, seed=17)
+    from oracle import oracle as O
+    st = O.Store(w.namespaces, 100)
+    for cols in w.batches(4093):
+        st.add_columnar(cols)
+    want = st.finalize(presorted=True).check_batch(w.requests(range(w.n_checks)), nthreads=4)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_c5_worker, args=(2, 29670, d), nprocs=2, join=True, start_method="spawn")
+        got = [np.load(os.path.join(d, f"rank{r}.npy")) for r in range(2)]
+        stats = [np.load(os.path.join(d, f"stats{r}.npy")) for r in range(2)]
+    for g in got:
+        np.testing.assert_array_equal(g, want)
+    assert want[w.chk_pos.astype(bool)].all() and not want.all()
+    assert all(s[0] > 0 for s in stats)
+
+
 # --------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("direction", ["forward", "backward"])
@@ -218,6 +261,30 @@ def test_partition_device_rbac_matches_oracle():
     # the whole-graph engine agrees
     snap = Snapshot.from_columns(w.namespaces, w.columns)
     np.testing.assert_array_equal(check.Engine(snap).check_ids(*w.resolve(snap)), want)
+
+
+@pytest.mark.gpu
+def test_partition_device_config5_matches_oracle():
+    """BASELINE config #5's shape (synth.config5, streamed) at reduced size through the
+    partition-aware loader and the HIP steps, every request against the oracle"""
+    from keto_amd import synth
+    from keto_amd.partition import PartitionedEngine, Shard
+    w = synth.config5(users=100000, groups=10000, docs=40000, tuples=1_000_000, checks=20000, seed=23)
+    from oracle import oracle as O
+    st = O.Store(w.namespaces, 100)
+    for cols in w.batches(1 << 16):
+        st.add_columnar(cols)
+    want = st.finalize(presorted=True).check_batch(w.requests(range(w.n_checks)), nthreads=8).astype(bool)
+    sh = Shard.load(w.namespaces, lambda: w.batches(1 << 16))
+    roots, targets, status = sh.resolve_batch(w.request_batch())
+    for direction in ("forward", "backward", "auto"):
+        eng = PartitionedEngine(sh, device=0, direction=direction)
+        np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    eng.local.set_timing(True)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    k = eng.local.stats()["kernels"]
+    assert k["part_apply_kernel"]["launches"] > 0 and k["part_apply_kernel"]["ms"] > 0
+    assert want[w.chk_pos.astype(bool)].all()
 
 
 @pytest.mark.gpu
