@@ -60,6 +60,28 @@ class Engine:
             raise NilSubject("subject is not allowed to be nil")
         return [bool(a) for a in allowed[:n]]
 
+    def check_batch(self, tuples):
+        """check_many through the throughput path: ketogpu_resolve_batch on the host, one
+        ketogpu_check_ids over the resolved ids (H2D, traversal, D2H).  Requests that need
+        the sequential semantics — a wildcard root without a snapshot node (status
+        ENOTFOUND) or a traversal that touched a shared String() key (R4 flag) — are
+        re-answered by ketogpu_check.  Nil subjects raise NilSubject like check_many."""
+        from .persistence import request_columns
+        n = len(tuples)
+        if not n:
+            return []
+        cols = request_columns([(t.namespace, t.object, t.relation, t.subject) for t in tuples])
+        roots, targets, status = self.snapshot.resolve_batch(cols)
+        if (status == L.EINVAL).any():
+            raise NilSubject("subject is not allowed to be nil")
+        allowed, flagged = self.check_ids(roots, targets, with_flags=True)
+        redo = np.flatnonzero(flagged | (status == L.ENOTFOUND))
+        out = [bool(a) for a in allowed]
+        if len(redo):
+            for i, a in zip(redo, self.check_many([tuples[i] for i in redo])):
+                out[i] = a
+        return out
+
     # ------------------------------------------------------------ id-level API
     def check_ids(self, roots, targets, with_flags=False):
         roots = np.ascontiguousarray(roots, dtype=np.uint32)

@@ -15,8 +15,10 @@ missing namespace/object/relation are "" (no filter, R5).  Deliberate divergence
 reference's postCheck writes its 400 for a bad body and then goes on to evaluate a zero
 tuple (handler.go:130-132); here the 400 is the whole response.
 
-The batch endpoint takes many tuples in one request and answers them with ONE engine call
-(ketogpu_check: one H2D copy, the traversal, one D2H copy), per-tuple errors inline.
+The batch endpoint takes many tuples in one request and answers them through the engine's
+throughput path (check.Engine.check_batch: ketogpu_resolve_batch, then ONE
+ketogpu_check_ids — chunked H2D overlapped with the traversal, one D2H — with only
+wildcard-root and R4-flagged requests re-answered sequentially), per-tuple errors inline.
 `python -m keto_amd.handler --port P --tuples FILE --namespaces a:1,b:2` serves these
 routes with http.server (a demo harness; the production server is Keto's own).
 """
@@ -225,7 +227,8 @@ class Handler:
                 where.append(i)
             except (BadRequest, ValueError, AttributeError) as e:
                 results[i] = {"error": {"code": 400, "reason": str(e)}}
-        for i, ok in zip(where, self.check.check_many(tuples) if tuples else []):
+        batch = getattr(self.check, "check_batch", None) or self.check.check_many
+        for i, ok in zip(where, batch(tuples) if tuples else []):
             results[i] = {"allowed": bool(ok)}
         return 200, {"results": results}
 

@@ -159,6 +159,18 @@ class Snapshot:
         L.check(self.L.ketogpu_resolve(self.h, C.byref(req), C.byref(r), C.byref(t)))
         return r.value, t.value
 
+    def resolve_batch(self, cols):
+        """ketogpu_resolve_batch over request columns (persistence.request_columns) or a
+        ready L.RequestBatch -> (roots, targets, status)"""
+        rb = cols if isinstance(cols, L.RequestBatch) else L.request_batch(cols)
+        n = rb.n
+        roots = np.empty(max(n, 1), dtype=np.uint32)
+        targets = np.empty(max(n, 1), dtype=np.uint32)
+        status = np.empty(max(n, 1), dtype=np.int32)
+        L.check(self.L.ketogpu_resolve_batch(self.h, C.byref(rb), roots.ctypes.data, targets.ctypes.data,
+                                             status.ctypes.data))
+        return roots[:n], targets[:n], status[:n]
+
     def resolve_many(self, requests):
         roots = np.empty(len(requests), dtype=np.uint32)
         targets = np.empty(len(requests), dtype=np.uint32)

@@ -1,0 +1,67 @@
+"""Timeline of host-to-host check calls from a rocprofv3 trace (kernel + memory copy).
+
+    python tools/timeline.py gpurun_out/<dir>/trace [--calls 2]
+
+Reads *kernel_trace.csv and *memory_copy_trace.csv, groups activity into calls (idle gaps
+of more than 200 us separate them) and prints, for the last --calls calls that contain a
+pipelined bidi chunk launch, every kernel and copy relative to the call's first event:
+where the chunked upload, the chunk launches, the spill stages and the result copy sit,
+and the GPU-idle gaps between them.
+"""
+import csv
+import glob
+import os
+import sys
+
+
+def rows(pattern):
+    out = []
+    for p in glob.glob(pattern, recursive=True):
+        with open(p, newline="") as f:
+            out += list(csv.DictReader(f))
+    return out
+
+
+def short(name):
+    name = name.split("(")[0]
+    if "bidi_kernel" in name:
+        return name.replace("(anonymous namespace)::", "")
+    return name.replace("(anonymous namespace)::", "")[:60]
+
+
+def main():
+    src = sys.argv[1]
+    ncalls = int(sys.argv[sys.argv.index("--calls") + 1]) if "--calls" in sys.argv else 2
+    ev = []
+    for r in rows(os.path.join(src, "**", "*kernel_trace.csv")):
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K", short(r.get("Kernel_Name", "?"))))
+    for r in rows(os.path.join(src, "**", "*memory_copy_trace.csv")):
+        kind = r.get("Direction") or r.get("Operation") or r.get("Kind") or "copy"
+        size = r.get("Bytes") or r.get("Size") or ""
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", f"{kind} {size}"))
+    ev.sort()
+    calls, cur, last_end = [], [], None
+    for e in ev:
+        if last_end is not None and e[0] - last_end > 200_000:
+            calls.append(cur)
+            cur = []
+        cur.append(e)
+        last_end = max(last_end or 0, e[1])
+    if cur:
+        calls.append(cur)
+    piped = [c for c in calls if any(", 1>" in e[3] for e in c)]
+    for c in piped[-ncalls:]:
+        t0 = c[0][0]
+        end = max(e[1] for e in c)
+        print(f"--- call: {len(c)} events, {(end - t0) / 1e3:.1f} us first event to last")
+        busy_until = t0
+        for s, e, k, name in c:
+            gap = (s - busy_until) / 1e3 if k == "K" and s > busy_until else 0.0
+            print(f"{(s - t0) / 1e3:9.1f} {(e - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {k} {name}"
+                  + (f"   [idle {gap:.1f}]" if gap > 1 else ""))
+            if k == "K":
+                busy_until = max(busy_until, e)
+
+
+if __name__ == "__main__":
+    main()
