@@ -142,6 +142,14 @@ int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats
 int ketogpu_snapshot_apply(const ketogpu_snapshot *base, const ketogpu_row_batch *inserts,
                            const ketogpu_row_batch *deletes, ketogpu_snapshot **out);
 
+/* Namespace-configuration reload (internal/driver/config/provider.go:87-110: Keto drops
+ * its namespace manager whenever KeyNamespaces changes): the next version holds the base's
+ * rows under the new configuration, so page poisoning (R7) and name resolution follow it —
+ * rows of a namespace id that is no longer configured poison their pages, rows of a
+ * re-added one are visible again.  Duplicate names or ids are refused (KETOGPU_EINVAL). */
+int ketogpu_snapshot_set_namespaces(const ketogpu_snapshot *base, const ketogpu_namespace *namespaces,
+                                    size_t num_namespaces, ketogpu_snapshot **out);
+
 /* Persisted snapshots (fast restart): a versioned binary image of
  * a finished snapshot.  Loading rebuilds only the derived indexes; a file written by a
  * different format version is refused with KETOGPU_EINVAL. */

@@ -187,6 +187,7 @@ SIGNATURES = {
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),
     "ketogpu_snapshot_apply": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(vp)]),
     "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
+    "ketogpu_snapshot_set_namespaces": (C.c_int, [vp, C.POINTER(Namespace), sz, C.POINTER(vp)]),
     "ketogpu_resolve": (C.c_int, [vp, C.POINTER(CheckRequest), C.POINTER(u32), C.POINTER(u32)]),
     "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
     "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),

@@ -601,14 +601,19 @@ void ketogpu_builder_free(ketogpu_builder *b) { delete b; }
 // the order of KETOGPU_BUILD_SORT); a base whose rows are not in that order fails loudly
 // (EINVAL) when the merged stream is not grouped.  O(rows) on the host: the new version is complete
 // and immutable, and engines swap to it (keto_amd/freshness.py).
-int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batch *inserts,
-                           const ketogpu_row_batch *deletes, ketogpu_snapshot **out) {
+// The next version from the base's rows, a write batch and (namespaces != NULL) a new
+// namespace configuration: ketogpu_snapshot_apply and ketogpu_snapshot_set_namespaces.
+static int rebuild(const ketogpu_snapshot *basep, const ketogpu_row_batch *inserts, const ketogpu_row_batch *deletes,
+                   const ketogpu_namespace *namespaces, size_t num_namespaces, ketogpu_snapshot **out) {
     try {
         if (!basep || !out) throw Error(KETOGPU_EINVAL, "null argument");
         *out = nullptr;
         const Snapshot &B = *reinterpret_cast<const Snapshot *>(basep);
         std::vector<ketogpu_namespace> nss;
-        for (const Namespace &n : B.namespaces) nss.push_back(ketogpu_namespace{n.id, n.name.c_str()});
+        if (namespaces)
+            nss.assign(namespaces, namespaces + num_namespaces);
+        else
+            for (const Namespace &n : B.namespaces) nss.push_back(ketogpu_namespace{n.id, n.name.c_str()});
         ketogpu_build_opts opts{B.page_size, B.nulls_last ? KETOGPU_ORDER_NULLS_LAST : 0u};
         ketogpu_builder *raw_b = nullptr;
         int rc = ketogpu_builder_new(nss.data(), nss.size(), &opts, &raw_b);
@@ -700,6 +705,25 @@ int ketogpu_snapshot_apply(const ketogpu_snapshot *basep, const ketogpu_row_batc
         return KETOGPU_ENOMEM;
     }
     return KETOGPU_OK;
+}
+
+int ketogpu_snapshot_apply(const ketogpu_snapshot *base, const ketogpu_row_batch *inserts,
+                           const ketogpu_row_batch *deletes, ketogpu_snapshot **out) {
+    return rebuild(base, inserts, deletes, nullptr, 0, out);
+}
+
+// Namespace-configuration reload (internal/driver/config/provider.go:87-110 resets the
+// namespace manager on every change of KeyNamespaces): the same rows under the new
+// configuration, so page poisoning (R7, relationtuples.go:43-80) and name resolution
+// follow it — rows of a removed namespace id poison their pages, a re-added one heals them.
+int ketogpu_snapshot_set_namespaces(const ketogpu_snapshot *base, const ketogpu_namespace *namespaces,
+                                    size_t num_namespaces, ketogpu_snapshot **out) {
+    if (num_namespaces && !namespaces) {
+        set_last_error("null argument");
+        return KETOGPU_EINVAL;
+    }
+    static const ketogpu_namespace none{0, ""};
+    return rebuild(base, nullptr, nullptr, num_namespaces ? namespaces : &none, num_namespaces, out);
 }
 
 void ketogpu_snapshot_free(ketogpu_snapshot *s) { delete reinterpret_cast<Snapshot *>(s); }

@@ -56,6 +56,15 @@ class VersionedEngine:
             self.version += 1
             return self.version
 
+    def reload_namespaces(self, namespaces):
+        """Keto's KeyNamespaces reload (internal/driver/config/provider.go:87-110): the next
+        version holds the same rows under the new configuration (page poisoning and name
+        resolution follow it); engines swap before this returns the new version"""
+        with self._lock:
+            self._install(self._state[0].set_namespaces(namespaces))
+            self.version += 1
+            return self.version
+
     def WriteRelationTuples(self, *tuples):
         return self.transact(insert=tuples)
 

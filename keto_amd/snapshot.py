@@ -117,6 +117,17 @@ class Snapshot:
         s.L, s.namespaces, s._builder, s.h = self.L, list(self.namespaces), None, h
         return s
 
+    def set_namespaces(self, namespaces):
+        """the next version under a new namespace configuration (ketogpu_snapshot_set_namespaces;
+        Keto's KeyNamespaces reload, internal/driver/config/provider.go:87-110)"""
+        ns = [(n, int(i)) for n, i in namespaces]
+        arr = (L.Namespace * max(len(ns), 1))(*[L.Namespace(i, L.b(n)) for n, i in ns])
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_snapshot_set_namespaces(self.h, arr, len(ns), C.byref(h)))
+        s = Snapshot.__new__(Snapshot)
+        s.L, s.namespaces, s._builder, s.h = self.L, ns, None, h
+        return s
+
     # ---- persistence (ketogpu_snapshot_save / _load)
     def save(self, path):
         L.check(self.L.ketogpu_snapshot_save(self.h, str(path).encode()))

@@ -94,6 +94,52 @@ def test_apply_delete_everything_and_empty_batches():
     assert empty.stats()["num_rows"] == 0
 
 
+@pytest.mark.parametrize("seed", [121, 122])
+def test_namespace_reload_equals_a_load_under_the_new_config(seed):
+    """ketogpu_snapshot_set_namespaces: removing a namespace poisons the pages of its rows
+    (R7), renaming changes resolution, re-adding heals; each equals a fresh load of the same
+    rows under that configuration (expand trees, errors and the device graph)"""
+    namespaces, rows = randgraph.make_graph(seed, n_rows=500, n_obj=15, poison=True)
+    base = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
+    configs = [namespaces[:-1],                                      # a namespace removed
+               [(n + "x", i) for n, i in namespaces],                # renamed
+               namespaces + [("n9", 98)],                            # the poisoning id 98 configured
+               namespaces]                                           # back to the original
+    cur = base
+    for cfg in configs:
+        cur = cur.set_namespaces(cfg)
+        want = Snapshot.from_rows(cfg, rows, page_size=4, sort=True)
+        _same(cur, want)
+        e_got, e_want = expand.Engine(cur), expand.Engine(want)
+        for ns, _ in cfg:
+            for o in sorted({r[1] for r in rows})[:8]:
+                for rel in ("r0", "r1"):
+                    res = []
+                    for e in (e_got, e_want):
+                        try:
+                            res.append(e.build_tree_json(rt.SubjectSet(ns, o, rel), 3))
+                        except expand.NotFound:
+                            res.append("not_found")
+                    assert res[0] == res[1], (cfg, ns, o, rel)
+    with pytest.raises(L.KetoError):
+        base.set_namespaces([("a", 1), ("a", 2)])  # duplicate names are refused
+
+
+@pytest.mark.gpu
+def test_versioned_engine_namespace_reload():
+    from keto_amd.freshness import VersionedEngine
+    if L.lib().ketogpu_device_count() < 1:
+        pytest.fail("no HIP device visible")
+    namespaces, rows = randgraph.make_graph(131, n_rows=600, n_obj=25, n_users=30, poison=True)
+    ve = VersionedEngine(Snapshot.from_rows(namespaces, rows, sort=True))
+    for cfg in (namespaces[:-1], namespaces[1:] + [("extra", 98)], namespaces):
+        ve.reload_namespaces(cfg)
+        reqs = randgraph.make_requests(140, cfg, rows, n=400)
+        want = randgraph.oracle_store(cfg, rows).check_batch(reqs)
+        got = ve.check_many([rt.InternalRelationTuple(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs])
+        assert got == [bool(x) for x in want], cfg
+
+
 @pytest.mark.gpu
 def test_versioned_engine_reads_its_writes():
     from keto_amd.freshness import VersionedEngine
