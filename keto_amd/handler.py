@@ -227,7 +227,7 @@ class Handler:
                 where.append(i)
             except (BadRequest, ValueError, AttributeError) as e:
                 results[i] = {"error": {"code": 400, "reason": str(e)}}
-        batch = getattr(self.check, "check_batch", None) or self.check.check_many
+        batch = (getattr(self.check, "check_batch", None) or self.check.check_many) if tuples else None
         for i, ok in zip(where, batch(tuples) if tuples else []):
             results[i] = {"allowed": bool(ok)}
         return 200, {"results": results}

@@ -13,10 +13,11 @@ shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 B="bench.py --no-cpu-baseline --parity sample --steps 5 --warmup 2 $*"
-KRX="bidi_kernel|unit2_kernel|expand_kernel|pull_kernel"
+KRX="bidi_kernel|unit2_kernel|expand_kernel|pull_kernel|part_"
 echo "[profile] kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $B \
-  > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/trace" -o run \
+  -- python3 $B > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
+python3 tools/timeline.py "$OUT/trace" --calls 2 > "$OUT/timeline.txt" 2>&1 || true
 grep '^{"metric"' "$OUT/trace.log" > "$OUT/bench_line.json"
 for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
          "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD" \
