@@ -81,5 +81,32 @@ def build(force=False, jobs=4):
     return LIB
 
 
+def build_variant(name, defines, jobs=4):
+    """libketogpu built with extra -D flags on the device sources, for A/B measurements
+    (keto_amd/variants/libketogpu_<name>.so; select it with KETOGPU_LIB)"""
+    build(jobs=jobs)
+    objdir = os.path.join(HERE, "build", "v_" + name)
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS]
+    objs = []
+    for src in SOURCES:
+        if src.endswith(".cpp"):
+            objs.append(os.path.join(HERE, "build", src + ".o"))
+            continue
+        s = os.path.join(CSRC, src)
+        o = os.path.join(objdir, src + ".o")
+        objs.append(o)
+        if _stale(o, [s] + hdrs):
+            _run([HIPCC, "-c", "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-mllvm",
+                  "-amdgpu-atomic-optimizer-strategy=None", "-I", os.path.join(ROOT, "include")] + list(defines) +
+                 [s, "-o", o])
+    out = os.path.join(HERE, "variants", f"libketogpu_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    if _stale(out, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs +
+             ["-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)

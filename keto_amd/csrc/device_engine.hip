@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstring>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -1102,6 +1103,57 @@ __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert,
     return -1;
 }
 
+// Pending degree sums: cost[d][j] += (sub ? -1 : 1) * sum over the wave's lanes whose
+// `bits` hold request j, in direction d, of `val`.  Called by every lane of the wave.
+// KETO_COST_ATOMIC=1 (A/B builds): one LDS atomic per lane and bit, the lanes of a wave
+// that carry the same request serializing on its counter.  Default: the wave reduces each
+// (direction, request) sum with DPP and one lane updates it (no contention: the counters
+// are only written this way, one wave at a time for one-wave units, atomically otherwise).
+#ifndef KETO_COST_ATOMIC
+#define KETO_COST_ATOMIC 0
+#endif
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) | __builtin_amdgcn_readlane((int)x, 31) |
+                      __builtin_amdgcn_readlane((int)x, 47) | __builtin_amdgcn_readlane((int)x, 63));
+}
+
+template <int BT, class SH>
+__device__ __forceinline__ void cost_update(SH &S, uint32_t bits, int d, uint32_t val, bool sub) {
+#if KETO_COST_ATOMIC
+    for (uint32_t b = bits; b; b &= b - 1) {
+        if (sub)
+            atomicSub(&S.cost[d][__ffs(b) - 1], val);
+        else
+            atomicAdd(&S.cost[d][__ffs(b) - 1], val);
+    }
+#else
+    const int lane = threadIdx.x & 63;
+    for (int dd = 0; dd < 2; dd++) {
+        const uint32_t mine = d == dd ? bits : 0u;
+        uint32_t any = wave_or_u32(mine);  // wave-uniform
+        while (any) {
+            const int j = __ffs(any) - 1;
+            any &= any - 1;
+            const uint32_t v = (mine >> j) & 1u ? val : 0u;
+            const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(v), 63);
+            if (lane == 0) {
+                if constexpr (BT == 64) {
+                    S.cost[dd][j] = sub ? S.cost[dd][j] - sum : S.cost[dd][j] + sum;
+                } else if (sub) {
+                    atomicSub(&S.cost[dd][j], sum);
+                } else {
+                    atomicAdd(&S.cost[dd][j], sum);
+                }
+            }
+        }
+    }
+#endif
+}
+
 // Push mask m into node u in direction d.  Bits in L.lookup[d] belong to requests whose
 // other side is closed: for them u is only looked up (a meet or nothing), never inserted
 // nor made pending.  New pending bits add deg to their requests' pending sums.
@@ -1121,6 +1173,7 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
     // table load: counted without a return value, compared with HMAX after the next barrier
     if (bal && lane == __ffsll((unsigned long long)bal) - 1) atomicAdd(&S.n_used, (uint32_t)__popcll(bal));
     bool app = false;
+    uint32_t pend = 0;  // requests for which u becomes pending
     if (h >= 0) {
         const int vs = 32 * d;
         // one 64-bit atomic per push: the old word also carries the other direction's
@@ -1133,9 +1186,10 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
         if (newly && deg) {
             unsigned long long o2 = atomicOr(&S.st[h], (unsigned long long)newly << (vs + 16));
             app = !((uint32_t)(o2 >> (vs + 16)) & 0xFFFFu);
-            for (uint32_t b = newly; b; b &= b - 1) atomicAdd(&S.cost[d][__ffs(b) - 1], deg);
+            pend = newly;
         }
     }
+    cost_update<BT>(S, pend, d, deg, false);
     uint32_t idx = lds_append(app, &S.n_p[nxt]);
     if (app) {
         if (idx < (uint32_t)F) {
@@ -1459,7 +1513,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         for (uint32_t base = 0; base < cnt && !S.spill && S.n_used <= (uint32_t)SH::HMAX; base += BT) {  // read after a barrier
             const uint32_t k = cnt - base < (uint32_t)BT ? cnt - base : (uint32_t)BT;
             const uint32_t i = base + tid;
-            uint32_t take = 0, rest = 0, sd = 0, dg = 0, bg = 0;
+            uint32_t take = 0, rest = 0, sd = 0, dg = 0, bg = 0, clr = 0;
             if ((uint32_t)tid < k) {
                 sd = S.p_sd[cur][i];
                 dg = S.p_deg[cur][i];
@@ -1468,13 +1522,11 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                 const uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
                 take = pb & (d ? L.sel[1] : L.sel[0]);
                 rest = pb & act2 & ~take;
-                const uint32_t clr = pb & ~rest;
-                if (clr) {
-                    atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
-                    for (uint32_t b = clr; b; b &= b - 1) atomicSub(&S.cost[d][__ffs(b) - 1], dg);
-                }
+                clr = pb & ~rest;
+                if (clr) atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
                 S.e_mask[tid] = (uint16_t)take;
             }
+            cost_update<BT>(S, clr, (int)(sd >> 15), dg, true);
             const uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
             if (rest) {
                 if (pi < (uint32_t)F) {
@@ -1586,6 +1638,33 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(uint32_t *roots, uint3
         targets[i] = KETOGPU_NODE_NONE;
         atomicMin(first_bad, (unsigned long long)(base + i));
     }
+}
+
+// The chunk's requests read straight from pinned host memory (device-accessible, zero
+// copy over PCIe), validated as validate_kernel does and stored in HBM: no DMA copy per
+// chunk (each costs ~20 us of setup on the copy engine, two per chunk) and no separate
+// validation launch.
+__global__ __launch_bounds__(kBlock) void load_kernel(const uint32_t *hr, const uint32_t *ht, uint64_t c0, uint64_t m,
+                                                      uint32_t *dr, uint32_t *dt, uint32_t Nx, uint32_t N,
+                                                      unsigned long long *first_bad) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t r = hr[c0 + i], t = ht[c0 + i];
+        if ((r != KETOGPU_NODE_NONE && r >= Nx) || (t != KETOGPU_NODE_NONE && t >= N)) {
+            atomicMin(first_bad, (unsigned long long)(c0 + i));
+            r = t = KETOGPU_NODE_NONE;
+        }
+        dr[c0 + i] = r;
+        dt[c0 + i] = t;
+    }
+}
+
+// The run's results in one launch into pinned host memory: result words, flag words (when
+// wanted) and the first invalid request index — instead of one DMA copy each.
+__global__ __launch_bounds__(kBlock) void emit_kernel(const uint64_t *allowed, const uint64_t *flags, uint64_t words,
+                                                      const unsigned long long *first_bad, uint64_t *out) {
+    const uint64_t nf = flags ? words : 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words + nf + 1; i += (uint64_t)gridDim.x * kBlock)
+        out[i] = i < words ? allowed[i] : i < words + nf ? flags[i - words] : (uint64_t)*first_bad;
 }
 
 // sum the spread statistics slots of `regions` regions into out[3 * region + k]
@@ -1933,9 +2012,11 @@ struct Batch {
     bool has_dyn = false;
 };
 
-// host arrays of a batch that check_host copies in chunk by chunk
+// host arrays of a batch that check_host brings in chunk by chunk; mapped: pinned memory
+// the device reads directly (load_kernel), else DMA copies + validate_kernel
 struct HostSrc {
     const uint32_t *roots, *targets;
+    bool mapped;
 };
 
 struct ketogpu_queries {
@@ -2137,6 +2218,8 @@ struct ketogpu_engine {
     hipStream_t copy_stream = nullptr, stream2 = nullptr;
     unsigned long long *d_bad = nullptr;  // smallest request index with an id outside the snapshot
     uint64_t pipe_chunk = 1 << 18;        // requests per pipelined chunk (KETOGPU_PIPE_CHUNK)
+    uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
+    uint64_t res_cap = 0;
 
     hipEvent_t ev() {
         if (ev_used == ev_pool.size()) {
@@ -2158,6 +2241,7 @@ struct ketogpu_engine {
                         (void *)spill_flags})
             if (p) (void)hipFree(p);
         if (h_ctr) (void)hipHostFree(h_ctr);
+        if (h_res) (void)hipHostFree(h_res);
         delete io;
         for (hipStream_t x : {copy_stream, stream2})
             if (x) (void)hipStreamDestroy(x);
@@ -2562,19 +2646,29 @@ struct ketogpu_engine {
                     // chunk's start.  All chunks append spilled units to the one list, so the
                     // spill stages below run once for the whole batch.
                     HIP_CHECK(hipStreamWaitEvent(stream2, a, 0));  // after the clear
-                    const uint64_t U = (uint64_t)bidi_cfg.u, chunk = pipe_chunk;
-                    for (uint64_t c0 = 0, k = 0; c0 < q.n; c0 += chunk, k++) {
+                    HIP_CHECK(hipStreamWaitEvent(copy_stream, a, 0));  // d_bad reset by the clear
+                    const uint64_t U = (uint64_t)bidi_cfg.u;
+                    // a short first chunk starts the traversal early; the rest in full chunks
+                    uint64_t chunk = std::max<uint64_t>(64, pipe_chunk / 4 / 64 * 64);
+                    for (uint64_t c0 = 0, k = 0; c0 < q.n; c0 += chunk, k++, chunk = pipe_chunk) {
                         const uint64_t m = std::min<uint64_t>(chunk, q.n - c0);
-                        HIP_CHECK(hipMemcpyAsync(io->d_roots + c0, src->roots + c0, m * 4, hipMemcpyHostToDevice,
-                                                 copy_stream));
-                        HIP_CHECK(hipMemcpyAsync(io->d_targets + c0, src->targets + c0, m * 4, hipMemcpyHostToDevice,
-                                                 copy_stream));
+                        hipStream_t cs = (k & 1) ? stream2 : stream;
+                        if (src->mapped) {
+                            KLAUNCH(load_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(m), 256)), dim3(kBlock), 0,
+                                    copy_stream, src->roots, src->targets, c0, m, io->d_roots, io->d_targets, g.Nx, g.N,
+                                    d_bad);
+                        } else {
+                            HIP_CHECK(hipMemcpyAsync(io->d_roots + c0, src->roots + c0, m * 4, hipMemcpyDefault,
+                                                     copy_stream));
+                            HIP_CHECK(hipMemcpyAsync(io->d_targets + c0, src->targets + c0, m * 4, hipMemcpyDefault,
+                                                     copy_stream));
+                        }
                         hipEvent_t h = ev();
                         HIP_CHECK(hipEventRecord(h, copy_stream));
-                        hipStream_t cs = (k & 1) ? stream2 : stream;
                         HIP_CHECK(hipStreamWaitEvent(cs, h, 0));
-                        KLAUNCH(validate_kernel, dim3(blocks_for(m)), dim3(kBlock), 0, cs, io->d_roots + c0,
-                                io->d_targets + c0, m, g.Nx, g.N, c0, d_bad);
+                        if (!src->mapped)
+                            KLAUNCH(validate_kernel, dim3(blocks_for(m)), dim3(kBlock), 0, cs, io->d_roots + c0,
+                                    io->d_targets + c0, m, g.Nx, g.N, c0, d_bad);
                         launch_bidi(bidi_cfg, (unsigned)((m + U - 1) / U), lds_pad, q, nullptr, nullptr, list[0],
                                     &spill_count[0], st.stats, nullptr, c0 / U, cs, true);
                     }
@@ -2923,6 +3017,28 @@ struct ketogpu_engine {
         io = q.release();
     }
 
+    // host memory the device can read in place (pinned: ketogpu_host_alloc / hipHostMalloc /
+    // hipHostRegister) for [p, p + bytes)
+    bool device_readable(const void *p, uint64_t bytes) {
+        if (!p || !bytes) return false;
+        hipPointerAttribute_t at{};
+        const hipError_t e = hipPointerGetAttributes(&at, p);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: clear the query's error
+            return false;
+        }
+        (void)bytes;
+        return at.type == hipMemoryTypeHost && at.devicePointer == p;
+    }
+
+    void ensure_res(uint64_t n) {
+        if (n <= res_cap) return;
+        if (h_res) (void)hipHostFree(h_res);
+        h_res = nullptr;
+        res_cap = std::max<uint64_t>(n, 1 << 14);
+        HIP_CHECK(hipHostMalloc((void **)&h_res, res_cap * 8, hipHostMallocDefault));
+    }
+
     void check_bad(uint64_t first_bad) {
         if (first_bad != ~0ull)
             throw Error(KETOGPU_EINVAL, "request " + std::to_string(first_bad) + " has a node id outside the snapshot");
@@ -2952,17 +3068,18 @@ struct ketogpu_engine {
             }
             run(q);
         } else {
-            const HostSrc src{roots, targets};
-            run_once(q, &src, [&] {
-                if (words && allowed)
-                    HIP_CHECK(hipMemcpyAsync(allowed, q.d_allowed, words * 8, hipMemcpyDeviceToHost, stream));
-                if (words && flagged)
-                    HIP_CHECK(hipMemcpyAsync(flagged, q.d_flags, words * 8, hipMemcpyDeviceToHost, stream));
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 40, d_bad, 8, hipMemcpyDeviceToHost, stream));
+            const HostSrc src{roots, targets, device_readable(roots, n * 4) && device_readable(targets, n * 4)};
+            ensure_res(2 * words + 1);
+            run_once(q, &src, [&] {  // results, flags and the validation verdict in one launch
+                KLAUNCH(emit_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(2 * words + 1), 256)), dim3(kBlock), 0,
+                        stream, q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res);
             });
-            // the copies above were final unless requests went on to the global path
+            // the staged words were final unless requests went on to the global path
             if (!last.spilled_requests) {
-                check_bad(h_ctr[40]);
+                const uint64_t nf = flagged ? words : 0;
+                if (allowed) memcpy(allowed, h_res, words * 8);
+                if (flagged) memcpy(flagged, h_res + words, words * 8);
+                check_bad(h_res[words + nf]);
                 return;
             }
         }

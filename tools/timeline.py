@@ -23,10 +23,18 @@ def rows(pattern):
 
 
 def short(name):
-    name = name.split("(")[0]
-    if "bidi_kernel" in name:
-        return name.replace("(anonymous namespace)::", "")
-    return name.replace("(anonymous namespace)::", "")[:60]
+    """the kernel name without namespaces, return type and parameter list"""
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    depth, cut = 0, len(name)
+    for i, ch in enumerate(name):  # the parameter list starts at the first '(' outside <...>
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    return name[:cut][:70]
 
 
 def main():
