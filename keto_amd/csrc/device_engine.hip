@@ -1105,13 +1105,14 @@ __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert,
 
 // Pending degree sums: cost[d][j] += (sub ? -1 : 1) * sum over the wave's lanes whose
 // `bits` hold request j, in direction d, of `val`.  Called by every lane of the wave.
-// KETO_COST_ATOMIC=1 (A/B builds): one LDS atomic per lane and bit, the lanes of a wave
-// that carry the same request serializing on its counter.  Default: the wave reduces each
-// (direction, request) sum with DPP and one lane updates it (no contention: the counters
-// are only written this way, one wave at a time for one-wave units, atomically otherwise).
+// KETO_COST_ATOMIC=1 (default): one LDS atomic per lane and bit.  KETO_COST_ATOMIC=0: the
+// wave reduces each (direction, request) sum with DPP and one lane updates it — fewer LDS
+// bank conflicts, but measured 1.5x slower on config #2 (0.618 vs 0.405 ms per 1M
+// requests): the reductions cost more VALU/SALU issue than the conflicts they remove.
 #ifndef KETO_COST_ATOMIC
-#define KETO_COST_ATOMIC 0
+#define KETO_COST_ATOMIC 1  // measured: per-lane atomics 0.405 ms, the wave reductions 0.618 ms per 1M requests
 #endif
+#if !KETO_COST_ATOMIC
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -1120,6 +1121,7 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t x) {
     return (uint32_t)(__builtin_amdgcn_readlane((int)x, 15) | __builtin_amdgcn_readlane((int)x, 31) |
                       __builtin_amdgcn_readlane((int)x, 47) | __builtin_amdgcn_readlane((int)x, 63));
 }
+#endif
 
 template <int BT, class SH>
 __device__ __forceinline__ void cost_update(SH &S, uint32_t bits, int d, uint32_t val, bool sub) {
@@ -3017,18 +3019,30 @@ struct ketogpu_engine {
         io = q.release();
     }
 
-    // host memory the device can read in place (pinned: ketogpu_host_alloc / hipHostMalloc /
-    // hipHostRegister) for [p, p + bytes)
-    bool device_readable(const void *p, uint64_t bytes) {
-        if (!p || !bytes) return false;
+    // The device's view of host memory it can read in place (pinned: ketogpu_host_alloc /
+    // hipHostMalloc / hipHostRegister; or device memory of this engine's GPU), else nullptr
+    // (pageable memory goes through DMA copies).
+    const uint32_t *device_view(const uint32_t *p) {
+        if (!p) return nullptr;
         hipPointerAttribute_t at{};
         const hipError_t e = hipPointerGetAttributes(&at, p);
+        static const bool dbg = getenv("KETOGPU_DEBUG_PTR") != nullptr;
+        if (dbg)
+            fprintf(stderr, "[ptr] %p: err %d type %d device %d devptr %p hostptr %p managed %d flags %u\n", p, (int)e,
+                    (int)at.type, at.device, at.devicePointer, at.hostPointer, (int)at.isManaged, at.allocationFlags);
         if (e != hipSuccess) {
             (void)hipGetLastError();  // pageable memory: clear the query's error
-            return false;
+            return nullptr;
         }
-        (void)bytes;
-        return at.type == hipMemoryTypeHost && at.devicePointer == p;
+        if (!at.devicePointer) return nullptr;
+        if (at.type == hipMemoryTypeDevice && at.device != device) return nullptr;
+        if (at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeUnified &&
+            at.type != hipMemoryTypeManaged)
+            return nullptr;
+        // the attributes describe the allocation: offset the device view like p
+        const char *host = at.hostPointer ? (const char *)at.hostPointer : (const char *)at.devicePointer;
+        const char *dev = (const char *)at.devicePointer + ((const char *)p - host);
+        return (const uint32_t *)dev;
     }
 
     void ensure_res(uint64_t n) {
@@ -3068,7 +3082,8 @@ struct ketogpu_engine {
             }
             run(q);
         } else {
-            const HostSrc src{roots, targets, device_readable(roots, n * 4) && device_readable(targets, n * 4)};
+            const uint32_t *dr = device_view(roots), *dt = dr ? device_view(targets) : nullptr;
+            const HostSrc src{dr && dt ? dr : roots, dr && dt ? dt : targets, dr && dt};
             ensure_res(2 * words + 1);
             run_once(q, &src, [&] {  // results, flags and the validation verdict in one launch
                 KLAUNCH(emit_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(2 * words + 1), 256)), dim3(kBlock), 0,
