@@ -66,6 +66,12 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--sample", type=int, default=100_000)
+    p.add_argument("--oracle-sample", type=int, default=0,
+                   help="uniform requests diffed against oracle/keto_oracle.c (the whole graph is loaded into "
+                        "the oracle too: host memory for two copies) and, with --expand-sample, the expand "
+                        "trees of those roots diffed against the oracle's BuildTree")
+    p.add_argument("--oracle-seconds", type=float, default=300.0,
+                   help="bound on the oracle's check time: the sample is cut to what fits (reported)")
     p.add_argument("--expand-sample", type=int, default=None,
                    help="BuildTree roots timed per max-depth (default 200 for folders, config #3's expand; "
                         "0 elsewhere: power-law groups expand into trees of millions of members)")
@@ -86,6 +92,15 @@ def main():
     roots, targets = w.resolve(snap)
     pos = w.chk_pos.astype(bool)
     expand_roots = [q[:3] for q in w.requests(range(min(a.expand_sample, w.n_checks)))]
+    orc = None
+    if a.oracle_sample:
+        PHASE[0] = "building the oracle store"
+        from tests import randgraph
+        t0 = time.time()
+        orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
+        log(f"oracle store in {time.time() - t0:.1f}s")
+        oidx = np.random.default_rng(5).permutation(w.n_checks)[:a.oracle_sample]
+        oreqs = w.requests(oidx)
     del w  # the rows are no longer needed
     PHASE[0] = "uploading the device graph"
     t0 = time.time()
@@ -114,11 +129,39 @@ def main():
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
     log(f"cross-check against the {other} engine: {int((ref != got[idx]).sum())} mismatches of {len(idx)}")
+    oracle = None
+    if orc is not None:
+        PHASE[0] = "oracle sample"
+        threads = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        want, done = [], 0
+        for k in range(0, len(oreqs), 256):  # bounded: stop when the time budget is spent
+            want.append(orc.check_batch(oreqs[k:k + 256], nthreads=threads))
+            done += len(want[-1])
+            if time.perf_counter() - t0 > a.oracle_seconds:
+                break
+        want = np.concatenate(want) if want else np.zeros(0, bool)
+        mism = int((want != got[oidx[:done]]).sum())
+        oracle = {"against": "oracle/keto_oracle.c", "sample": int(done), "requested": int(len(oidx)),
+                  "mismatches": mism, "seconds": round(time.perf_counter() - t0, 1), "threads": threads,
+                  "oracle_checks_per_s": round(done / (time.perf_counter() - t0), 1)}
+        log(f"oracle: {oracle}")
     PHASE[0] = "expand"
     from keto_amd import expand
     from keto_amd.relationtuple import SubjectSet
     xe = expand.Engine(snap)
     exp = {}
+    if orc is not None and expand_roots:  # BuildTree parity: the same trees as the oracle's
+        bad = 0
+        for depth in (3, 5, 10):
+            for ns, o, r in expand_roots:
+                t = xe.BuildTree(SubjectSet(ns, o, r), depth)
+                mine = t.to_node() if t else None
+                ref = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, depth)
+                bad += mine != ref
+        exp["parity"] = {"against": "oracle/keto_oracle.c BuildTree", "trees": 3 * len(expand_roots),
+                         "max_depths": [3, 5, 10], "mismatches": bad}
+        log(f"expand parity: {exp['parity']}")
     for depth in (3, 5, 10) if expand_roots else ():  # config #3: expand at max-depth 3, 5, 10 (host DFS, R10)
         t0 = time.perf_counter()
         nodes = [xe.tree_size(SubjectSet(ns, o, r), depth) for ns, o, r in expand_roots]
@@ -133,6 +176,7 @@ def main():
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
                            "against": f"{other} engine without the hub index, same snapshot"},
+           "parity": oracle,
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},

@@ -48,9 +48,11 @@ def main():
         size = r.get("Bytes") or r.get("Size") or ""
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", f"{kind} {size}"))
     ev.sort()
+    # a run starts with its clear_kernel (results, flags and statistics zeroed); idle gaps of
+    # more than 200 us also separate calls
     calls, cur, last_end = [], [], None
     for e in ev:
-        if last_end is not None and e[0] - last_end > 200_000:
+        if cur and ((last_end is not None and e[0] - last_end > 200_000) or e[3] == "clear_kernel"):
             calls.append(cur)
             cur = []
         cur.append(e)
@@ -58,6 +60,8 @@ def main():
     if cur:
         calls.append(cur)
     piped = [c for c in calls if any(", 1>" in e[3] for e in c)]
+    if "--first" in sys.argv:  # the earliest pipelined calls (the bench's timed steps)
+        piped = piped[:ncalls + 2]
     for c in piped[-ncalls:]:
         t0 = c[0][0]
         end = max(e[1] for e in c)
