@@ -128,7 +128,8 @@ def main():
     ref_eng = check.Engine(snap)
     idx = np.random.default_rng(3).permutation(len(roots))[:a.sample]
     ref = ref_eng.check_ids(roots[idx], targets[idx])
-    log(f"cross-check against the {other} engine: {int((ref != got[idx]).sum())} mismatches of {len(idx)}")
+    xmism = int((ref != got[idx]).sum())
+    log(f"cross-check against the {other} engine: {xmism} mismatches of {len(idx)}")
     oracle = None
     if orc is not None:
         PHASE[0] = "oracle sample"
@@ -157,8 +158,8 @@ def main():
             for ns, o, r in expand_roots:
                 t = xe.BuildTree(SubjectSet(ns, o, r), depth)
                 mine = t.to_node() if t else None
-                ref = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, depth)
-                bad += mine != ref
+                want = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, depth)
+                bad += mine != want
         exp["parity"] = {"against": "oracle/keto_oracle.c BuildTree", "trees": 3 * len(expand_roots),
                          "max_depths": [3, 5, 10], "mismatches": bad}
         log(f"expand parity: {exp['parity']}")
@@ -174,7 +175,7 @@ def main():
            "main_bytes": rs["main_bytes"], "spilled_units": rs["spilled_units"],
            "spilled_requests": rs["spilled_requests"], "allowed_fraction": round(float(got.mean()), 4),
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
-           "cross_check": {"sample": int(len(idx)), "mismatches": int((ref != got[idx]).sum()),
+           "cross_check": {"sample": int(len(idx)), "mismatches": xmism,
                            "against": f"{other} engine without the hub index, same snapshot"},
            "parity": oracle,
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
