@@ -138,6 +138,16 @@ int ko_add_rows_columnar(ko_store *s, size_t n, const int32_t *namespace_id,
                          const char *ss_relation_data, const uint64_t *ss_relation_off,
                          const int64_t *commit_time) {
     if (grow((void **)&s->rows, &s->cap_rows, s->nrows + n, sizeof(ko_row))) return KO_ENOMEM;
+    /* the batch's strings in one arena growth (no doubling copies at 10^9 rows) */
+    size_t bytes = 5 * n + object_off[n] - object_off[0] + relation_off[n] - relation_off[0] +
+                   subject_id_off[n] - subject_id_off[0] + ss_object_off[n] - ss_object_off[0] +
+                   ss_relation_off[n] - ss_relation_off[0];
+    if (s->arena_len + bytes > s->arena_cap) {
+        char *q = (char *)realloc(s->arena, s->arena_len + bytes);
+        if (!q) return KO_ENOMEM;
+        s->arena = q;
+        s->arena_cap = s->arena_len + bytes;
+    }
     for (size_t i = 0; i < n; i++) {
         int kind = subject_kind[i] ? KO_SUBJECT_SET : KO_SUBJECT_ID;
         int rc = add_row_len(

@@ -41,8 +41,11 @@ def heartbeat():
         log(f"... {PHASE[0]}")
 
 
-def make(kind, tuples, checks):
+def make(kind, tuples, checks, users=None, groups=None):
     f = tuples / {"rbac": 50e6, "folders": 500e6, "social": 1e9}[kind]
+    if kind == "social" and (users or groups):  # config #4 with explicit sizes (the rows budget is `tuples`)
+        return synth.social(users=users or int(100e6 * f), groups=groups or int(10e6 * f), tuples=tuples,
+                            checks=checks, check_seed=synth.SEED + 1)
     if kind == "rbac":  # config #2 shape scaled: users, groups, docs grow with the tuple count
         return synth.rbac(users=int(10e6 * f), groups=int(100e3 * f), docs=int(2e6 * f), tuples=tuples, checks=checks,
                           check_seed=synth.SEED + 1)
@@ -51,6 +54,24 @@ def make(kind, tuples, checks):
                              checks=checks, check_seed=synth.SEED + 1)
     return synth.social(users=int(100e6 * f), groups=int(10e6 * f), tuples=tuples, checks=checks,
                         check_seed=synth.SEED + 1)
+
+
+def rss_gb():
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
+
+
+def mem_available():
+    """bytes this process may still allocate: MemAvailable, capped by the box's per-command
+    host memory limit (270 GiB) less the peak RSS so far"""
+    avail = 1 << 62
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return min(avail, int(270 * 2**30 - rss_gb() * 1e9))
 
 
 def check_plan(k):
@@ -75,12 +96,14 @@ def main():
     p.add_argument("--expand-sample", type=int, default=None,
                    help="BuildTree roots timed per max-depth (default 200 for folders, config #3's expand; "
                         "0 elsewhere: power-law groups expand into trees of millions of members)")
+    p.add_argument("--users", type=int, default=None, help="social: users (default 100M x tuples/1e9)")
+    p.add_argument("--groups", type=int, default=None, help="social: groups (default 10M x tuples/1e9)")
     a = p.parse_args()
     if a.expand_sample is None:
         a.expand_sample = 200 if a.workload == "folders" else 0
     threading.Thread(target=heartbeat, daemon=True).start()
     PHASE[0] = "generating"
-    w = make(a.workload, a.tuples, a.checks)
+    w = make(a.workload, a.tuples, a.checks, a.users, a.groups)
     t_gen = time.time() - T0
     log(f"generated {w.counts}")
     PHASE[0] = "building the snapshot"
@@ -93,6 +116,16 @@ def main():
     pos = w.chk_pos.astype(bool)
     expand_roots = [q[:3] for q in w.requests(range(min(a.expand_sample, w.n_checks)))]
     orc = None
+    oracle_skipped = None
+    if a.oracle_sample:  # the oracle holds its own copy: ~72 B per row + the strings
+        need = 72 * len(w.columns["namespace_id"]) + sum(int(w.columns[c + "_off"][-1]) + len(w.columns["namespace_id"])
+                                                        for c in ("object", "relation", "subject_id", "ss_object",
+                                                                  "ss_relation"))
+        avail = mem_available()
+        log(f"oracle store needs ~{need / 1e9:.1f} GB; available {avail / 1e9:.1f} GB; RSS {rss_gb():.1f} GB")
+        if need * 1.15 > avail:
+            oracle_skipped = f"oracle store needs ~{need / 1e9:.0f} GB, {avail / 1e9:.0f} GB available"
+            a.oracle_sample = 0
     if a.oracle_sample:
         PHASE[0] = "building the oracle store"
         from tests import randgraph
@@ -177,7 +210,8 @@ def main():
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": xmism,
                            "against": f"{other} engine without the hub index, same snapshot"},
-           "parity": oracle,
+           "parity": oracle if oracle is not None else ({"skipped": oracle_skipped} if oracle_skipped else None),
+           "peak_rss_gb": round(rss_gb(), 1),
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
