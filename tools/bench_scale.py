@@ -163,14 +163,19 @@ def main():
     ref = ref_eng.check_ids(roots[idx], targets[idx])
     xmism = int((ref != got[idx]).sum())
     log(f"cross-check against the {other} engine: {xmism} mismatches of {len(idx)}")
+    # a first result line now: a run cut short in the oracle phase still reports the timing
+    print(json.dumps({"workload": f"{a.workload}_{a.tuples}", "phase": "timed", "checks": len(roots),
+                      "checks_per_s": round(len(roots) * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 4),
+                      "plan": check_plan(rs["plan"]), "positives_denied": int((pos & ~got.astype(bool)).sum()),
+                      "cross_check": {"sample": int(len(idx)), "mismatches": xmism}}), flush=True)
     oracle = None
     if orc is not None:
         PHASE[0] = "oracle sample"
         threads = min(16, os.cpu_count() or 1)
         t0 = time.perf_counter()
         want, done = [], 0
-        for k in range(0, len(oreqs), 256):  # bounded: stop when the time budget is spent
-            want.append(orc.check_batch(oreqs[k:k + 256], nthreads=threads))
+        for k in range(0, len(oreqs), threads):  # bounded: one check per thread between budget checks
+            want.append(orc.check_batch(oreqs[k:k + threads], nthreads=threads))
             done += len(want[-1])
             if time.perf_counter() - t0 > a.oracle_seconds:
                 break
