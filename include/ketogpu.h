@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 4 /* 4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
+#define KETOGPU_ABI_VERSION 5 /* 5: writable snapshots (in-place writes, engine sync);
+                                 4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
 
 #define KETOGPU_OK 0
 #define KETOGPU_ENOTFOUND 1 /* unknown namespace (herodot.ErrNotFound)              */
@@ -64,6 +65,10 @@ extern "C" {
  * unpinned).  The order only matters where the library itself places rows: sorting
  * (KETOGPU_BUILD_SORT) and ketogpu_snapshot_apply; rows appended in order are kept. */
 #define KETOGPU_ORDER_NULLS_LAST 2u /* Postgres ORDER BY (NULLS LAST, C collation) */
+/* Writable snapshot (ketogpu_snapshot_write): the device rows are laid out with free slots
+ * (about 1/8 of each row, at least one per row part) and ids are reserved for new subjects,
+ * so a write batch patches the rows it touches in place instead of rebuilding the graph. */
+#define KETOGPU_BUILD_WRITABLE 4u
 
 typedef struct ketogpu_builder ketogpu_builder;
 typedef struct ketogpu_snapshot ketogpu_snapshot;
@@ -149,6 +154,45 @@ int ketogpu_snapshot_apply(const ketogpu_snapshot *base, const ketogpu_row_batch
  * re-added one are visible again.  Duplicate names or ids are refused (KETOGPU_EINVAL). */
 int ketogpu_snapshot_set_namespaces(const ketogpu_snapshot *base, const ketogpu_namespace *namespaces,
                                     size_t num_namespaces, ketogpu_snapshot **out);
+
+/* In-place write (R14 at O(delta)) on a KETOGPU_BUILD_WRITABLE
+ * snapshot: the same TransactRelationTuples semantics as ketogpu_snapshot_apply (inserts
+ * after equal rows, then every row matching a delete removed), applied to THIS snapshot:
+ * the touched groups' rows (host: expand, exact checks, resolution) and the touched device
+ * rows (a patch list each engine uploads at its next call, or at ketogpu_engine_sync).
+ * Cost: O(rows of the touched groups + touched device rows), independent of the graph.
+ * A batch the free slots cannot represent leaves the snapshot unchanged and reports
+ * applied = 0 with a reason; the caller then builds the next version with
+ * ketogpu_snapshot_apply (which keeps the snapshot writable).  Not representable: a row
+ * that creates a group or makes an expandable node interior (node classes are fixed
+ * between rebuilds), rows with unconfigured namespace ids or touching a poisoned group (R7),
+ * snapshots with wildcard subject sets (R5) or shared Subject.String() keys (R4), a new
+ * subject whose key is shared, a full row, no reserved ids left.  Concurrent calls on the
+ * snapshot and its engines are serialized against the write (reader/writer lock).
+ * Nodes keep their class after their last row is deleted (an expandable node without rows
+ * answers like a non-expandable one). */
+#define KETOGPU_WRITE_APPLIED 0
+#define KETOGPU_WRITE_NOT_WRITABLE 1
+#define KETOGPU_WRITE_WILDCARD 2   /* R5 wildcard subject sets in the snapshot or the batch */
+#define KETOGPU_WRITE_POISON 3     /* unconfigured namespace id, or a poisoned group (R7) */
+#define KETOGPU_WRITE_CLASS 4      /* a new group, or an expandable node becoming interior */
+#define KETOGPU_WRITE_AMBIGUOUS 5  /* shared Subject.String() keys (R4) */
+#define KETOGPU_WRITE_FULL 6       /* a touched row has no free slot left */
+#define KETOGPU_WRITE_RESERVE 7    /* no reserved node id left for a new subject */
+typedef struct {
+    int32_t applied;          /* 1: written in place; 0: unchanged, see reason */
+    int32_t reason;           /* KETOGPU_WRITE_* */
+    uint64_t rows_inserted;   /* rows added to groups */
+    uint64_t rows_deleted;    /* rows removed (all duplicates of a deleted tuple) */
+    uint64_t groups_touched;
+    uint64_t device_rows;     /* device rows patched (forward + reverse) */
+    uint64_t new_nodes;       /* subjects that got a reserved id */
+    uint64_t version;         /* the snapshot's write version after the call */
+    double seconds;           /* host time of the call */
+} ketogpu_write_result;
+int ketogpu_snapshot_write(ketogpu_snapshot *s, const ketogpu_row_batch *inserts, const ketogpu_row_batch *deletes,
+                           ketogpu_write_result *result);
+uint64_t ketogpu_snapshot_version(const ketogpu_snapshot *s);
 
 /* Persisted snapshots (fast restart): a versioned binary image of
  * a finished snapshot.  Loading rebuilds only the derived indexes; a file written by a
@@ -334,6 +378,11 @@ typedef struct {
     uint32_t plan_unit;         /* bidi: requests per first-stage unit (16 or 8)        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
+
+/* Upload the device rows patched by ketogpu_snapshot_write since the engine's last sync
+ * (every check entry point also does this first).  ms: host time of the sync (may be NULL);
+ * rows: device rows uploaded (may be NULL). */
+int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows);
 
 /* ----------------------------------------------- partition-aware loader */
 /* BASELINE config #5 (SURVEY.md 8(e) "Partitioned"): a graph that fits neither one GPU nor

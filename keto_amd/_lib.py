@@ -17,6 +17,9 @@ NODE_NOT_OWNED = 0xFFFFFFFE
 BUILD_SORT = 1
 ORDER_NULLS_LAST = 2  # Postgres row order (include/ketogpu.h KETOGPU_ORDER_NULLS_LAST)
 ORDERS = {"sqlite": 0, "mysql-bin": 0, "cockroach": 0, "postgres": ORDER_NULLS_LAST}
+BUILD_WRITABLE = 4  # rows with free slots: ketogpu_snapshot_write patches in place
+WRITE_REASONS = {0: "applied", 1: "not_writable", 2: "wildcard", 3: "poison", 4: "class", 5: "ambiguous",
+                 6: "full", 7: "reserve"}
 NODE_UNION, NODE_LEAF = 0, 1
 
 
@@ -61,6 +64,18 @@ class SnapshotStats(C.Structure):
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class WriteResult(C.Structure):
+    _fields_ = [("applied", C.c_int32), ("reason", C.c_int32)] + [(n, C.c_uint64) for n in (
+        "rows_inserted", "rows_deleted", "groups_touched", "device_rows", "new_nodes", "version")] + [
+        ("seconds", C.c_double)]
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_}
+        d["applied"] = bool(d["applied"])
+        d["reason"] = WRITE_REASONS.get(d["reason"], d["reason"])
+        return d
 
 
 class Subject(C.Structure):
@@ -188,6 +203,9 @@ SIGNATURES = {
     "ketogpu_snapshot_apply": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(vp)]),
     "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
     "ketogpu_snapshot_set_namespaces": (C.c_int, [vp, C.POINTER(Namespace), sz, C.POINTER(vp)]),
+    "ketogpu_snapshot_write": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(WriteResult)]),
+    "ketogpu_snapshot_version": (C.c_uint64, [vp]),
+    "ketogpu_engine_sync": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "ketogpu_resolve": (C.c_int, [vp, C.POINTER(CheckRequest), C.POINTER(u32), C.POINTER(u32)]),
     "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
     "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),

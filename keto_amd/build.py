@@ -14,7 +14,7 @@ SYNTH_LIB = os.path.join(HERE, "libketosynth.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
 
-SOURCES = ["snapshot.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip"]
+SOURCES = ["snapshot.cpp", "snapshot_write.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip"]
 HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
 
 
@@ -60,8 +60,8 @@ def build(force=False, jobs=4):
                    "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
                    "-I", os.path.join(ROOT, "include"), s, "-o", o]
             if src.endswith(".cpp"):
-                cmd = [HIPCC, "-c", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(ROOT, "include"), s,
-                       "-o", o]
+                cmd = [HIPCC, "-c", "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+                       "-I", os.path.join(ROOT, "include"), s, "-o", o]
             print("+", " ".join(cmd), flush=True)
             procs.append(subprocess.Popen(cmd))
             if len(procs) >= jobs:

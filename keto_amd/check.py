@@ -102,6 +102,13 @@ class Engine:
     def upload(self, roots, targets):
         return DeviceQueries(self, roots, targets)
 
+    def sync(self):
+        """upload the device rows an in-place write patched (ketogpu_engine_sync; every
+        check call does it first) -> (host ms, rows uploaded)"""
+        ms, rows = C.c_double(), C.c_uint64()
+        L.check(self.L.ketogpu_engine_sync(self.h, C.byref(ms), C.byref(rows)))
+        return ms.value, rows.value
+
     def last_stats(self):
         st = L.RunStats()
         L.check(self.L.ketogpu_engine_last_stats(self.h, C.byref(st)))

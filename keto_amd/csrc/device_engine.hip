@@ -675,6 +675,24 @@ __global__ __launch_bounds__(kBlock) void unit_kernel(DevGraph g, const uint32_t
 struct FRec {
     uint32_t node, deg, begin, pad;
 };
+
+// Writable snapshots: rewrite patched rows in place (engine::sync).  seg holds
+// (destination, source, length, 0 = forward row / 1 = reverse row) per row; one workgroup
+// per row (grid-stride), the records only where the engine keeps them.
+__global__ __launch_bounds__(256) void patch_rows_kernel(const uint64_t *seg, uint64_t nseg, const uint32_t *cols,
+                                                         const FRec *recs, uint32_t *fint_col, FRec *frec,
+                                                         uint32_t *rev_col, FRec *brec) {
+    for (uint64_t i = blockIdx.x; i < nseg; i += gridDim.x) {
+        const uint64_t dst = seg[4 * i], src = seg[4 * i + 1], len = seg[4 * i + 2];
+        const bool rev = seg[4 * i + 3] != 0;
+        uint32_t *col = rev ? rev_col : fint_col;
+        FRec *rec = rev ? brec : frec;
+        for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) {
+            col[dst + k] = cols[src + k];
+            if (rec) rec[dst + k] = recs[src + k];
+        }
+    }
+}
 constexpr int kFront = 512;  // frontier entries per level (spill beyond)
 constexpr int kRevCache = 16;
 constexpr int kHubList = 128;  // hubs a unit may reach (spill beyond)
@@ -2232,6 +2250,65 @@ struct ketogpu_engine {
         return ev_pool[ev_used++];
     }
 
+    // Writable snapshots (snapshot_write.cpp): replay the device rows patched since the last
+    // sync — each row's entries and its edge records, recomputed from the host rows (records
+    // point at rows whose position and capacity never change between rebuilds).  One
+    // upload of the packed rows and one scatter launch; called under the snapshot's shared
+    // lock before every traversal.
+    uint64_t synced_version = 0;
+    size_t patch_pos = 0;
+    uint64_t sync() {
+        const Snapshot &s = *snap;
+        if (!s.writable || synced_version == s.version) return 0;
+        HIP_CHECK(hipSetDevice(device));
+        std::vector<uint32_t> fr, rr;
+        for (size_t i = patch_pos; i < s.patches.size(); i++) (s.patches[i].rev ? rr : fr).push_back(s.patches[i].node);
+        for (auto *v : {&fr, &rr}) {
+            std::sort(v->begin(), v->end());
+            v->erase(std::unique(v->begin(), v->end()), v->end());
+        }
+        std::vector<uint64_t> seg;  // (destination, source, length, which) per row
+        std::vector<uint32_t> cols;
+        std::vector<FRec> recs;
+        auto ideg = [&](uint32_t v) {
+            const uint32_t *b = s.rev_col.data() + s.rev_off[v], *e = s.rev_col.data() + s.rev_off[v + 1];
+            return (uint32_t)(std::lower_bound(b, e, s.Ni) - b);
+        };
+        for (uint32_t v : fr) {
+            const uint64_t b = s.fint_off[v], e = s.fint_off[v + 1];
+            seg.insert(seg.end(), {b, (uint64_t)cols.size(), e - b, 0});
+            for (uint64_t k = b; k < e; k++) {
+                const uint32_t u = s.fint_col[k];
+                cols.push_back(u);
+                recs.push_back(FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u], 0});
+            }
+        }
+        for (uint32_t v : rr) {
+            const uint64_t b = s.rev_off[v], e = s.rev_off[v + 1];
+            seg.insert(seg.end(), {b, (uint64_t)cols.size(), e - b, 1});
+            for (uint64_t k = b; k < e; k++) {
+                const uint32_t u = s.rev_col[k];
+                cols.push_back(u);
+                recs.push_back(u < s.Ni ? FRec{u, ideg(u), (uint32_t)s.rev_off[u], 0} : FRec{u, 0, 0, 0});
+            }
+        }
+        const uint64_t nseg = seg.size() / 4;
+        if (nseg && !cols.empty()) {
+            uint64_t *d_seg = dupload(seg);
+            uint32_t *d_cols = dupload(cols);
+            FRec *d_recs = dupload(recs);
+            KLAUNCH(patch_rows_kernel, dim3((unsigned)std::min<uint64_t>(nseg, 65535)), dim3(256), 0, stream, d_seg,
+                    nseg, d_cols, d_recs, const_cast<uint32_t *>(g.fint_col), const_cast<FRec *>(frec),
+                    const_cast<uint32_t *>(g.rev_col), const_cast<FRec *>(brec));
+            HIP_CHECK(hipStreamSynchronize(stream));
+            for (void *p : {(void *)d_seg, (void *)d_cols, (void *)d_recs}) (void)hipFree(p);
+        }
+        g.N = s.N;
+        patch_pos = s.patches.size();
+        synced_version = s.version;
+        return nseg;
+    }
+
     ~ketogpu_engine() {
         if (stream) {
             (void)hipSetDevice(device);
@@ -2417,7 +2494,8 @@ struct ketogpu_engine {
     static constexpr uint64_t kHubDeg = 8;
     std::vector<uint32_t> hub_nodes, hub_of_h;
     void choose_hubs(const Snapshot &s) {
-        if (s.has_ambiguous || !s.Ni) return;
+        // writable snapshots: an in-place write would change hub closures (no hub index)
+        if (s.has_ambiguous || !s.Ni || s.writable) return;
         auto deg = [&](uint32_t v) { return s.fint_off[v + 1] - s.fint_off[v]; };
         uint64_t maxdeg = 0, heavy = 0;
         for (uint32_t v = 0; v < s.Ni; v++) {
@@ -3167,7 +3245,11 @@ int ketogpu_engine_new(const ketogpu_snapshot *s, const ketogpu_engine_opts *opt
     if (!s || !out) throw Error(KETOGPU_EINVAL, "null argument");
     *out = nullptr;
     auto e = std::make_unique<ketogpu_engine>();
-    e->init(*reinterpret_cast<const Snapshot *>(s), opts);
+    const Snapshot &snap = *reinterpret_cast<const Snapshot *>(s);
+    std::shared_lock<std::shared_mutex> rd(snap.mu);
+    e->init(snap, opts);
+    e->synced_version = snap.version;  // built from the current rows
+    e->patch_pos = snap.patches.size();
     *out = e.release();
     API_END
 }
@@ -3178,7 +3260,9 @@ int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint3
                            ketogpu_queries **out) {
     API_BEGIN
     if (!e || !out || (n && (!roots || !targets))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
     std::lock_guard<std::mutex> lk(e->mu);
+    e->sync();
     *out = e->upload(roots, targets, n);  // ids are validated on the device
     API_END
 }
@@ -3186,7 +3270,9 @@ int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint3
 int ketogpu_queries_run(ketogpu_engine *e, ketogpu_queries *q) {
     API_BEGIN
     if (!e || !q) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
     std::lock_guard<std::mutex> lk(e->mu);
+    e->sync();
     e->run(*q);
     API_END
 }
@@ -3206,7 +3292,9 @@ int ketogpu_check_ids(ketogpu_engine *e, const uint32_t *roots, const uint32_t *
                       uint64_t *allowed_bits, uint64_t *flagged_bits) {
     API_BEGIN
     if (!e || (n && (!roots || !targets || !allowed_bits))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
     std::lock_guard<std::mutex> lk(e->mu);
+    e->sync();
     e->check_host(roots, targets, n, allowed_bits, flagged_bits);
     API_END
 }
@@ -3226,7 +3314,9 @@ void ketogpu_host_free(void *p) {
 int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n, uint8_t *allowed, int32_t *status) {
     API_BEGIN
     if (!e || (n && (!reqs || !allowed))) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
     std::lock_guard<std::mutex> lk(e->mu);
+    e->sync();
     const Snapshot &s = *e->snap;
     std::vector<uint32_t> roots(n, NONE), targets(n, NONE);
     // dynamic roots: wildcard queries with no snapshot node, materialized per batch
@@ -3303,6 +3393,19 @@ int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n
             allowed[i] = exact_check(s, rp, rl, reqs[i].subject, targets[i]) ? 1 : 0;
         }
     }
+    API_END
+}
+
+int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows) {
+    API_BEGIN
+    if (!e) throw Error(KETOGPU_EINVAL, "null argument");
+    const auto t0 = std::chrono::steady_clock::now();
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_CHECK(hipSetDevice(e->device));
+    const uint64_t n = e->sync();
+    if (rows) *rows = n;
+    if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     API_END
 }
 

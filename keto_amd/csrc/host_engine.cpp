@@ -283,6 +283,7 @@ int ketogpu_resolve(const ketogpu_snapshot *sp, const ketogpu_check_request *req
         return KETOGPU_EINVAL;
     }
     const Snapshot &s = *reinterpret_cast<const Snapshot *>(sp);
+    std::shared_lock<std::shared_mutex> rd(s.mu);  // against in-place writes
     *root = NONE;
     *target = NONE;
     if (req->subject.kind != KETOGPU_SUBJECT_ID && req->subject.kind != KETOGPU_SUBJECT_SET) {
@@ -306,6 +307,7 @@ int ketogpu_resolve_batch(const ketogpu_snapshot *sp, const ketogpu_request_batc
         return KETOGPU_EINVAL;
     }
     const Snapshot &s = *reinterpret_cast<const Snapshot *>(sp);
+    std::shared_lock<std::shared_mutex> rd(s.mu);  // against in-place writes
     auto col = [](const char *d, const uint64_t *o, size_t i) {
         return (d && o) ? std::string_view(d + o[i], o[i + 1] - o[i]) : std::string_view();
     };
@@ -335,6 +337,7 @@ int ketogpu_expand(const ketogpu_snapshot *sp, const ketogpu_subject *subj, int3
         if (!sp || !subj || !out) throw Error(KETOGPU_EINVAL, "null argument");
         *out = nullptr;
         const Snapshot &s = *reinterpret_cast<const Snapshot *>(sp);
+        std::shared_lock<std::shared_mutex> rd(s.mu);  // against in-place writes
         if (subj->kind != KETOGPU_SUBJECT_ID && subj->kind != KETOGPU_SUBJECT_SET)
             throw Error(KETOGPU_EINVAL, "subject is not allowed to be nil");
         if (rest_depth <= 0) return KETOGPU_OK;  // engine.go:31-33

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <string_view>
@@ -168,6 +169,25 @@ struct Snapshot {
 
     ketogpu_snapshot_stats stats{};
 
+    // ---- writable layout (KETOGPU_BUILD_WRITABLE, snapshot_write.cpp)
+    // Device rows carry free slots filled with placeholder nodes that have no rows and no
+    // names: Df (interior, the largest interior id) pads forward rows, Dbi (interior, the
+    // next smaller id) pads the interior part of reverse rows and Dbo (the largest
+    // expandable id) their other part.  The forward search can only reach Df and the
+    // backward search only Dbi/Dbo, so a meet or a pull never happens at a placeholder and
+    // sorted rows stay sorted.  Ids [N, n_cap) are reserved for new subjects (reverse rows
+    // of only free slots).
+    bool writable = false;
+    uint32_t Df = NONE, Dbi = NONE, Dbo = NONE, n_cap = 0;
+    TripleMap group_idx;                // (namespace id, object, relation) -> index into groups
+    uint64_t version = 0;               // writes applied in place
+    struct Patch {
+        uint8_t rev;                    // 0: forward row of node, 1: reverse row
+        uint32_t node;
+    };
+    std::vector<Patch> patches;         // device rows changed, in write order (engines replay)
+    mutable std::shared_mutex mu;       // writes exclusive; engine, resolve and expand calls shared
+
     // ---- helpers
     const Namespace *ns_by_name(std::string_view name) const {
         for (auto &n : namespaces)
@@ -185,6 +205,10 @@ struct Snapshot {
     RowRef materialize(bool any_ns, int32_t ns, uint32_t obj, bool any_obj, uint32_t rel,
                        bool any_rel, std::vector<uint32_t> &out) const;
 };
+
+// writable layout: pad the compact device rows (snapshot_write.cpp)
+void make_writable(Snapshot &s);
+void index_groups(Snapshot &s);  // group_idx from groups
 
 // ---- host engine entry points (host_engine.cpp)
 struct ResolvedRoot {

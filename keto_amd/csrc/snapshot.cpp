@@ -295,6 +295,19 @@ void finish_snapshot(ketogpu_builder *b) {
     for (const Group &g : S.groups)
         if (b->ns_known(g.ns)) b->set_node(g.ns, g.obj, g.rel);
 
+    // writable layout: three placeholder nodes (no name, no rows) that pad device rows
+    // (ketogpu_internal.hpp, snapshot_write.cpp); created last so they take the largest ids
+    // of their classes
+    const bool writable = (b->flags & KETOGPU_BUILD_WRITABLE) != 0;
+    uint32_t ph[3] = {NONE, NONE, NONE};  // Dbi, Df (interior), Dbo (expandable)
+    if (writable)
+        for (uint32_t &x : ph) {
+            x = (uint32_t)S.node_kind.size();
+            S.node_kind.push_back(KETOGPU_SUBJECT_ID);
+            S.node_ns.push_back(0);
+            S.node_a.push_back(0);
+            S.node_b.push_back(0);
+        }
     const uint32_t N = (uint32_t)S.node_kind.size();
     const size_t ps = (size_t)S.page_size;
     std::vector<RowRef> row(N);
@@ -340,6 +353,7 @@ void finish_snapshot(ketogpu_builder *b) {
         for (uint32_t i = 0; i < row[v].len; i++)
             if (cls[p[i]] == 1) cls[p[i]] = 0;
     }
+    if (writable) cls[ph[0]] = cls[ph[1]] = 0, cls[ph[2]] = 1;
     std::vector<uint32_t> perm(N), inv(N);
     {
         uint32_t c[3] = {0, 0, 0};
@@ -357,6 +371,7 @@ void finish_snapshot(ketogpu_builder *b) {
     for (auto &x : S.sid_node)
         if (x != NONE) x = perm[x];
     S.set_node.remap(perm);
+    if (writable) S.writable = true, S.Dbi = perm[ph[0]], S.Df = perm[ph[1]], S.Dbo = perm[ph[2]];
     {
         std::vector<uint8_t> k(N);
         std::vector<int32_t> ns(N);
@@ -464,6 +479,7 @@ void finish_snapshot(ketogpu_builder *b) {
     st.num_interior_edges = nint;
     st.num_rev_edges = nrev;
     st.num_wildcard_nodes = wild;
+    if (writable) make_writable(S);
     st.build_seconds =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - b->t0).count();
 }
@@ -498,7 +514,7 @@ int ketogpu_builder_new(const ketogpu_namespace *namespaces, size_t num_namespac
         if (opts) {
             if (opts->page_size < 0) throw Error(KETOGPU_EINVAL, "negative page size");
             if (opts->page_size) S.page_size = opts->page_size;
-            if (opts->flags & ~(KETOGPU_BUILD_SORT | KETOGPU_ORDER_NULLS_LAST))
+            if (opts->flags & ~(KETOGPU_BUILD_SORT | KETOGPU_ORDER_NULLS_LAST | KETOGPU_BUILD_WRITABLE))
                 throw Error(KETOGPU_EINVAL, "unknown builder flags");
             b->flags = opts->flags;
             S.nulls_last = (opts->flags & KETOGPU_ORDER_NULLS_LAST) != 0;
@@ -609,12 +625,14 @@ static int rebuild(const ketogpu_snapshot *basep, const ketogpu_row_batch *inser
         if (!basep || !out) throw Error(KETOGPU_EINVAL, "null argument");
         *out = nullptr;
         const Snapshot &B = *reinterpret_cast<const Snapshot *>(basep);
+        std::shared_lock<std::shared_mutex> rd(B.mu);
         std::vector<ketogpu_namespace> nss;
         if (namespaces)
             nss.assign(namespaces, namespaces + num_namespaces);
         else
             for (const Namespace &n : B.namespaces) nss.push_back(ketogpu_namespace{n.id, n.name.c_str()});
-        ketogpu_build_opts opts{B.page_size, B.nulls_last ? KETOGPU_ORDER_NULLS_LAST : 0u};
+        ketogpu_build_opts opts{B.page_size, (B.nulls_last ? KETOGPU_ORDER_NULLS_LAST : 0u) |
+                                                 (B.writable ? KETOGPU_BUILD_WRITABLE : 0u)};
         ketogpu_builder *raw_b = nullptr;
         int rc = ketogpu_builder_new(nss.data(), nss.size(), &opts, &raw_b);
         if (rc) return rc;
@@ -733,7 +751,9 @@ int ketogpu_snapshot_stats_get(const ketogpu_snapshot *s, ketogpu_snapshot_stats
         set_last_error("null argument");
         return KETOGPU_EINVAL;
     }
-    *out = reinterpret_cast<const Snapshot *>(s)->stats;
+    const Snapshot &S = *reinterpret_cast<const Snapshot *>(s);
+    std::shared_lock<std::shared_mutex> rd(S.mu);
+    *out = S.stats;
     return KETOGPU_OK;
 }
 

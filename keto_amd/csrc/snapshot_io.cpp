@@ -18,7 +18,7 @@ using namespace ketogpu;
 namespace {
 
 constexpr char kMagic[8] = {'K', 'E', 'T', 'O', 'S', 'N', 'A', 'P'};
-constexpr uint32_t kFormat = 3;  // 3: row order flag
+constexpr uint32_t kFormat = 4;  // 4: writable layout; 3: row order flag
 
 struct File {
     FILE *f = nullptr;
@@ -138,7 +138,12 @@ void validate(const Snapshot &s, const std::string &path) {
             if (x >= lim) bad(what);
     };
     csr(s.fint_off, s.fint_col, s.Nx, s.Ni, "forward rows");
-    csr(s.rev_off, s.rev_col, N, s.Nx, "reverse rows");
+    if (s.writable) {
+        if (!(s.n_cap >= N && s.Df < s.Ni && s.Dbi < s.Ni && s.Dbo >= s.Ni && s.Dbo < s.Nx)) bad("writable layout");
+        csr(s.rev_off, s.rev_col, s.n_cap, s.Nx, "reverse rows");
+    } else {
+        csr(s.rev_off, s.rev_col, N, s.Nx, "reverse rows");
+    }
     if (s.has_ambiguous && s.row_amb.size() < ((uint64_t)s.Nx + 31) / 32) bad("ambiguous-row bitmap");
 }
 
@@ -150,6 +155,7 @@ int ketogpu_snapshot_save(const ketogpu_snapshot *sp, const char *path) {
     try {
         if (!sp || !path) throw Error(KETOGPU_EINVAL, "null argument");
         const Snapshot &s = *reinterpret_cast<const Snapshot *>(sp);
+        std::shared_lock<std::shared_mutex> rd(s.mu);
         File f(path, "wb");
         f.write(kMagic, sizeof kMagic);
         f.put<uint32_t>(kFormat);
@@ -188,6 +194,11 @@ int ketogpu_snapshot_save(const ketogpu_snapshot *sp, const char *path) {
         f.put_vec(s.rev_off);
         f.put_vec(s.rev_col);
         f.put_vec(s.row_amb);
+        f.put<uint8_t>(s.writable);
+        f.put<uint32_t>(s.Df);
+        f.put<uint32_t>(s.Dbi);
+        f.put<uint32_t>(s.Dbo);
+        f.put<uint32_t>(s.n_cap);
         f.put(s.stats);
         f.write(kMagic, sizeof kMagic);  // trailer: a complete file ends with the magic again
     } catch (const Error &e) {
@@ -248,12 +259,18 @@ int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out) {
         f.get_vec(s->rev_off);
         f.get_vec(s->rev_col);
         f.get_vec(s->row_amb);
+        s->writable = f.get<uint8_t>() != 0;
+        s->Df = f.get<uint32_t>();
+        s->Dbi = f.get<uint32_t>();
+        s->Dbo = f.get<uint32_t>();
+        s->n_cap = f.get<uint32_t>();
         s->stats = f.get<ketogpu_snapshot_stats>();
         f.read(magic, sizeof magic);
         if (memcmp(magic, kMagic, sizeof magic)) throw Error(KETOGPU_EINVAL, std::string(path) + ": truncated snapshot");
         validate(*s, path);
         for (uint32_t v = 0; v < s->N; v++)  // the subject-set index (sid_node is stored)
             if (s->node_kind[v] == KETOGPU_SUBJECT_SET) s->set_node.get_or_insert(s->node_ns[v], s->node_a[v], s->node_b[v], v);
+        if (s->writable) index_groups(*s);
         *out = reinterpret_cast<ketogpu_snapshot *>(s.release());
     } catch (const Error &e) {
         set_last_error(e.what());

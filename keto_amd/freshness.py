@@ -12,11 +12,18 @@ started on (the old engine lives until its last reference is dropped).  Unknown
 namespace names fail the whole transaction (GetNamespaceByName -> ErrNotFound), as in
 the reference.
 
-Cost: O(rows) host work plus one device-graph upload per transaction; batch writes (or
-coalesce them in a writer queue) on large graphs.  A device-side delta overlay that
-avoids the rebuild is the planned next step.
+Cost.  On a writable snapshot (Snapshot(..., writable=True): device rows with free slots,
+KETOGPU_BUILD_WRITABLE) a transaction is written IN PLACE (ketogpu_snapshot_write): the
+touched groups' host rows and the touched device rows are rewritten and the engine uploads
+just those rows (ketogpu_engine_sync) before `transact` returns — O(rows of the touched
+groups), not O(graph).  A batch the free slots cannot hold (a new group, an expandable node
+becoming interior, a full row, ...; include/ketogpu.h KETOGPU_WRITE_*) falls back to the
+rebuild below, which lays the rows out with fresh free slots.  On other snapshots every
+transaction rebuilds: O(rows) host work plus one device-graph upload.  `last_write`
+reports which path the last transaction took and its cost.
 """
 import threading
+import time
 
 from . import check, expand, persistence
 from .relationtuple import InternalRelationTuple, NilSubject
@@ -28,6 +35,7 @@ class VersionedEngine:
         self.engine_opts = engine_opts
         self._lock = threading.Lock()  # one writer at a time
         self.version = 0
+        self.last_write = None
         self._install(snapshot)
 
     def _install(self, snapshot):
@@ -50,11 +58,21 @@ class VersionedEngine:
     def transact(self, insert=(), delete=()):
         """TransactRelationTuples: insert, then delete; returns the new version"""
         with self._lock:
-            snap = self._state[0]
-            new = snap.apply(self._rows(insert), self._rows(delete))
-            self._install(new)
+            snap, eng = self._state[0], self._state[1]
+            ins, dele = self._rows(insert), self._rows(delete)
+            t0 = time.perf_counter()
+            res = snap.write(ins, dele)  # reason "not_writable" on a snapshot without free slots
+            if res["applied"]:
+                sync_ms, rows = eng.sync()  # the patched device rows, before returning
+                self.last_write = dict(res, path="in_place", sync_ms=sync_ms, synced_rows=rows,
+                                       ms=(time.perf_counter() - t0) * 1e3)
+            else:
+                self._install(snap.apply(ins, dele))
+                self.last_write = {"applied": False, "reason": res["reason"], "path": "rebuild",
+                                   "ms": (time.perf_counter() - t0) * 1e3}
             self.version += 1
             return self.version
+
 
     def reload_namespaces(self, namespaces):
         """Keto's KeyNamespaces reload (internal/driver/config/provider.go:87-110): the next

@@ -30,11 +30,12 @@ class Snapshot:
     KETOGPU_ORDER_*): "sqlite" (default), "mysql-bin", "cockroach" (NULLs first) or
     "postgres" (NULLs last); it decides where sorting and apply() place rows."""
 
-    def __init__(self, namespaces, page_size=100, sort=False, order="sqlite"):
+    def __init__(self, namespaces, page_size=100, sort=False, order="sqlite", writable=False):
         self.L = L.lib()
         self.namespaces = [(n, int(i)) for n, i in namespaces]
         arr = (L.Namespace * max(len(self.namespaces), 1))(*[L.Namespace(i, L.b(n)) for n, i in self.namespaces])
-        opts = L.BuildOpts(page_size, (L.BUILD_SORT if sort else 0) | L.ORDERS[order])
+        opts = L.BuildOpts(page_size, (L.BUILD_SORT if sort else 0) | L.ORDERS[order] |
+                           (L.BUILD_WRITABLE if writable else 0))
         h = C.c_void_p()
         L.check(self.L.ketogpu_builder_new(arr, len(self.namespaces), C.byref(opts), C.byref(h)))
         self._builder = h
@@ -77,38 +78,57 @@ class Snapshot:
         return s.finish()
 
     @classmethod
-    def from_rows(cls, namespaces, rows, page_size=100, sort=True, order="sqlite"):
-        s = cls(namespaces, page_size, sort=sort, order=order)
+    def from_rows(cls, namespaces, rows, page_size=100, sort=True, order="sqlite", writable=False):
+        s = cls(namespaces, page_size, sort=sort, order=order, writable=writable)
         if rows:
             s.append(persistence.columnar(rows))
         return s.finish()
 
     @classmethod
-    def from_tuples(cls, namespaces, tuples, page_size=100):
-        return cls.from_rows(namespaces, persistence.rows_from_tuples(namespaces, tuples), page_size, sort=True)
+    def from_tuples(cls, namespaces, tuples, page_size=100, writable=False):
+        return cls.from_rows(namespaces, persistence.rows_from_tuples(namespaces, tuples), page_size, sort=True,
+                             writable=writable)
 
     @classmethod
-    def from_columns(cls, namespaces, cols, page_size=100, sort=False, order="sqlite"):
-        s = cls(namespaces, page_size, sort=sort, order=order)
+    def from_columns(cls, namespaces, cols, page_size=100, sort=False, order="sqlite", writable=False):
+        s = cls(namespaces, page_size, sort=sort, order=order, writable=writable)
         s.append(cols)
         return s.finish()
 
-    # ---- freshness (ketogpu_snapshot_apply)
+    # ---- freshness (ketogpu_snapshot_apply / ketogpu_snapshot_write)
+    @staticmethod
+    def _batch(rows):
+        if not rows:
+            return None, None
+        cols = persistence.columnar(list(rows))
+        rb = L.RowBatch(len(rows), _ptr(cols["namespace_id"]), _ptr(cols["object_data"]), _ptr(cols["object_off"]),
+                        _ptr(cols["relation_data"]), _ptr(cols["relation_off"]), _ptr(cols["subject_kind"]),
+                        _ptr(cols["subject_id_data"]), _ptr(cols["subject_id_off"]),
+                        _ptr(cols["ss_namespace_id"]), _ptr(cols["ss_object_data"]), _ptr(cols["ss_object_off"]),
+                        _ptr(cols["ss_relation_data"]), _ptr(cols["ss_relation_off"]))
+        return rb, cols
+
+    def write(self, insert_rows=(), delete_rows=()):
+        """in-place write on a writable snapshot (ketogpu_snapshot_write): the same batch
+        semantics as apply(); returns the result dict — "applied" False (with a "reason")
+        leaves the snapshot unchanged and the caller rebuilds with apply()"""
+        ins, keep_i = self._batch(insert_rows)
+        dele, keep_d = self._batch(delete_rows)
+        res = L.WriteResult()
+        L.check(self.L.ketogpu_snapshot_write(self.h, C.byref(ins) if ins else None, C.byref(dele) if dele else None,
+                                              C.byref(res)))
+        del keep_i, keep_d
+        return res.as_dict()
+
+    def version(self):
+        """writes applied in place so far"""
+        return int(self.L.ketogpu_snapshot_version(self.h))
+
     def apply(self, insert_rows=(), delete_rows=()):
         """the next version: raw rows (namespace_id, object, relation, subject_id|None, ss_ns,
         ss_obj, ss_rel) inserted, then every row matching a delete removed"""
-        def batch(rows):
-            if not rows:
-                return None, None
-            cols = persistence.columnar(list(rows))
-            rb = L.RowBatch(len(rows), _ptr(cols["namespace_id"]), _ptr(cols["object_data"]), _ptr(cols["object_off"]),
-                            _ptr(cols["relation_data"]), _ptr(cols["relation_off"]), _ptr(cols["subject_kind"]),
-                            _ptr(cols["subject_id_data"]), _ptr(cols["subject_id_off"]),
-                            _ptr(cols["ss_namespace_id"]), _ptr(cols["ss_object_data"]), _ptr(cols["ss_object_off"]),
-                            _ptr(cols["ss_relation_data"]), _ptr(cols["ss_relation_off"]))
-            return rb, cols
-        ins, keep_i = batch(insert_rows)
-        dele, keep_d = batch(delete_rows)
+        ins, keep_i = self._batch(insert_rows)
+        dele, keep_d = self._batch(delete_rows)
         h = C.c_void_p()
         L.check(self.L.ketogpu_snapshot_apply(self.h, C.byref(ins) if ins else None, C.byref(dele) if dele else None,
                                               C.byref(h)))

@@ -1,0 +1,153 @@
+"""Write-path freshness at config #2 scale: what an in-place write
+costs on a writable snapshot, what the free slots cost the checks, and that the engine
+answers like a rebuilt one afterwards.
+
+    python tools/bench_writes.py [--tuples 50000000] [--sizes 1,10,100,1000,10000]
+
+Steps: the config #2 RBAC graph (synth.rbac) is built twice — compact and writable
+(KETOGPU_BUILD_WRITABLE) — and 1M requests are timed on both (HBM-resident, as bench.py's
+hbm leg, and host to host from pinned memory, as bench.py's value).  Then write batches of
+each size (half group-membership inserts — existing and new users — half deletes of
+existing membership rows) go through ketogpu_snapshot_write + ketogpu_engine_sync; every
+inserted membership must be allowed right after its write (read-your-writes).  Finally
+the compact snapshot gets the same batches through ketogpu_snapshot_apply (the rebuild
+path, timed) and a request sample — the config's requests plus every written pair — must
+agree bit for bit between the written engine and the rebuilt one.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime in the process)
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from keto_amd import check, synth  # noqa: E402
+from keto_amd.relationtuple import InternalRelationTuple, SubjectID  # noqa: E402
+from keto_amd.snapshot import Snapshot  # noqa: E402
+
+T0 = time.time()
+
+
+def log(msg):
+    print(f"[writes {time.time() - T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def timed_hbm(eng, roots, targets, steps=5):
+    q = eng.upload(roots, targets)
+    q.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        q.run()
+    torch.cuda.synchronize()
+    return len(roots) * steps / (time.perf_counter() - t0)
+
+
+def timed_host(eng, roots, targets, steps=5):
+    n = len(roots)
+    r, t = check.pinned(roots), check.pinned(targets)
+    a = check.PinnedBuffer((n + 63) // 64, np.uint64)
+    eng.check_ids_raw(r.p, t.p, n, a.p)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.check_ids_raw(r.p, t.p, n, a.p)
+    return n * steps / (time.perf_counter() - t0)
+
+
+def membership_rows(cols, k, rng):
+    """k random existing groups:g#member@u rows"""
+    ns, kind = cols["namespace_id"], cols["subject_kind"]
+    cand = np.flatnonzero((ns == 1) & (kind == 0))
+    pick = cand[rng.integers(0, len(cand), size=k)]
+    s = lambda c, i: bytes(cols[c + "_data"][cols[c + "_off"][i]:cols[c + "_off"][i + 1]]).decode()
+    return [(1, s("object", i), s("relation", i), s("subject_id", i), None, None, None) for i in pick]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--tuples", type=int, default=50_000_000)
+    p.add_argument("--sizes", default="1,10,100,1000,10000")
+    p.add_argument("--sample", type=int, default=100_000)
+    a = p.parse_args()
+    f = a.tuples / 50e6
+    w = synth.rbac(users=int(10e6 * f), groups=int(100e3 * f), docs=int(2e6 * f), tuples=a.tuples, checks=1_000_000,
+                   check_seed=synth.SEED + 1)
+    log(f"generated {w.counts}")
+    out = {"workload": f"config2_rbac_{a.tuples}", "checks": w.n_checks}
+    t0 = time.time()
+    compact = Snapshot.from_columns(w.namespaces, w.columns)
+    out["build_s"] = {"compact": round(time.time() - t0, 1)}
+    t0 = time.time()
+    wsnap = Snapshot.from_columns(w.namespaces, w.columns, writable=True)
+    out["build_s"]["writable"] = round(time.time() - t0, 1)
+    gc, gw = compact.graph(), wsnap.graph()
+    out["device_entries"] = {"compact": {"fint": int(gc["fint_off"][-1]), "rev": int(gc["rev_off"][-1])},
+                             "writable": {"fint": int(gw["fint_off"][-1]), "rev": int(gw["rev_off"][-1])}}
+    log(f"snapshots built {out['build_s']}, device entries {out['device_entries']}")
+    roots, targets = w.resolve(compact)
+    wroots, wtargets = w.resolve(wsnap)
+    ec, ew = check.Engine(compact), check.Engine(wsnap)
+    out["checks_per_s"] = {
+        "compact_hbm": round(timed_hbm(ec, roots, targets)), "writable_hbm": round(timed_hbm(ew, wroots, wtargets)),
+        "compact_host": round(timed_host(ec, roots, targets)), "writable_host": round(timed_host(ew, wroots, wtargets))}
+    log(f"throughput {out['checks_per_s']}")
+    base_answers = ew.check_ids(wroots, wtargets)
+    same0 = int((base_answers == ec.check_ids(roots, targets)).all())
+    del ec
+
+    rng = np.random.default_rng(7)
+    prng = random.Random(7)
+    batches, written = [], []
+    n_groups = int(100e3 * f)
+    for size in [int(x) for x in a.sizes.split(",")]:
+        n_ins, n_del = (size + 1) // 2, size // 2
+        ins = [(1, f"g{prng.randrange(n_groups)}", "member",
+                f"u{prng.randrange(int(10e6 * f))}" if prng.random() < 0.8 else f"newuser{len(written)}_{k}",
+                None, None, None) for k in range(n_ins)]
+        dele = membership_rows(w.columns, n_del, rng)
+        res = wsnap.write(ins, dele)
+        t1 = time.perf_counter()
+        sync_ms, rows = ew.sync()
+        entry = {"size": size, "applied": res["applied"], "reason": res["reason"],
+                 "write_ms": round(res["seconds"] * 1e3, 3), "sync_ms": round(sync_ms, 3),
+                 "total_ms": round(res["seconds"] * 1e3 + (time.perf_counter() - t1) * 1e3, 3),
+                 "device_rows": rows, "groups_touched": res["groups_touched"], "new_nodes": res["new_nodes"]}
+        if res["applied"]:
+            tuples = [InternalRelationTuple("groups", r[1], "member", SubjectID(r[3])) for r in ins]
+            got = ew.check_batch(tuples)
+            entry["inserted_allowed"] = f"{int(np.sum(got))}/{len(tuples)}"
+        batches.append((ins, dele))
+        written += ins + dele
+        out.setdefault("writes", []).append(entry)
+        log(f"write {entry}")
+
+    # the rebuild path on the compact snapshot, and the cross-check
+    t0 = time.time()
+    cur = compact
+    rebuild_s = []
+    for ins, dele in batches:
+        t1 = time.time()
+        cur = cur.apply(ins, dele)
+        rebuild_s.append(round(time.time() - t1, 1))
+    out["rebuild_s_per_batch"] = rebuild_s
+    log(f"rebuilt in {time.time() - t0:.1f}s: {rebuild_s}")
+    er = check.Engine(cur)
+    idx = np.random.default_rng(3).permutation(w.n_checks)[:a.sample]
+    reqs = [InternalRelationTuple(ns, o, r, SubjectID(s["subject_id"])) for ns, o, r, s in w.requests(idx)]
+    reqs += [InternalRelationTuple("groups", r[1], "member", SubjectID(r[3])) for r in written]
+    reqs += [InternalRelationTuple("docs", f"d{prng.randrange(int(2e6 * f))}", "viewer", SubjectID(r[3]))
+             for r in written]
+    got, want = ew.check_batch(reqs), er.check_batch(reqs)
+    out["cross_check"] = {"requests": len(reqs), "mismatches": int(np.sum(np.asarray(got) != np.asarray(want))),
+                          "against": "engine over the rebuilt snapshot (ketogpu_snapshot_apply per batch)",
+                          "before_writes_equal": bool(same0)}
+    log(f"cross-check {out['cross_check']}")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,6 @@
 """Per-rank host memory of the partition-aware loader against world size (CPU, gloo).
 
-    python tools/shard_rss.py --scale 0.004 --worlds 1,2,4 > profiles/r02/shard_rss.json
+    python tools/shard_rss.py --scale 0.01 --worlds 1,2,4,8 --out profiles/r02/shard_rss.json
 
 For each world size, `world` processes (gloo over 127.0.0.1) stream the same config #5
 row stream (synth.config5 at --scale x 5B tuples) through Shard.load — the loader and id
@@ -62,6 +62,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=0.004)
     ap.add_argument("--worlds", default="1,2,4")
+    ap.add_argument("--out", default="-", help="JSON file (default stdout; gloo logs to stdout too)")
     a = ap.parse_args()
     out = {"workload": f"config5 x{a.scale} ({int(5e9 * a.scale)} tuples)", "backend": "gloo (CPU)", "runs": []}
     ctx = mp.get_context("spawn")
@@ -85,7 +86,12 @@ def main():
     for r in out["runs"]:
         r["loader_array_ratio_vs_world1"] = round(r["max_loader_array_gb"] / base["max_loader_array_gb"], 3)
         r["rss_growth_ratio_vs_world1"] = round(r["max_rss_growth_gb"] / max(base["max_rss_growth_gb"], 1e-9), 3)
-    print(json.dumps(out, indent=1))
+    text = json.dumps(out, indent=1)
+    if a.out == "-":
+        print(text)
+    else:
+        with open(a.out, "w") as f:
+            f.write(text + "\n")
 
 
 if __name__ == "__main__":
