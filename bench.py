@@ -323,6 +323,11 @@ def main_partitioned(a, rank, world, local):
     log(f"shard loaded in {t_load:.1f}s: {sst['rows']} rows streamed, {sst['owned_nodes']} nodes owned, "
         f"host arrays {sst['host_bytes'] / 1e9:.2f} GB, peak RSS {rss_load:.2f} GB")
     roots, targets, status = sh.resolve_batch(w.request_batch())
+    # requests in pinned host memory, as for the replicated line (ketogpu_part_begin copies
+    # them to HBM by DMA)
+    from keto_amd import check
+    pinned = (check.pinned(roots), check.pinned(targets))
+    roots, targets = pinned[0].array, pinned[1].array
     eng = PartitionedEngine(sh, device=local, record_capacity=1 << 26)
     for _ in range(max(a.warmup, 1)):  # the first call also picks the direction (auto)
         got = eng.check_ids(roots, targets)
