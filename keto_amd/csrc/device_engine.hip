@@ -2257,6 +2257,19 @@ struct ketogpu_engine {
     // lock before every traversal.
     uint64_t synced_version = 0;
     size_t patch_pos = 0;
+    // what edge records carry about the node they point at: its forward row's interior
+    // successors and its reverse row's interior predecessors.  In a writable layout only the
+    // real entries count (they come first; the free slots after them are never read through
+    // a record), so leaf groups stay dead ends and placeholders never become pending.
+    static uint32_t fdeg(const Snapshot &s, uint32_t u) {
+        if (!s.writable) return (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]);
+        const uint32_t *b = s.fint_col.data() + s.fint_off[u], *e = s.fint_col.data() + s.fint_off[u + 1];
+        return (uint32_t)(std::lower_bound(b, e, s.Df) - b);
+    }
+    static uint32_t ideg(const Snapshot &s, uint32_t v) {
+        const uint32_t *b = s.rev_col.data() + s.rev_off[v], *e = s.rev_col.data() + s.rev_off[v + 1];
+        return (uint32_t)(std::lower_bound(b, e, s.writable ? s.Dbi : s.Ni) - b);
+    }
     uint64_t sync() {
         const Snapshot &s = *snap;
         if (!s.writable || synced_version == s.version) return 0;
@@ -2270,17 +2283,13 @@ struct ketogpu_engine {
         std::vector<uint64_t> seg;  // (destination, source, length, which) per row
         std::vector<uint32_t> cols;
         std::vector<FRec> recs;
-        auto ideg = [&](uint32_t v) {
-            const uint32_t *b = s.rev_col.data() + s.rev_off[v], *e = s.rev_col.data() + s.rev_off[v + 1];
-            return (uint32_t)(std::lower_bound(b, e, s.Ni) - b);
-        };
         for (uint32_t v : fr) {
             const uint64_t b = s.fint_off[v], e = s.fint_off[v + 1];
             seg.insert(seg.end(), {b, (uint64_t)cols.size(), e - b, 0});
             for (uint64_t k = b; k < e; k++) {
                 const uint32_t u = s.fint_col[k];
                 cols.push_back(u);
-                recs.push_back(FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u], 0});
+                recs.push_back(FRec{u, fdeg(s, u), (uint32_t)s.fint_off[u], 0});
             }
         }
         for (uint32_t v : rr) {
@@ -2289,7 +2298,7 @@ struct ketogpu_engine {
             for (uint64_t k = b; k < e; k++) {
                 const uint32_t u = s.rev_col[k];
                 cols.push_back(u);
-                recs.push_back(u < s.Ni ? FRec{u, ideg(u), (uint32_t)s.rev_off[u], 0} : FRec{u, 0, 0, 0});
+                recs.push_back(u < s.Ni ? FRec{u, ideg(s, u), (uint32_t)s.rev_off[u], 0} : FRec{u, 0, 0, 0});
             }
         }
         const uint64_t nseg = seg.size() / 4;
@@ -2419,22 +2428,18 @@ struct ketogpu_engine {
             for (size_t e = 0; e < rec.size(); e++) {
                 uint32_t u = s.fint_col[e];
                 const uint32_t hid = hub_of_h.empty() ? KETOGPU_NODE_NONE : hub_of_h[u];
-                rec[e] = FRec{u, (uint32_t)(s.fint_off[u + 1] - s.fint_off[u]), (uint32_t)s.fint_off[u],
-                              hid == KETOGPU_NODE_NONE ? 0u : hid + 1};
+                rec[e] = FRec{u, fdeg(s, u), (uint32_t)s.fint_off[u], hid == KETOGPU_NODE_NONE ? 0u : hid + 1};
             }
             frec = up(rec);
         }
         if (use_bidi) {
             // interior predecessors of v = the prefix of rev(v) below Ni (sorted rows)
-            std::vector<uint32_t> ideg(s.Ni);
-            for (uint32_t v = 0; v < s.Ni; v++) {
-                const uint32_t *b = s.rev_col.data() + s.rev_off[v], *e = s.rev_col.data() + s.rev_off[v + 1];
-                ideg[v] = (uint32_t)(std::lower_bound(b, e, s.Ni) - b);
-            }
+            std::vector<uint32_t> id(s.Ni);
+            for (uint32_t v = 0; v < s.Ni; v++) id[v] = ideg(s, v);
             std::vector<FRec> rec(s.rev_col.size());
             for (size_t e = 0; e < rec.size(); e++) {
                 uint32_t v = s.rev_col[e];
-                rec[e] = v < s.Ni ? FRec{v, ideg[v], (uint32_t)s.rev_off[v], 0} : FRec{v, 0, 0, 0};
+                rec[e] = v < s.Ni ? FRec{v, id[v], (uint32_t)s.rev_off[v], 0} : FRec{v, 0, 0, 0};
             }
             brec = up(rec);
         }

@@ -181,6 +181,7 @@ struct Snapshot {
     uint32_t Df = NONE, Dbi = NONE, Dbo = NONE, n_cap = 0;
     TripleMap group_idx;                // (namespace id, object, relation) -> index into groups
     uint64_t version = 0;               // writes applied in place
+    uint64_t row_garbage = 0;           // stale group rows left by grown groups (group_col, row_col)
     struct Patch {
         uint8_t rev;                    // 0: forward row of node, 1: reverse row
         uint32_t node;

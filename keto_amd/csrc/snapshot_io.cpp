@@ -199,6 +199,7 @@ int ketogpu_snapshot_save(const ketogpu_snapshot *sp, const char *path) {
         f.put<uint32_t>(s.Dbi);
         f.put<uint32_t>(s.Dbo);
         f.put<uint32_t>(s.n_cap);
+        f.put<uint64_t>(s.row_garbage);
         f.put(s.stats);
         f.write(kMagic, sizeof kMagic);  // trailer: a complete file ends with the magic again
     } catch (const Error &e) {
@@ -264,6 +265,7 @@ int ketogpu_snapshot_load(const char *path, ketogpu_snapshot **out) {
         s->Dbi = f.get<uint32_t>();
         s->Dbo = f.get<uint32_t>();
         s->n_cap = f.get<uint32_t>();
+        s->row_garbage = f.get<uint64_t>();
         s->stats = f.get<ketogpu_snapshot_stats>();
         f.read(magic, sizeof magic);
         if (memcmp(magic, kMagic, sizeof magic)) throw Error(KETOGPU_EINVAL, std::string(path) + ": truncated snapshot");

@@ -94,6 +94,15 @@ void make_writable(Snapshot &S) {
     S.rev_off.swap(ro);
     S.rev_col.swap(rc);
     index_groups(S);
+    // room for the writes: new nodes take reserved ids, grown groups are appended
+    for (auto *v : {&S.node_a, &S.node_b, &S.key_id}) v->reserve(S.n_cap);
+    S.node_kind.reserve(S.n_cap);
+    S.ambiguous.reserve(S.n_cap);
+    S.node_ns.reserve(S.n_cap);
+    S.node_row.reserve(S.n_cap);
+    S.sid_node.reserve(S.sid_node.size() + reserve);
+    S.group_col.reserve(S.group_col.size() + S.group_col.size() / 4 + 1024);
+    S.row_col.reserve(S.row_col.size() + S.row_col.size() / 4 + 1024);
 }
 
 void index_groups(Snapshot &S) {
@@ -294,7 +303,9 @@ struct Writer {
         }
     }
 
-    // new row lists of the touched groups (subjects, DB order)
+    // new row lists of the touched groups (subjects, DB order).  An insert goes after the
+    // last old row that sorts before or equal to it (binary search: the group's rows are
+    // in ORDER BY order), deletes filter node ids; O(group rows) copying, O(log) compares.
     void merge() {
         for (auto &[gi, op] : ops) {
             const Group &g = S.groups[gi];
@@ -304,14 +315,21 @@ struct Writer {
             });
             std::vector<uint32_t> out;
             out.reserve(g.valid + op.ins.size());
-            size_t k = 0;
-            for (uint32_t i = 0; i < g.valid; i++) {
-                const SubjKey ko = key_of(old[i]);
-                // an inserted row goes after every row that sorts before or equal to it
-                while (k < op.ins.size() && cmp_subj(op.ins[k].first, ko, S.nulls_last) < 0) out.push_back(op.ins[k++].second);
-                out.push_back(old[i]);
+            uint32_t done = 0;
+            for (const auto &[key, subj] : op.ins) {
+                uint32_t lo = done, hi = g.valid;  // first old row that sorts after the insert
+                while (lo < hi) {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    if (cmp_subj(key_of(old[mid]), key, S.nulls_last) <= 0)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                out.insert(out.end(), old + done, old + lo);
+                out.push_back(subj);
+                done = lo;
             }
-            while (k < op.ins.size()) out.push_back(op.ins[k++].second);
+            out.insert(out.end(), old + done, old + g.valid);
             if (!op.del.empty()) {
                 std::vector<uint32_t> &dl = op.del;
                 std::sort(dl.begin(), dl.end());
@@ -325,31 +343,53 @@ struct Writer {
         }
     }
 
+    // grown groups are copied to the end of the row arrays; once the stale copies would
+    // outweigh the live rows, the batch goes to the rebuild (which compacts)
+    void budget() const {
+        uint64_t grow = 0;
+        for (const auto &[gi, rows] : new_rows)
+            if (rows.size() > S.groups[gi].valid) grow += S.groups[gi].valid;
+        if (S.row_garbage + grow > std::max<uint64_t>(S.stats.num_edges, 1u << 20)) throw Refuse{KETOGPU_WRITE_FULL};
+    }
+
     // device row edits: node -> (added, removed) neighbours
     struct RowEdit {
         std::vector<uint32_t> add, rem;
     };
     std::map<uint32_t, RowEdit> fwd, rev;  // fint(g) edits, rev(s) edits
 
+    // edges that appear or disappear: only the batch's subjects can change, so one pass over
+    // the old rows marks which of them were present
     void diff() {
         for (auto &[gi, rows] : new_rows) {
             const Group &g = S.groups[gi];
             const uint32_t v = S.set_node.get(g.ns, g.obj, g.rel);
-            std::vector<uint32_t> a(S.group_col.begin() + g.begin, S.group_col.begin() + g.begin + g.valid), b(rows);
-            std::sort(a.begin(), a.end());
-            a.erase(std::unique(a.begin(), a.end()), a.end());
-            std::sort(b.begin(), b.end());
-            b.erase(std::unique(b.begin(), b.end()), b.end());
-            std::vector<uint32_t> add, rem;
-            std::set_difference(b.begin(), b.end(), a.begin(), a.end(), std::back_inserter(add));
-            std::set_difference(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(rem));
-            for (uint32_t s : add) {
-                if (!(s & kNew) && s < S.Ni) fwd[v].add.push_back(s);
-                rev[s].add.push_back(v);
-            }
-            for (uint32_t s : rem) {
-                if (!(s & kNew) && s < S.Ni) fwd[v].rem.push_back(s);
-                rev[s].rem.push_back(v);
+            const GroupOps &op = ops[gi];
+            std::vector<uint32_t> cand;
+            for (const auto &x : op.ins) cand.push_back(x.second);
+            cand.insert(cand.end(), op.del.begin(), op.del.end());
+            std::sort(cand.begin(), cand.end());
+            cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+            std::vector<uint8_t> before(cand.size(), 0), after(cand.size(), 0);
+            auto mark = [&](const uint32_t *p, size_t n, std::vector<uint8_t> &m) {
+                for (size_t i = 0; i < n; i++) {
+                    auto it = std::lower_bound(cand.begin(), cand.end(), p[i]);
+                    if (it != cand.end() && *it == p[i]) m[it - cand.begin()] = 1;
+                }
+            };
+            mark(S.group_col.data() + g.begin, g.valid, before);
+            mark(rows.data(), rows.size(), after);
+            for (size_t k = 0; k < cand.size(); k++) {
+                if (before[k] == after[k]) continue;
+                const uint32_t s = cand[k];
+                const bool interior = !(s & kNew) && s < S.Ni;
+                if (after[k]) {
+                    if (interior) fwd[v].add.push_back(s);
+                    rev[s].add.push_back(v);
+                } else {
+                    if (interior) fwd[v].rem.push_back(s);
+                    rev[s].rem.push_back(v);
+                }
             }
         }
     }
@@ -373,14 +413,26 @@ struct Writer {
         return true;
     }
 
+    // real entries of a row region (the sorted prefix below the placeholder)
+    uint32_t real(const std::vector<uint32_t> &col, uint64_t b, uint64_t e, uint32_t pad) const {
+        return (uint32_t)(std::lower_bound(col.begin() + b, col.begin() + e, pad) - (col.begin() + b));
+    }
+    std::vector<uint32_t> fcount_changed, icount_changed;  // nodes whose record fields changed
+
     // check (commit = false) or apply (commit = true) the device row edits
     uint64_t device(bool commit) {
         auto id = [&](uint32_t s) { return (s & kNew) ? S.N + (s & ~kNew) : s; };
         uint64_t rows = 0;
         for (auto &[v, ed] : fwd) {
+            const uint32_t before = real(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df);
             if (!rewrite(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df, ed.add, ed.rem, commit))
                 throw Refuse{KETOGPU_WRITE_FULL};
-            if (commit) S.patches.push_back({0, v});
+            if (commit) {
+                S.patches.push_back({0, v});
+                // only an interior node is pointed at by forward records
+                if (v < S.Ni && real(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df) != before)
+                    fcount_changed.push_back(v);
+            }
             rows++;
         }
         for (auto &[s0, ed] : rev) {
@@ -393,7 +445,9 @@ struct Writer {
             if (u < S.Ni) {  // interior part [b, m) padded with Dbi, then the other part
                 uint64_t m = b;
                 while (m < e && S.rev_col[m] < S.Ni) m++;
+                const uint32_t before = real(S.rev_col, b, m, S.Dbi);
                 ok = rewrite(S.rev_col, b, m, S.Dbi, ai, ri, commit) && rewrite(S.rev_col, m, e, S.Dbo, ao, ro, commit);
+                if (ok && commit && real(S.rev_col, b, m, S.Dbi) != before) icount_changed.push_back(u);
             } else {
                 std::vector<uint32_t> add(ai), rem(ri);
                 add.insert(add.end(), ao.begin(), ao.end());
@@ -413,7 +467,7 @@ struct Writer {
             const uint32_t v = S.N++;
             if (f.key.kind == KETOGPU_SUBJECT_ID) {
                 const uint32_t sid = S.pool.intern(f.key.a.data(), f.key.a.size());
-                if (S.sid_node.size() <= sid) S.sid_node.resize(std::max<size_t>(sid + 1, S.sid_node.size() * 2), NONE);
+                if (S.sid_node.size() <= sid) S.sid_node.resize(sid + 1, NONE);  // capacity reserved
                 S.sid_node[sid] = v;
                 S.node_kind.push_back(KETOGPU_SUBJECT_ID);
                 S.node_ns.push_back(0);
@@ -446,15 +500,36 @@ struct Writer {
             const uint32_t v = S.set_node.get(g.ns, g.obj, g.rel);
             edges_minus += g.valid;
             edges_delta += rows.size();
-            g.begin = S.group_col.size();
-            for (uint32_t s : rows) S.group_col.push_back(id(s));
-            RowRef rr;
-            rr.off = S.row_col.size();
-            for (uint32_t s : rows) S.row_col.push_back(id(s));
+            RowRef rr = S.node_row[v];
+            if (rows.size() > g.valid) {  // grown: a new copy at the end (the old one is garbage)
+                S.row_garbage += g.valid;
+                g.begin = S.group_col.size();
+                rr.off = S.row_col.size();
+                S.group_col.resize(S.group_col.size() + rows.size());
+                S.row_col.resize(S.row_col.size() + rows.size());
+            }
+            for (size_t k = 0; k < rows.size(); k++) S.group_col[g.begin + k] = S.row_col[rr.off + k] = id(rows[k]);
             rr.len = rr.full_len = (uint32_t)rows.size();
             rr.first_bad = -1;
             g.valid = g.full_len = (uint32_t)rows.size();
             S.node_row[v] = rr;
+        }
+        // Edge records carry the real entry counts of the rows they point at (the free slots
+        // are never read through a record): rows holding a record for a node whose count
+        // changed are re-uploaded too — fint(p) for each interior predecessor p of a node
+        // whose interior successors changed, rev(x) for each successor x of an interior node
+        // whose interior predecessors changed
+        for (uint32_t v : fcount_changed) {
+            const uint64_t b = S.rev_off[v];
+            const uint32_t n = real(S.rev_col, b, S.rev_off[v + 1], S.Dbi);
+            for (uint32_t k = 0; k < n; k++) S.patches.push_back({0, S.rev_col[b + k]}), res.device_rows++;
+        }
+        for (uint32_t u : icount_changed) {
+            const RowRef &r = S.node_row[u];
+            std::vector<uint32_t> xs(S.row_col.begin() + r.off, S.row_col.begin() + r.off + r.len);
+            std::sort(xs.begin(), xs.end());
+            xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+            for (uint32_t x : xs) S.patches.push_back({1, x}), res.device_rows++;
         }
         auto &st = S.stats;
         st.num_rows = st.num_rows + n_ins - n_del;
@@ -496,6 +571,7 @@ int ketogpu_snapshot_write(ketogpu_snapshot *sp, const ketogpu_row_batch *insert
             try {
                 w.plan(ins, del);
                 w.merge();
+                w.budget();
                 w.diff();
                 w.device(false);  // every touched row fits: nothing below can refuse
             } catch (const Refuse &r) {

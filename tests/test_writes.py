@@ -239,7 +239,8 @@ def test_versioned_engine_writes_in_place_and_reads_them():
         assert ve.check_many(tuples) == [bool(x) for x in want], step
         assert list(ve._state[1].check_batch(tuples)) == [bool(x) for x in want], step  # the id path
         orc = randgraph.oracle_store(namespaces, cur)
-        for ns, o, r, _ in reqs[:40]:
+        known = {n for n, _ in namespaces}
+        for ns, o, r, _ in [q for q in reqs if q[0] in known][:40]:
             got = json.loads(ve._state[2].build_tree_json(rt.SubjectSet(ns, o, r), 3))
             want_tree = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, 3)
             assert got == want_tree, (step, ns, o, r)

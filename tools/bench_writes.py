@@ -38,7 +38,8 @@ def log(msg):
 
 def timed_hbm(eng, roots, targets, steps=5):
     q = eng.upload(roots, targets)
-    q.run()
+    for _ in range(3):  # the first two runs of >= 65536 requests are the plan trials
+        q.run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -94,7 +95,9 @@ def main():
     out["checks_per_s"] = {
         "compact_hbm": round(timed_hbm(ec, roots, targets)), "writable_hbm": round(timed_hbm(ew, wroots, wtargets)),
         "compact_host": round(timed_host(ec, roots, targets)), "writable_host": round(timed_host(ew, wroots, wtargets))}
-    log(f"throughput {out['checks_per_s']}")
+    keys = ("plan", "spilled_units", "spilled_requests", "main_ms", "main_bytes", "unit_launches")
+    out["run_stats"] = {"compact": {k: ec.last_stats()[k] for k in keys}, "writable": {k: ew.last_stats()[k] for k in keys}}
+    log(f"throughput {out['checks_per_s']} stats {out['run_stats']}")
     base_answers = ew.check_ids(wroots, wtargets)
     same0 = int((base_answers == ec.check_ids(roots, targets)).all())
     del ec
@@ -102,21 +105,28 @@ def main():
     rng = np.random.default_rng(7)
     prng = random.Random(7)
     batches, written = [], []
-    n_groups = int(100e3 * f)
     for size in [int(x) for x in a.sizes.split(",")]:
         n_ins, n_del = (size + 1) // 2, size // 2
-        ins = [(1, f"g{prng.randrange(n_groups)}", "member",
+        # inserts into existing groups (a row of a group that has none creates a group: a
+        # rebuild), 80% existing users, 20% new ones
+        groups = [r[1] for r in membership_rows(w.columns, n_ins, rng)]
+        ins = [(1, groups[k], "member",
                 f"u{prng.randrange(int(10e6 * f))}" if prng.random() < 0.8 else f"newuser{len(written)}_{k}",
                 None, None, None) for k in range(n_ins)]
         dele = membership_rows(w.columns, n_del, rng)
         res = wsnap.write(ins, dele)
         t1 = time.perf_counter()
-        sync_ms, rows = ew.sync()
+        if res["applied"]:
+            sync_ms, rows = ew.sync()
+        else:  # the rebuild path (VersionedEngine's fallback): next version + a new engine
+            wsnap = wsnap.apply(ins, dele)
+            ew = check.Engine(wsnap)
+            sync_ms, rows = 0.0, 0
         entry = {"size": size, "applied": res["applied"], "reason": res["reason"],
                  "write_ms": round(res["seconds"] * 1e3, 3), "sync_ms": round(sync_ms, 3),
                  "total_ms": round(res["seconds"] * 1e3 + (time.perf_counter() - t1) * 1e3, 3),
                  "device_rows": rows, "groups_touched": res["groups_touched"], "new_nodes": res["new_nodes"]}
-        if res["applied"]:
+        if True:
             tuples = [InternalRelationTuple("groups", r[1], "member", SubjectID(r[3])) for r in ins]
             got = ew.check_batch(tuples)
             entry["inserted_allowed"] = f"{int(np.sum(got))}/{len(tuples)}"
@@ -129,7 +139,7 @@ def main():
     t0 = time.time()
     cur = compact
     rebuild_s = []
-    for ins, dele in batches:
+    for ins, dele in batches:  # the compact snapshot through the rebuild path
         t1 = time.time()
         cur = cur.apply(ins, dele)
         rebuild_s.append(round(time.time() - t1, 1))
