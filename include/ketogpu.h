@@ -383,6 +383,9 @@ int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
  * (every check entry point also does this first).  ms: host time of the sync (may be NULL);
  * rows: device rows uploaded (may be NULL). */
 int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows);
+/* Test hook: the engine's device rows and edge records compared entry by entry with the
+ * snapshot's host rows (after a sync); mismatches = entries that differ. */
+int ketogpu_engine_check_graph(ketogpu_engine *e, uint64_t *mismatches);
 
 /* ----------------------------------------------- partition-aware loader */
 /* BASELINE config #5 (SURVEY.md 8(e) "Partitioned"): a graph that fits neither one GPU nor

@@ -206,6 +206,7 @@ SIGNATURES = {
     "ketogpu_snapshot_write": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(WriteResult)]),
     "ketogpu_snapshot_version": (C.c_uint64, [vp]),
     "ketogpu_engine_sync": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "ketogpu_engine_check_graph": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "ketogpu_resolve": (C.c_int, [vp, C.POINTER(CheckRequest), C.POINTER(u32), C.POINTER(u32)]),
     "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
     "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),

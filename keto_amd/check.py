@@ -102,6 +102,14 @@ class Engine:
     def upload(self, roots, targets):
         return DeviceQueries(self, roots, targets)
 
+    def check_graph(self):
+        """test hook (ketogpu_engine_check_graph): device rows and records that differ from
+        the snapshot's host rows"""
+        bad = C.c_uint64()
+        L.check(self.L.ketogpu_engine_check_graph(self.h, C.byref(bad)))
+        self.check_graph_first = self.L.ketogpu_last_error().decode("utf-8", "replace") if bad.value else ""
+        return bad.value
+
     def sync(self):
         """upload the device rows an in-place write patched (ketogpu_engine_sync; every
         check call does it first) -> (host ms, rows uploaded)"""

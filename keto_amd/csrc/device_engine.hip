@@ -3414,6 +3414,48 @@ int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows) {
     API_END
 }
 
+int ketogpu_engine_check_graph(ketogpu_engine *e, uint64_t *mismatches) {
+    API_BEGIN
+    if (!e || !mismatches) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_CHECK(hipSetDevice(e->device));
+    e->sync();
+    const Snapshot &s = *e->snap;
+    uint64_t bad = 0;
+    std::string first;
+    auto note = [&](const char *what, size_t k, uint64_t got, uint64_t want) {
+        if (first.empty())
+            first = std::string(what) + " entry " + std::to_string(k) + ": device " + std::to_string(got) + ", host " +
+                    std::to_string(want);
+    };
+    auto cmp_rows = [&](const uint32_t *dcol, const FRec *drec, const std::vector<uint32_t> &col, bool rev) {
+        std::vector<uint32_t> c(col.size());
+        if (!col.empty()) HIP_CHECK(hipMemcpy(c.data(), dcol, col.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < col.size(); k++)
+            if (c[k] != col[k]) bad++, note(rev ? "reverse col" : "forward col", k, c[k], col[k]);
+        if (!drec) return;
+        std::vector<FRec> r(col.size());
+        if (!col.empty()) HIP_CHECK(hipMemcpy(r.data(), drec, col.size() * sizeof(FRec), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < col.size(); k++) {
+            const uint32_t u = col[k];
+            const FRec want = rev ? (u < s.Ni ? FRec{u, ketogpu_engine::ideg(s, u), (uint32_t)s.rev_off[u], 0}
+                                              : FRec{u, 0, 0, 0})
+                                  : FRec{u, ketogpu_engine::fdeg(s, u), (uint32_t)s.fint_off[u], r[k].pad};
+            if (r[k].node != want.node || r[k].deg != want.deg || r[k].begin != want.begin) {
+                bad++;
+                note(rev ? "reverse record (node<<32|deg)" : "forward record (node<<32|deg)", k,
+                     (uint64_t)r[k].node << 32 | r[k].deg, (uint64_t)want.node << 32 | want.deg);
+            }
+        }
+    };
+    cmp_rows(e->g.fint_col, e->frec, s.fint_col, false);
+    cmp_rows(e->g.rev_col, e->brec, s.rev_col, true);
+    *mismatches = bad;
+    set_last_error(first);
+    API_END
+}
+
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out) {
     if (!e || !out) {
         set_last_error("null argument");

@@ -116,6 +116,7 @@ struct TupleRow {
 struct Group {
     int32_t ns;
     uint32_t obj, rel;       // StrPool ids
+    uint32_t cap;            // writable snapshots: slots reserved at begin / the row_col copy (0: valid)
     uint64_t begin;          // into Snapshot::group_col (valid prefix only)
     uint32_t valid;          // rows before the first bad row
     uint32_t full_len;       // all rows of the group

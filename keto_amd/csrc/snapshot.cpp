@@ -214,7 +214,7 @@ struct ketogpu_builder {
                         "rows are not in ORDER BY order: group (namespace_id, object, relation) "
                         "appears twice (use KETOGPU_BUILD_SORT)");
         seen_groups.get_or_insert(ns, obj, rel, (uint32_t)s->groups.size());
-        cur = Group{ns, obj, rel, s->group_col.size(), 0, 0, -1, 0};
+        cur = Group{ns, obj, rel, 0, s->group_col.size(), 0, 0, -1, 0};
         open = true;
     }
     // one row, already grouped

@@ -333,10 +333,20 @@ struct Writer {
             if (!op.del.empty()) {
                 std::vector<uint32_t> &dl = op.del;
                 std::sort(dl.begin(), dl.end());
+                dl.erase(std::unique(dl.begin(), dl.end()), dl.end());
                 const size_t before = out.size();
-                out.erase(std::remove_if(out.begin(), out.end(),
-                                         [&dl](uint32_t s) { return std::binary_search(dl.begin(), dl.end(), s); }),
-                          out.end());
+                if (dl.size() <= 8)  // a few deleted subjects: compare each row with all of them
+                    out.erase(std::remove_if(out.begin(), out.end(),
+                                             [&dl](uint32_t s) {
+                                                 bool hit = false;
+                                                 for (uint32_t d : dl) hit |= s == d;
+                                                 return hit;
+                                             }),
+                              out.end());
+                else
+                    out.erase(std::remove_if(out.begin(), out.end(),
+                                             [&dl](uint32_t s) { return std::binary_search(dl.begin(), dl.end(), s); }),
+                              out.end());
                 n_del += before - out.size();
             }
             new_rows.push_back({gi, std::move(out)});
@@ -345,10 +355,11 @@ struct Writer {
 
     // grown groups are copied to the end of the row arrays; once the stale copies would
     // outweigh the live rows, the batch goes to the rebuild (which compacts)
+    static uint32_t room(const Group &g) { return std::max(g.valid, g.cap); }
     void budget() const {
         uint64_t grow = 0;
         for (const auto &[gi, rows] : new_rows)
-            if (rows.size() > S.groups[gi].valid) grow += S.groups[gi].valid;
+            if (rows.size() > room(S.groups[gi])) grow += room(S.groups[gi]);
         if (S.row_garbage + grow > std::max<uint64_t>(S.stats.num_edges, 1u << 20)) throw Refuse{KETOGPU_WRITE_FULL};
     }
 
@@ -358,32 +369,32 @@ struct Writer {
     };
     std::map<uint32_t, RowEdit> fwd, rev;  // fint(g) edits, rev(s) edits
 
-    // edges that appear or disappear: only the batch's subjects can change, so one pass over
-    // the old rows marks which of them were present
+    // edges that appear or disappear: only the batch's subjects can change.  Edge g -> s
+    // existed iff g is in the (sorted) reverse row of s; afterwards it exists iff s was
+    // inserted or was there, and was not deleted (a delete removes every duplicate)
     void diff() {
         for (auto &[gi, rows] : new_rows) {
             const Group &g = S.groups[gi];
             const uint32_t v = S.set_node.get(g.ns, g.obj, g.rel);
             const GroupOps &op = ops[gi];
-            std::vector<uint32_t> cand;
-            for (const auto &x : op.ins) cand.push_back(x.second);
+            std::vector<uint32_t> ins_s, cand;
+            for (const auto &x : op.ins) ins_s.push_back(x.second);
+            std::sort(ins_s.begin(), ins_s.end());
+            cand = ins_s;
             cand.insert(cand.end(), op.del.begin(), op.del.end());
             std::sort(cand.begin(), cand.end());
             cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-            std::vector<uint8_t> before(cand.size(), 0), after(cand.size(), 0);
-            auto mark = [&](const uint32_t *p, size_t n, std::vector<uint8_t> &m) {
-                for (size_t i = 0; i < n; i++) {
-                    auto it = std::lower_bound(cand.begin(), cand.end(), p[i]);
-                    if (it != cand.end() && *it == p[i]) m[it - cand.begin()] = 1;
+            for (uint32_t s : cand) {
+                bool before = false;
+                if (!(s & kNew)) {
+                    const uint32_t *b = S.rev_col.data() + S.rev_off[s], *e = S.rev_col.data() + S.rev_off[s + 1];
+                    before = std::binary_search(b, e, v);
                 }
-            };
-            mark(S.group_col.data() + g.begin, g.valid, before);
-            mark(rows.data(), rows.size(), after);
-            for (size_t k = 0; k < cand.size(); k++) {
-                if (before[k] == after[k]) continue;
-                const uint32_t s = cand[k];
+                const bool deleted = std::binary_search(op.del.begin(), op.del.end(), s);  // sorted in merge()
+                const bool after = !deleted && (before || std::binary_search(ins_s.begin(), ins_s.end(), s));
+                if (before == after) continue;
                 const bool interior = !(s & kNew) && s < S.Ni;
-                if (after[k]) {
+                if (after) {
                     if (interior) fwd[v].add.push_back(s);
                     rev[s].add.push_back(v);
                 } else {
@@ -501,12 +512,14 @@ struct Writer {
             edges_minus += g.valid;
             edges_delta += rows.size();
             RowRef rr = S.node_row[v];
-            if (rows.size() > g.valid) {  // grown: a new copy at the end (the old one is garbage)
-                S.row_garbage += g.valid;
+            if (rows.size() > room(g)) {  // outgrown: a new copy with a quarter free at the end
+                S.row_garbage += room(g);
+                const uint64_t cap = rows.size() + rows.size() / 4 + 4;
+                g.cap = (uint32_t)std::min<uint64_t>(cap, 0xffffffffu);
                 g.begin = S.group_col.size();
                 rr.off = S.row_col.size();
-                S.group_col.resize(S.group_col.size() + rows.size());
-                S.row_col.resize(S.row_col.size() + rows.size());
+                S.group_col.resize(S.group_col.size() + g.cap);
+                S.row_col.resize(S.row_col.size() + g.cap);
             }
             for (size_t k = 0; k < rows.size(); k++) S.group_col[g.begin + k] = S.row_col[rr.off + k] = id(rows[k]);
             rr.len = rr.full_len = (uint32_t)rows.size();
@@ -516,14 +529,14 @@ struct Writer {
         }
         // Edge records carry the real entry counts of the rows they point at (the free slots
         // are never read through a record): rows holding a record for a node whose count
-        // changed are re-uploaded too — fint(p) for each interior predecessor p of a node
-        // whose interior successors changed, rev(x) for each successor x of an interior node
-        // whose interior predecessors changed
-        for (uint32_t v : fcount_changed) {
-            const uint64_t b = S.rev_off[v];
-            const uint32_t n = real(S.rev_col, b, S.rev_off[v + 1], S.Dbi);
-            for (uint32_t k = 0; k < n; k++) S.patches.push_back({0, S.rev_col[b + k]}), res.device_rows++;
-        }
+        // changed are re-uploaded too — fint(p) for each (expandable) predecessor p of an
+        // interior node whose interior successors changed, rev(x) for each successor x of an
+        // interior node whose interior predecessors changed
+        for (uint32_t v : fcount_changed)  // every expandable predecessor (fint rows of all of them)
+            for (uint64_t k = S.rev_off[v]; k < S.rev_off[v + 1]; k++) {
+                const uint32_t p = S.rev_col[k];
+                if (p != S.Dbi && p != S.Dbo) S.patches.push_back({0, p}), res.device_rows++;
+            }
         for (uint32_t u : icount_changed) {
             const RowRef &r = S.node_row[u];
             std::vector<uint32_t> xs(S.row_col.begin() + r.off, S.row_col.begin() + r.off + r.len);

@@ -233,10 +233,20 @@ def test_versioned_engine_writes_in_place_and_reads_them():
         ve.transact(insert=[_tuple(r, id2name) for r in ins], delete=[_tuple(d, id2name) for d in dele])
         paths.append(ve.last_write["path"])
         cur = _expected(cur, ins, dele)
+        eng = ve._state[1]
+        assert eng.check_graph() == 0, (step, paths, eng.check_graph_first, eng.last_stats()["plan"])
         reqs = randgraph.make_requests(500 + step, namespaces, cur, n=500, wildcard=False)
         want = randgraph.oracle_store(namespaces, cur).check_batch(reqs)
         tuples = [rt.InternalRelationTuple(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs]
-        assert ve.check_many(tuples) == [bool(x) for x in want], step
+        got = ve.check_many(tuples)
+        if got != [bool(x) for x in want]:  # diagnose: a fresh writable / compact engine on the same rows
+            from keto_amd import check
+            fresh_w = check.Engine(Snapshot.from_rows(namespaces, cur, sort=True, writable=True)).check_many(tuples)
+            fresh_c = check.Engine(Snapshot.from_rows(namespaces, cur, sort=True)).check_many(tuples)
+            bad = [i for i in range(len(want)) if got[i] != bool(want[i])]
+            pytest.fail(f"step {step} paths {paths}: {len(bad)} mismatches (e.g. {[reqs[i] for i in bad[:3]]}); "
+                        f"fresh writable engine {sum(a != bool(b) for a, b in zip(fresh_w, want))}, "
+                        f"fresh compact engine {sum(a != bool(b) for a, b in zip(fresh_c, want))}")
         assert list(ve._state[1].check_batch(tuples)) == [bool(x) for x in want], step  # the id path
         orc = randgraph.oracle_store(namespaces, cur)
         known = {n for n, _ in namespaces}
