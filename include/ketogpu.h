@@ -66,7 +66,7 @@ extern "C" {
  * (KETOGPU_BUILD_SORT) and ketogpu_snapshot_apply; rows appended in order are kept. */
 #define KETOGPU_ORDER_NULLS_LAST 2u /* Postgres ORDER BY (NULLS LAST, C collation) */
 /* Writable snapshot (ketogpu_snapshot_write): the device rows are laid out with free slots
- * (about 1/8 of each row, at least one per row part) and ids are reserved for new subjects,
+ * (2 + 1/8 of each row part) and ids are reserved for new subjects,
  * so a write batch patches the rows it touches in place instead of rebuilding the graph. */
 #define KETOGPU_BUILD_WRITABLE 4u
 

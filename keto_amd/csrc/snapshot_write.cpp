@@ -29,14 +29,14 @@ namespace {
 
 constexpr uint32_t kReservedRowSlots = 4;  // reverse-row capacity of a reserved (new) node
 
-inline uint64_t free_slots(uint64_t deg) { return 1 + deg / 8; }
+inline uint64_t free_slots(uint64_t deg) { return 2 + deg / 8; }
 
 }  // namespace
 
 // Lay out the compact device rows with free slots (KETOGPU_BUILD_WRITABLE):
-//   fint(v), v < Nx:   real interior successors | Df x (1 + d/8)
-//   rev(u), u < Ni:    real interior preds | Dbi x (1 + di/8) | other preds | Dbo x (1 + do/8)
-//   rev(u), u >= Ni:   real preds | Dbo x (1 + d/8)
+//   fint(v), v < Nx:   real interior successors | Df x (2 + d/8)
+//   rev(u), u < Ni:    real interior preds | Dbi x (2 + di/8) | other preds | Dbo x (2 + do/8)
+//   rev(u), u >= Ni:   real preds | Dbo x (2 + d/8)
 //   rev(u), N <= u < n_cap (reserved ids): Dbo x 4
 // Only the interior prefix of an interior node's reverse row is read through records
 // (its length is the record's `deg`), so only those rows need two free regions.
