@@ -243,6 +243,27 @@ def test_partition_device_single_rank(seed, direction):
 
 
 @pytest.mark.gpu
+def test_partition_device_rejects_ids_outside_the_snapshot():
+    """an id outside the snapshot fails the round with KETOGPU_EINVAL (validated by the
+    seed kernel), and the engine answers the next valid batch"""
+    from keto_amd.partition import PartitionedEngine
+    if L.lib().ketogpu_device_count() < 1:
+        pytest.fail("no HIP device visible")
+    namespaces, rows, reqs = _case(73, n_rows=800, n_req=500)
+    sh = _load(namespaces, rows)
+    want = _want(namespaces, rows, reqs)
+    roots, targets, status = sh.resolve_batch(persistence.request_columns(reqs))
+    eng = PartitionedEngine(sh, device=0, direction="backward")
+    for bad_r, bad_t in ((1 << 30, 0), (0, 1 << 30)):
+        r, t = roots.copy(), targets.copy()
+        r[7], t[7] = (bad_r, t[7]) if bad_r else (r[7], bad_t)
+        with pytest.raises(L.KetoError) as e:
+            eng.check_ids(r, t)
+        assert e.value.code == L.EINVAL
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+
+
+@pytest.mark.gpu
 def test_partition_device_rbac_matches_oracle():
     from keto_amd import check, synth
     from keto_amd.partition import PartitionedEngine, Shard
