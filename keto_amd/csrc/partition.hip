@@ -702,10 +702,11 @@ struct ketogpu_part {
             return overflow_bits() & 4u ? KETOGPU_EINVAL : KETOGPU_ENOMEM;
         }
         if (n && world == 1) {  // one destination: the records are already grouped
+            // no copy: the caller hands `send` straight back to apply (its own records),
+            // which then reads them where the kernels wrote them (obuf_send, apply)
             counts[0] = n;
-            timed(KETOGPU_PART_K_PACK, 32 * n, [&] {
-                PHIP(hipMemcpyAsync(send, P.obuf, n * sizeof(ketogpu_record), hipMemcpyDeviceToDevice, stream));
-            });
+            obuf_send = send;
+            obuf_n = n;
         } else if (n) {
             PHIP(hipMemsetAsync(d_counts, 0, world * sizeof(unsigned long long), stream));
             unsigned grid = (unsigned)std::min<uint64_t>(pblocks(n), 2048);
@@ -735,7 +736,19 @@ struct ketogpu_part {
         return KETOGPU_OK;
     }
 
+    // world 1: the records of the last emit, left in obuf (pack); applying the caller's
+    // `send` buffer then means applying obuf.  obuf is rewritten only by the next seed /
+    // expand / pull_emit, all after this apply on the same stream.
+    const ketogpu_record *obuf_send = nullptr;
+    uint64_t obuf_n = 0;
+    const ketogpu_record *incoming(const ketogpu_record *recv, uint64_t n) {
+        const ketogpu_record *r = (world == 1 && recv && recv == obuf_send && n == obuf_n) ? P.obuf : recv;
+        obuf_send = nullptr;
+        return r;
+    }
+
     int apply(const ketogpu_record *recv, uint64_t n, uint64_t *frontier) {
+        recv = incoming(recv, n);
         const int nxt = cur ^ 1;
         PHIP(hipMemsetAsync(&P.ctr[nxt], 0, sizeof(unsigned long long), stream));
         const uint64_t base = lb + cnt;
@@ -787,6 +800,7 @@ struct ketogpu_part {
     }
 
     int pull_answer(const ketogpu_record *recv, uint64_t n) {
+        recv = incoming(recv, n);
         if (n)
             timed(KETOGPU_PART_K_PULL_ANSWER, 24 * n,
                   [&] { KLAUNCH(part_pull_answer_kernel, dim3(pblocks(n)), dim3(kPB), 0, stream, P, recv, n); });
