@@ -1688,8 +1688,12 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const uint64_t *allowed, c
 }
 
 // sum the spread statistics slots of `regions` regions into out[3 * region + k]
+// mirror (host-mapped pinned memory, may be null): out[0, mirror_words) is also written
+// there, so the host reads the statistics and the spill counters after its one
+// synchronization without a separate copy
 __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned long long *slots, int regions,
-                                                              unsigned long long *out) {
+                                                              unsigned long long *out, unsigned long long *mirror,
+                                                              int mirror_words) {
     __shared__ unsigned long long part[kBlock / 64][3];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int r = 0; r < regions; r++) {
@@ -1708,6 +1712,8 @@ __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned lon
         }
         __syncthreads();
     }
+    __threadfence_block();
+    if (mirror && (int)threadIdx.x < mirror_words) mirror[threadIdx.x] = out[threadIdx.x];
 }
 
 // ------------------------------------------------- wave-synchronous units
@@ -2079,6 +2085,7 @@ struct ketogpu_engine {
     const uint32_t *has_kids = nullptr;  // bitmap over Ni: interior node with interior successors
     uint64_t Wmax = 0;
     uint64_t *h_ctr = nullptr;  // pinned
+    unsigned long long *d_hctr = nullptr;  // its device view (kernels write results there)
     std::vector<void *> owned;
     ketogpu_run_stats last{};
     std::vector<hipEvent_t> ev_pool;
@@ -2160,28 +2167,40 @@ struct ketogpu_engine {
     // KETOGPU_CASCADE; w -> q -> s measured best on configs #2-#4 (profiles/r01/tune_cascades.txt)
     std::vector<SpillStage> cascade{{16, 'w'}, {4, 'q'}, {1, 's'}};
 
+    // Spill stages are persistent (grid-stride over the previous stage's spilled units, a
+    // count only the device knows when they launch).  Their grid follows the units the
+    // stage had in the previous run (x2, at least 32 workgroups, at most the stage's full
+    // grid): an empty stage of 1024 workgroups still cost ~18 us per call on config #2,
+    // where one unit in 60k spills; a grid that is too small for one run only slows it.
+    uint64_t stage_prev[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+    static unsigned stage_grid(uint64_t prev, unsigned full) {
+        if (prev >= full) return full;
+        unsigned g = 32;
+        while (g < full && g < 2 * prev) g <<= 1;
+        return std::min(g, full);
+    }
     void launch_stage(const SpillStage &sg, const Batch &q, const uint32_t *in, const unsigned int *in_count,
-                      uint32_t fan, uint32_t *out, unsigned int *out_count, unsigned long long *stats) {
+                      uint32_t fan, uint32_t *out, unsigned int *out_count, unsigned long long *stats, uint64_t prev) {
         switch (sg.kind) {
         case 'w':
-            KLAUNCH((bidi_kernel<16, 11, 384, 256, 6>), dim3(1024), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            KLAUNCH((bidi_kernel<16, 11, 384, 256, 6>), dim3(stage_grid(prev, 1024)), dim3(256), 0, stream, g, frec,
+                    brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'q':
-            KLAUNCH((bidi_kernel<4, 12, 512, 256, 7>), dim3(512), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            KLAUNCH((bidi_kernel<4, 12, 512, 256, 7>), dim3(stage_grid(prev, 512)), dim3(256), 0, stream, g, frec,
+                    brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'h':
-            KLAUNCH((bidi_kernel<16, 10, 256, 64, 6>), dim3(2048), dim3(64), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            KLAUNCH((bidi_kernel<16, 10, 256, 64, 6>), dim3(stage_grid(prev, 2048)), dim3(64), 0, stream, g, frec,
+                    brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         case 'r':
-            KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(1280), dim3(64), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(stage_grid(prev, 1280)), dim3(64), 0, stream, g, frec,
+                    brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         default:
-            KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(256), dim3(256), 0, stream, g, frec, brec, q.roots,
-                    q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(stage_grid(prev, 256)), dim3(256), 0, stream, g, frec,
+                    brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
         }
     }
@@ -2479,6 +2498,7 @@ struct ketogpu_engine {
         spill_count = (unsigned int *)(st.stats + 8 + 8 * kStatSlots + 8);
         for (void *p : {(void *)st.ctr, (void *)st.overflow, (void *)st.stats}) owned.push_back(p);  // spill_count lives in st.stats
         HIP_CHECK(hipHostMalloc((void **)&h_ctr, 64 * sizeof(uint64_t), hipHostMallocDefault));
+        HIP_CHECK(hipHostGetDevicePointer((void **)&d_hctr, h_ctr, 0));
         d_bad = dalloc<unsigned long long>(1);
         owned.push_back(d_bad);
         HIP_CHECK(hipStreamSynchronize(stream));
@@ -2596,7 +2616,7 @@ struct ketogpu_engine {
 
     // sum the spread unit-statistics slots of both regions (rows, edges, reverse entries)
     void read_unit_stats(uint64_t out[3]) {
-        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
+        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), nullptr, 0);
         HIP_CHECK(hipMemcpyAsync(h_ctr + 32, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
         for (int k = 0; k < 3; k++) out[k] = h_ctr[32 + k] + h_ctr[35 + k];
@@ -2624,21 +2644,23 @@ struct ketogpu_engine {
         for (const SpillStage &sg : cascade)
             if (sg.u <= (stages.empty() ? bidi_cfg.u : stages.back().u)) stages.push_back(sg);
         int cur = 0, u_prev = bidi_cfg.u;
+        std::vector<uint32_t> fans;
         for (size_t k = 0; k < stages.size(); k++) {
             const SpillStage sg = stages[k];
-            launch_stage(sg, q, list[cur], &spill_count[k], (uint32_t)(u_prev / sg.u), list[cur ^ 1],
-                         &spill_count[k + 1], st.stats + 4 * kStatSlots);
+            fans.push_back((uint32_t)(u_prev / sg.u));
+            launch_stage(sg, q, list[cur], &spill_count[k], fans.back(), list[cur ^ 1], &spill_count[k + 1],
+                         st.stats + 4 * kStatSlots, k < 8 ? stage_prev[k] : ~0ull);
             cur ^= 1;
             u_prev = sg.u;
         }
         HIP_CHECK(hipEventRecord(d, stream));
         const size_t ns = stages.size() + 1;
-        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out());
         // the spill counters sit 8 words after the reduced statistics (st.stats
-        // layout, kStatsLen): one copy brings both to h_ctr[16..21] and h_ctr + 24
+        // layout, kStatsLen): the reduction mirrors both into h_ctr[16..21] and h_ctr + 24
+        // (host-mapped: no copy launch between it and the sync)
         static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
         // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
-        HIP_CHECK(hipMemcpyAsync(h_ctr + 16, stat_out(), 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16, 12);
         if (before_sync) before_sync();
         HIP_CHECK(hipStreamSynchronize(stream));
         unit_end = d;
@@ -2653,6 +2675,7 @@ struct ketogpu_engine {
             fprintf(stderr, "\n");
         }
         for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
+        for (size_t k = 0; k < stages.size() && k < 8; k++) stage_prev[k] = (uint64_t)cnt[k] * fans[k];
         rs.push_launches += ns;
         rs.unit_launches += ns;
         const uint64_t left = cnt[ns - 1];
@@ -2738,19 +2761,22 @@ struct ketogpu_engine {
                     for (uint64_t c0 = 0, k = 0; c0 < q.n; c0 += chunk, k++, chunk = pipe_chunk) {
                         const uint64_t m = std::min<uint64_t>(chunk, q.n - c0);
                         hipStream_t cs = (k & 1) ? stream2 : stream;
+                        // the first chunk loads on the stream that traverses it (no cross-stream
+                        // event ahead of the first launch: ~18 us idle); the others on the
+                        // copy stream, overlapping the traversal of the chunks before them
+                        hipStream_t ls = k ? copy_stream : cs;
                         if (src->mapped) {
                             KLAUNCH(load_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(m), 256)), dim3(kBlock), 0,
-                                    copy_stream, src->roots, src->targets, c0, m, io->d_roots, io->d_targets, g.Nx, g.N,
-                                    d_bad);
+                                    ls, src->roots, src->targets, c0, m, io->d_roots, io->d_targets, g.Nx, g.N, d_bad);
                         } else {
-                            HIP_CHECK(hipMemcpyAsync(io->d_roots + c0, src->roots + c0, m * 4, hipMemcpyDefault,
-                                                     copy_stream));
-                            HIP_CHECK(hipMemcpyAsync(io->d_targets + c0, src->targets + c0, m * 4, hipMemcpyDefault,
-                                                     copy_stream));
+                            HIP_CHECK(hipMemcpyAsync(io->d_roots + c0, src->roots + c0, m * 4, hipMemcpyDefault, ls));
+                            HIP_CHECK(hipMemcpyAsync(io->d_targets + c0, src->targets + c0, m * 4, hipMemcpyDefault, ls));
                         }
-                        hipEvent_t h = ev();
-                        HIP_CHECK(hipEventRecord(h, copy_stream));
-                        HIP_CHECK(hipStreamWaitEvent(cs, h, 0));
+                        if (k) {
+                            hipEvent_t h = ev();
+                            HIP_CHECK(hipEventRecord(h, copy_stream));
+                            HIP_CHECK(hipStreamWaitEvent(cs, h, 0));
+                        }
                         if (!src->mapped)
                             KLAUNCH(validate_kernel, dim3(blocks_for(m)), dim3(kBlock), 0, cs, io->d_roots + c0,
                                     io->d_targets + c0, m, g.Nx, g.N, c0, d_bad);
