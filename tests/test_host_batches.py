@@ -124,6 +124,33 @@ def test_pipelined_call_with_global_path_spills(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_spill_stage_grids_follow_the_previous_run(monkeypatch):
+    """spill stages size their persistent grids from the previous run's spills: a run with
+    no spills (smallest grids) followed by one where most units spill must still answer
+    every request (the grids only change speed)"""
+    _gpu()
+    monkeypatch.setenv("KETOGPU_UNITS", "bidi")
+    n = 3000  # chains of 3000 subject sets outgrow the 512-slot first-stage tables
+    rows = [(1, f"g{i}", "m", None, 1, f"g{i + 1}", "m") for i in range(n)]
+    rows.append((1, f"g{n}", "m", "alice", None, None, None))
+    rows += [(1, f"s{i}", "m", f"u{i}", None, None, None) for i in range(2000)]
+    snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
+    eng = check.Engine(snap)
+    easy = [("n", f"s{i}", "m", rt.SubjectID(f"u{(i * 7) % 2000}")) for i in range(2000)]
+    r, t = snap.resolve_many(easy)
+    for _ in range(3):
+        np.testing.assert_array_equal(eng.check_ids(r, t), [(i * 7) % 2000 == i for i in range(2000)])
+    assert eng.last_stats()["spilled_units"] == 0
+    rng = np.random.default_rng(5)
+    pos = rng.integers(0, n + 1, size=8000)
+    who = rng.integers(0, 2, size=8000)
+    hard = [("n", f"g{i}", "m", rt.SubjectID("alice" if k == 0 else "u3")) for i, k in zip(pos, who)]
+    r, t = snap.resolve_many(hard)
+    np.testing.assert_array_equal(eng.check_ids(r, t), who == 0)
+    assert eng.last_stats()["spilled_units"] > 100
+
+
+@pytest.mark.gpu
 def test_multi_engine_matches_oracle(rbac):
     """every visible device (at least the box's one), and the same device count split into
     ranges whose boundaries fall inside 16-request units of the other split"""
