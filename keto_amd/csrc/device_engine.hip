@@ -37,6 +37,7 @@
 #include <chrono>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -2075,6 +2076,14 @@ struct ketogpu_queries {
     }
 };
 
+// pinned buffers handed out by ketogpu_host_alloc: base -> (bytes, device view)
+struct PinnedRange {
+    size_t bytes;
+    uintptr_t dev;
+};
+static std::mutex g_pinned_mu;
+static std::map<uintptr_t, PinnedRange> g_pinned;
+
 struct ketogpu_engine {
     const Snapshot *snap = nullptr;
     int device = 0;
@@ -3133,6 +3142,15 @@ struct ketogpu_engine {
     // (pageable memory goes through DMA copies).
     const uint32_t *device_view(const uint32_t *p) {
         if (!p) return nullptr;
+        {  // buffers of ketogpu_host_alloc: known without a runtime query (~10 us per call)
+            std::lock_guard<std::mutex> lk(g_pinned_mu);
+            auto it = g_pinned.upper_bound((uintptr_t)p);
+            if (it != g_pinned.begin()) {
+                --it;
+                const uintptr_t off = (uintptr_t)p - it->first;
+                if (off < it->second.bytes && it->second.dev) return (const uint32_t *)(it->second.dev + off);
+            }
+        }
         hipPointerAttribute_t at{};
         const hipError_t e = hipPointerGetAttributes(&at, p);
         static const bool dbg = getenv("KETOGPU_DEBUG_PTR") != nullptr;
@@ -3191,7 +3209,10 @@ struct ketogpu_engine {
             }
             run(q);
         } else {
-            const uint32_t *dr = device_view(roots), *dt = dr ? device_view(targets) : nullptr;
+            // KETOGPU_PIPE_DMA=1: pinned requests are copied by DMA per chunk (copy engines)
+            // instead of read in place by load_kernel (CUs); an A/B knob
+            static const bool dma = getenv("KETOGPU_PIPE_DMA") != nullptr;
+            const uint32_t *dr = dma ? nullptr : device_view(roots), *dt = dr ? device_view(targets) : nullptr;
             const HostSrc src{dr && dt ? dr : roots, dr && dt ? dt : targets, dr && dt};
             ensure_res(2 * words + 1);
             run_once(q, &src, [&] {  // results, flags and the validation verdict in one launch
@@ -3334,12 +3355,25 @@ int ketogpu_host_alloc(size_t bytes, void **out) {
     API_BEGIN
     if (!out) throw Error(KETOGPU_EINVAL, "null argument");
     *out = nullptr;
-    HIP_CHECK(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    const size_t n = std::max<size_t>(bytes, 1);
+    HIP_CHECK(hipHostMalloc(out, n, hipHostMallocDefault));
+    void *dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, *out, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_pinned_mu);
+    g_pinned[(uintptr_t)*out] = PinnedRange{n, (uintptr_t)dev};
     API_END
 }
 
 void ketogpu_host_free(void *p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned.erase((uintptr_t)p);
+    }
+    (void)hipHostFree(p);
 }
 
 int ketogpu_check(ketogpu_engine *e, const ketogpu_check_request *reqs, size_t n, uint8_t *allowed, int32_t *status) {
