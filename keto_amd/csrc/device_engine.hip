@@ -1031,6 +1031,9 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // is backward-visited only as t or as an entry of t's own reverse row; so once the other
 // side's seed row has been read (in an earlier level: its inserts are complete), a push
 // of such a node only looks it up.  Leaf groups (only subject-ID members) take no slot.
+#ifndef KETO_PACK
+#define KETO_PACK 0
+#endif
 constexpr uint32_t kBothMax = 12;      // both sides expand while both pending sums are <= this
 constexpr uint32_t kSeedBothMax = 32;  // seeds pushed eagerly when both seed rows are <= this
 
@@ -1044,10 +1047,18 @@ struct BidiShared {
     static constexpr int EM = BT > 2 * U ? BT : 2 * U;
     alignas(16) uint32_t key[H];
     alignas(16) unsigned long long st[H];
+#if KETO_PACK
+    // pending lists (ping-pong): slot | dir << 15 | deg << 16 (a row of more than 65535
+    // entries spills the unit), and the row's first record; the eager seed rows of the
+    // first expansion use list 1 (empty until the first level appends to it)
+    uint32_t p_sdd[2][F];
+    uint32_t p_begin[2][F];
+#else
     uint16_t p_sd[2][F];  // pending lists (ping-pong): slot | dir << 15
     uint32_t p_begin[2][F], p_deg[2][F];
     uint16_t e_sd[2 * U];  // eager seed rows: forward of r_j, backward of t_j
     uint32_t e_begin[2 * U], e_deg[2 * U];
+#endif
     uint16_t e_mask[EM];   // request bits of the entries being expanded
     uint32_t c_pre[BT + 1];
     uint32_t wave_sum[BT / 64];
@@ -1213,6 +1224,14 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
     cost_update<BT>(S, pend, d, deg, false);
     uint32_t idx = lds_append(app, &S.n_p[nxt]);
     if (app) {
+#if KETO_PACK
+        if (idx < (uint32_t)F && deg <= 0xFFFFu) {
+            S.p_sdd[nxt][idx] = (uint32_t)h | ((uint32_t)d << 15) | (deg << 16);
+            S.p_begin[nxt][idx] = begin;
+        } else {
+            S.spill = 1;
+        }
+#else
         if (idx < (uint32_t)F) {
             S.p_sd[nxt][idx] = (uint16_t)(h | (d << 15));
             S.p_begin[nxt][idx] = begin;
@@ -1220,6 +1239,7 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
         } else {
             S.spill = 1;
         }
+#endif
     }
 }
 
@@ -1238,10 +1258,10 @@ __device__ __forceinline__ void bidi_source_meet(BidiShared<U, HLOG, F, BT, LF> 
 // first position in it — positions are distinct — and a prefix maximum fills the gaps;
 // positions a chunk does not write hold owners of earlier edges, never larger), and the
 // record loads software-pipelined one chunk ahead of the pushes.
-template <int U, int HLOG, int F, int BT, int LF>
+template <int U, int HLOG, int F, int BT, int LF, class SDT>
 __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *frec, const FRec *brec,
                                               BidiShared<U, HLOG, F, BT, LF> &S, const BidiLevel &L, uint32_t my_deg,
-                                              const uint16_t *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
+                                              const SDT *sd, const uint32_t *begin, int nxt, uint64_t &edges) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
@@ -1265,7 +1285,7 @@ __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *fre
             const int o = wave_incl_max_i32((int)S.c_pre[lane]);
             x.lo = (uint32_t)(o < 0 ? 0 : o);
             x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
-            x.d = sd[x.lo] >> 15;
+            x.d = (int)((uint32_t)(sd[x.lo] >> 15) & 1u);
             e = min(eb + lane, total - 1);  // lanes past the end re-read the last edge
         } else {
             x.lo = prev.lo;
@@ -1307,13 +1327,13 @@ __device__ __forceinline__ void bidi_expand64(const DevGraph &g, const FRec *fre
 
 // Expand k entries (entry j: sd[j], begin[j], S.e_mask[j]); `my_deg` is the degree this
 // thread contributes for entry threadIdx.x (0 when it has none).  Block-uniform loop.
-template <int U, int HLOG, int F, int BT, int LF>
+template <int U, int HLOG, int F, int BT, int LF, class SDT>
 __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec, const FRec *brec,
                                             BidiShared<U, HLOG, F, BT, LF> &S, const BidiLevel &L, uint32_t my_deg,
-                                            uint32_t k, const uint16_t *sd, const uint32_t *begin, int nxt,
+                                            uint32_t k, const SDT *sd, const uint32_t *begin, int nxt,
                                             uint64_t &edges) {
     if constexpr (BT == 64) {
-        bidi_expand64<U, HLOG, F, BT, LF>(g, frec, brec, S, L, my_deg, sd, begin, nxt, edges);
+        bidi_expand64<U, HLOG, F, BT, LF, SDT>(g, frec, brec, S, L, my_deg, sd, begin, nxt, edges);
         return;
     }
     const uint32_t total = block_scan_sh<BT>(my_deg, S);
@@ -1331,7 +1351,7 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
                 else
                     hi = mid;
             }
-            d = sd[lo] >> 15;
+            d = (int)((uint32_t)(sd[lo] >> 15) & 1u);
             m = S.e_mask[lo] & L.active & ~S.found;
             FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
             u = rc.node;
@@ -1450,27 +1470,45 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             }
             uint32_t idx = lds_append(app, &S.n_p[0]);
             if (app) {  // idx < 2U <= F
+#if KETO_PACK
+                if (deg > 0xFFFFu) S.spill = 1;  // a seed row longer than the packed degree
+                S.p_sdd[0][idx] = (uint32_t)h | ((uint32_t)side << 15) | (deg << 16);
+                S.p_begin[0][idx] = (uint32_t)(side ? rb : fb);
+#else
                 S.p_sd[0][idx] = (uint16_t)(h | (side << 15));
                 S.p_begin[0][idx] = (uint32_t)(side ? rb : fb);
                 S.p_deg[0][idx] = deg;
+#endif
             }
         }
         if (tid < U) {  // eager rows (zero degree when not eager or not active)
             const bool e = v && eager;
+#if KETO_PACK
+            S.p_sdd[1][tid] = (e ? rdeg : 0u) << 16;  // eager degrees <= seed_max (< 65536)
+            S.p_begin[1][tid] = (uint32_t)fb;
+            S.p_sdd[1][U + tid] = (1u << 15) | ((e ? tdeg : 0u) << 16);
+            S.p_begin[1][U + tid] = (uint32_t)rb;
+#else
             S.e_sd[tid] = 0;
             S.e_begin[tid] = (uint32_t)fb;
             S.e_deg[tid] = e ? rdeg : 0;
             S.e_sd[U + tid] = (uint16_t)(1u << 15);
             S.e_begin[U + tid] = (uint32_t)rb;
             S.e_deg[U + tid] = e ? tdeg : 0;
+#endif
         }
         if (tid < 2 * U) S.e_mask[tid] = (uint16_t)(1u << (tid % U));
     }
     __syncthreads();
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
     BidiLevel L{S.active, {0, 0}, {0, 0}, {0, 0}};  // the seed rows: every push inserts
+#if KETO_PACK
+    bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, (uint32_t)tid < 2 * U ? S.p_sdd[1][tid] >> 16 : 0, 2 * U,
+                                    S.p_sdd[1], S.p_begin[1], 0, edges);
+#else
     bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, (uint32_t)tid < 2 * U ? S.e_deg[tid] : 0, 2 * U, S.e_sd,
                                     S.e_begin, 0, edges);
+#endif
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     int cur = 0;
     bool spilled = false;
@@ -1536,8 +1574,14 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const uint32_t i = base + tid;
             uint32_t take = 0, rest = 0, sd = 0, dg = 0, bg = 0, clr = 0;
             if ((uint32_t)tid < k) {
+#if KETO_PACK
+                const uint32_t w = S.p_sdd[cur][i];
+                sd = w & 0xFFFFu;
+                dg = w >> 16;
+#else
                 sd = S.p_sd[cur][i];
                 dg = S.p_deg[cur][i];
+#endif
                 bg = S.p_begin[cur][i];
                 const uint32_t d = sd >> 15, s = sd & 0x7FFFu;
                 const uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
@@ -1551,15 +1595,24 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const uint32_t pi = lds_append(rest != 0, &S.n_p[nxt]);
             if (rest) {
                 if (pi < (uint32_t)F) {
+#if KETO_PACK
+                    S.p_sdd[nxt][pi] = sd | (dg << 16);
+#else
                     S.p_sd[nxt][pi] = (uint16_t)sd;
-                    S.p_begin[nxt][pi] = bg;
                     S.p_deg[nxt][pi] = dg;
+#endif
+                    S.p_begin[nxt][pi] = bg;
                 } else {
                     S.spill = 1;
                 }
             }
+#if KETO_PACK
+            bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, take ? dg : 0, k, S.p_sdd[cur] + base,
+                                            S.p_begin[cur] + base, nxt, edges);
+#else
             bidi_expand<U, HLOG, F, BT, LF>(g, frec, brec, S, L, take ? dg : 0, k, S.p_sd[cur] + base,
                                             S.p_begin[cur] + base, nxt, edges);
+#endif
             __syncthreads();
         }
         if (stamp) {
@@ -1633,9 +1686,41 @@ void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
     }
 }
 
+// Host-to-host first stage in ONE launch (ketogpu_engine::check_host, pinned requests):
+// each unit reads its 16 roots and targets straight from pinned host memory over PCIe
+// (128 B per unit, ~8 MB per 10^6 requests spread over the whole traversal), validates
+// them as validate_kernel does and stores them in HBM for the spill stages.  Replaces
+// the chunk pipeline (load_kernel per chunk + one first-stage launch per chunk on two
+// streams): no exposed first-chunk upload, one launch tail instead of one per chunk.
+__global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+                                                       const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
+                                                       uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
+                                                       unsigned int *spill_count, unsigned long long *stats,
+                                                       unsigned long long *first_bad) {
+    __shared__ BidiShared<16, 9, 128, 64, 7> S;
+    const uint64_t unit = blockIdx.x;
+    const uint64_t c = unit * 16 + threadIdx.x;
+    uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+    if (threadIdx.x < 16 && c < n) {
+        r = hr[c];
+        t = ht[c];
+        if ((r != KETOGPU_NODE_NONE && r >= g.Nx) || (t != KETOGPU_NODE_NONE && t >= g.N)) {
+            atomicMin(first_bad, (unsigned long long)c);
+            r = t = KETOGPU_NODE_NONE;
+        }
+        dr[c] = r;
+        dt[c] = t;
+    }
+    bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count,
+                                 stats, nullptr);
+}
+
 // zero the per-run outputs and counters in one launch
+// bad (may be null): a host batch's first-invalid-request word, reset to "none" here
+// instead of by a separate memset launch
 __global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t *a, uint64_t na, uint64_t *b, uint64_t nb,
-                                                       unsigned long long *c, uint64_t nc) {
+                                                       unsigned long long *c, uint64_t nc, unsigned long long *bad) {
+    if (bad && blockIdx.x == 0 && threadIdx.x == 0) *bad = ~0ull;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < na + nb + nc; i += (uint64_t)gridDim.x * kBlock) {
         if (i < na)
             a[i] = 0;
@@ -1692,9 +1777,23 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const uint64_t *allowed, c
 // mirror (host-mapped pinned memory, may be null): out[0, mirror_words) is also written
 // there, so the host reads the statistics and the spill counters after its one
 // synchronization without a separate copy
+// Blocks >= 1 (when E.out is set): the host batch's emit (emit_kernel's work) in the same
+// launch, one launch less at the end of every host-to-host call.
+struct EmitReq {
+    const uint64_t *allowed = nullptr, *flags = nullptr;
+    uint64_t words = 0;
+    const unsigned long long *first_bad = nullptr;
+    uint64_t *out = nullptr;
+};
 __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned long long *slots, int regions,
                                                               unsigned long long *out, unsigned long long *mirror,
-                                                              int mirror_words) {
+                                                              int mirror_words, EmitReq E) {
+    if (blockIdx.x) {
+        const uint64_t nf = E.flags ? E.words : 0, m = E.words + nf + 1;
+        for (uint64_t i = (uint64_t)(blockIdx.x - 1) * kBlock + threadIdx.x; i < m; i += (uint64_t)(gridDim.x - 1) * kBlock)
+            E.out[i] = i < E.words ? E.allowed[i] : i < E.words + nf ? E.flags[i - E.words] : (uint64_t)*E.first_bad;
+        return;
+    }
     __shared__ unsigned long long part[kBlock / 64][3];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int r = 0; r < regions; r++) {
@@ -2266,7 +2365,12 @@ struct ketogpu_engine {
     hipStream_t copy_stream = nullptr, stream2 = nullptr;
     unsigned long long *d_bad = nullptr;  // smallest request index with an id outside the snapshot
     uint64_t pipe_chunk = 1 << 18;        // requests per pipelined chunk (KETOGPU_PIPE_CHUNK)
+    // pinned requests read in place by one first-stage launch (bidi_host_kernel);
+    // KETOGPU_PIPE_MODE=chunks restores the chunk pipeline (load_kernel + a launch per chunk)
+    bool pipe_direct = true;
     uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
+    EmitReq emit_req;                     // host batch: emit launched with the statistics reduction
+    unsigned long long *clear_bad = nullptr;  // host batch: d_bad reset by the run's clear launch
     uint64_t res_cap = 0;
 
     hipEvent_t ev() {
@@ -2376,6 +2480,7 @@ struct ketogpu_engine {
         HIP_CHECK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
         if (const char *pc = getenv("KETOGPU_PIPE_CHUNK"))  // requests per chunk, rounded to 64
             pipe_chunk = std::max<uint64_t>(64, (uint64_t)atoll(pc) / 64 * 64);
+        if (const char *pm = getenv("KETOGPU_PIPE_MODE")) pipe_direct = std::string(pm) != "chunks";
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
@@ -2625,7 +2730,8 @@ struct ketogpu_engine {
 
     // sum the spread unit-statistics slots of both regions (rows, edges, reverse entries)
     void read_unit_stats(uint64_t out[3]) {
-        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), nullptr, 0);
+        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), nullptr, 0,
+                EmitReq{});
         HIP_CHECK(hipMemcpyAsync(h_ctr + 32, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
         for (int k = 0; k < 3; k++) out[k] = h_ctr[32 + k] + h_ctr[35 + k];
@@ -2669,7 +2775,12 @@ struct ketogpu_engine {
         // (host-mapped: no copy launch between it and the sync)
         static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
         // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
-        KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16, 12);
+        // a pending host-batch emit rides in the same launch (blocks >= 1)
+        const EmitReq E = emit_req;
+        emit_req = EmitReq{};
+        const unsigned eb = E.out ? (unsigned)std::min<uint64_t>(blocks_for(2 * E.words + 1), 255) : 0;
+        KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16,
+                12, E);
         if (before_sync) before_sync();
         HIP_CHECK(hipStreamSynchronize(stream));
         unit_end = d;
@@ -2756,6 +2867,11 @@ struct ketogpu_engine {
                 if (!src) {
                     launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                                 st.stats, stamps);
+                } else if (src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, 128, 7, 16, 1}) {
+                    // pinned requests: one launch whose units read their requests in place
+                    KLAUNCH(bidi_host_kernel, dim3((unsigned)bunits), dim3(64), 0, stream, g, frec, brec, src->roots,
+                            src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],
+                            st.stats, d_bad);
                 } else {
                     // Host-to-host batch (check_host): the requests arrive in chunks on the
                     // copy stream; each chunk is validated and its units launched as soon as
@@ -3041,7 +3157,8 @@ struct ketogpu_engine {
         uint64_t words = (q.n + 63) / 64;
         // one launch zeroes results, flags, statistics and spill counters
         KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
-                           q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen);
+                           q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen, clear_bad);
+        clear_bad = nullptr;
         // A timing event costs ~5.6 us of GPU idle between the kernels it separates
         // (kernel trace of config #2): with the bidi first stage the run starts at that
         // stage's own start event, recorded right after this point.
@@ -3140,7 +3257,7 @@ struct ketogpu_engine {
     // The device's view of host memory it can read in place (pinned: ketogpu_host_alloc /
     // hipHostMalloc / hipHostRegister; or device memory of this engine's GPU), else nullptr
     // (pageable memory goes through DMA copies).
-    const uint32_t *device_view(const uint32_t *p) {
+    const uint32_t *device_view(const uint32_t *p, bool query = true) {
         if (!p) return nullptr;
         {  // buffers of ketogpu_host_alloc: known without a runtime query (~10 us per call)
             std::lock_guard<std::mutex> lk(g_pinned_mu);
@@ -3151,6 +3268,7 @@ struct ketogpu_engine {
                 if (off < it->second.bytes && it->second.dev) return (const uint32_t *)(it->second.dev + off);
             }
         }
+        if (!query) return nullptr;
         hipPointerAttribute_t at{};
         const hipError_t e = hipPointerGetAttributes(&at, p);
         static const bool dbg = getenv("KETOGPU_DEBUG_PTR") != nullptr;
@@ -3197,9 +3315,25 @@ struct ketogpu_engine {
         ketogpu_queries &q = *io;
         q.n = n;
         const uint64_t words = (n + 63) / 64;
-        HIP_CHECK(hipMemsetAsync(d_bad, 0xFF, sizeof(unsigned long long), stream));
-        const bool pipe = n >= 2 * pipe_chunk && use_units && !wave_u && use_v2 && use_bidi &&
-                          !(trials_left && n >= kTrialMin);
+        emit_req = EmitReq{};
+        clear_bad = nullptr;
+        const bool bidi_ok = n && use_units && !wave_u && use_v2 && use_bidi && !(trials_left && n >= kTrialMin);
+        // KETOGPU_PIPE_DMA=1: pinned requests are copied by DMA (copy engines) instead of
+        // read in place by the device (CUs); an A/B knob
+        static const bool dma = getenv("KETOGPU_PIPE_DMA") != nullptr;
+        const bool big = n >= 2 * pipe_chunk;
+        // the device's view of the request arrays: ketogpu_host_alloc buffers from the
+        // registry; other pinned memory by a runtime query, asked for big batches only
+        const uint32_t *dr = nullptr, *dt = nullptr;
+        if (bidi_ok && !dma) {
+            dr = device_view(roots, big);
+            dt = dr ? device_view(targets, big) : nullptr;
+        }
+        const bool mapped = dr && dt;
+        // host-batch first stage: pinned requests read in place by one launch (any size),
+        // else the chunk pipeline for big batches
+        const bool pipe = bidi_ok && ((mapped && pipe_direct) || big);
+        if (!pipe) HIP_CHECK(hipMemsetAsync(d_bad, 0xFF, sizeof(unsigned long long), stream));
         if (!pipe) {
             if (n) {
                 HIP_CHECK(hipMemcpyAsync(q.d_roots, roots, n * 4, hipMemcpyHostToDevice, stream));
@@ -3209,15 +3343,17 @@ struct ketogpu_engine {
             }
             run(q);
         } else {
-            // KETOGPU_PIPE_DMA=1: pinned requests are copied by DMA per chunk (copy engines)
-            // instead of read in place by load_kernel (CUs); an A/B knob
-            static const bool dma = getenv("KETOGPU_PIPE_DMA") != nullptr;
-            const uint32_t *dr = dma ? nullptr : device_view(roots), *dt = dr ? device_view(targets) : nullptr;
-            const HostSrc src{dr && dt ? dr : roots, dr && dt ? dt : targets, dr && dt};
+            const HostSrc src{mapped ? dr : roots, mapped ? dt : targets, mapped};
             ensure_res(2 * words + 1);
-            run_once(q, &src, [&] {  // results, flags and the validation verdict in one launch
-                KLAUNCH(emit_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(2 * words + 1), 256)), dim3(kBlock), 0,
-                        stream, q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res);
+            clear_bad = d_bad;  // reset by the run's clear launch
+            // results, flags and the validation verdict in one launch with the statistics
+            emit_req = EmitReq{q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res};
+            run_once(q, &src, [&] {
+                if (emit_req.out) {  // not taken by the bidi cascade's tail
+                    KLAUNCH(emit_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(2 * words + 1), 256)),
+                            dim3(kBlock), 0, stream, q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res);
+                    emit_req = EmitReq{};
+                }
             });
             // the staged words were final unless requests went on to the global path
             if (!last.spilled_requests) {

@@ -54,14 +54,17 @@ def _gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["direct", "chunks"])
 @pytest.mark.parametrize("chunk", ["4096", "65536", "1048576"])
-def test_pipelined_check_ids_matches_oracle(rbac, chunk, monkeypatch):
-    """bidi plan, chunked upload (several chunk sizes: many chunks, a few, one = not
-    pipelined) on pinned and pageable host arrays; the HBM-resident run agrees"""
+def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, monkeypatch):
+    """bidi plan, host batches: pinned requests read in place by one first-stage launch
+    (direct) or by the chunk pipeline (several chunk sizes: many chunks, a few, one = not
+    pipelined), and pageable host arrays; the HBM-resident run agrees"""
     _gpu()
     _, snap, roots, targets, want = rbac
     monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", chunk)
+    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
     eng = check.Engine(snap)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     pr, pt = check.pinned(roots), check.pinned(targets)
@@ -79,12 +82,17 @@ def test_pipelined_check_ids_matches_oracle(rbac, chunk, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_check_ids_rejects_ids_outside_the_snapshot(rbac, monkeypatch):
+@pytest.mark.parametrize("mode", ["direct", "chunks"])
+def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, monkeypatch):
     _gpu()
     _, snap, roots, targets, want = rbac
+    monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", "4096")
+    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
     eng = check.Engine(snap)
     st = snap.stats()
+    words = (len(roots) + 63) // 64
+    out = check.PinnedBuffer(words, np.uint64)
     for bad_at, which in ((0, "root"), (5000, "target"), (len(roots) - 1, "root")):
         r, t = roots.copy(), targets.copy()
         if which == "root":
@@ -94,6 +102,10 @@ def test_check_ids_rejects_ids_outside_the_snapshot(rbac, monkeypatch):
         with pytest.raises(L.KetoError) as e:
             eng.check_ids(r, t)
         assert e.value.code == L.EINVAL and f"request {bad_at} " in str(e.value)
+        pr, pt = check.pinned(r), check.pinned(t)  # read in place by the device
+        with pytest.raises(L.KetoError) as e:
+            eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, len(r), out.array.ctypes.data)
+        assert e.value.code == L.EINVAL and f"request {bad_at} " in str(e.value)
         with pytest.raises(L.KetoError):
             eng.upload(r, t)
     # the engine is still usable and exact afterwards
@@ -101,12 +113,14 @@ def test_check_ids_rejects_ids_outside_the_snapshot(rbac, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_pipelined_call_with_global_path_spills(monkeypatch):
+@pytest.mark.parametrize("mode", ["direct", "chunks"])
+def test_pipelined_call_with_global_path_spills(mode, monkeypatch):
     """a 20000-long chain of subject sets: requests whose search outgrows every LDS table
-    (8192 slots at most) finish on the global path after the pipelined first stage"""
+    (8192 slots at most) finish on the global path after the host-batch first stage"""
     _gpu()
     monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", "8192")
+    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
     n = 20000
     rows = [(1, f"g{i}", "m", None, 1, f"g{i + 1}", "m") for i in range(n)]
     rows.append((1, f"g{n}", "m", "alice", None, None, None))
@@ -120,6 +134,11 @@ def test_pipelined_call_with_global_path_spills(monkeypatch):
     eng = check.Engine(snap)
     got = eng.check_ids(roots, targets)
     np.testing.assert_array_equal(got, who == 0)
+    assert eng.last_stats()["spilled_requests"] > 0
+    pr, pt = check.pinned(roots), check.pinned(targets)  # pinned: read in place (direct)
+    out = check.PinnedBuffer((len(roots) + 63) // 64, np.uint64)
+    eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, len(roots), out.array.ctypes.data)
+    np.testing.assert_array_equal(check.unpack_bits(out.array.copy(), len(roots)), who == 0)
     assert eng.last_stats()["spilled_requests"] > 0
 
 
