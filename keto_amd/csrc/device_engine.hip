@@ -1031,8 +1031,12 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 // is backward-visited only as t or as an entry of t's own reverse row; so once the other
 // side's seed row has been read (in an earlier level: its inserts are complete), a push
 // of such a node only looks it up.  Leaf groups (only subject-ID members) take no slot.
+// KETO_PACK=1 (default): pending-list entries pack slot, direction and degree into one
+// word and the eager seed rows reuse list 1, 8,864 instead of 9,696 B of LDS per unit
+// and 81 instead of 97 VGPRs: 18 instead of 16 units per CU (config #2: 0.375 vs 0.400
+// ms per 10^6 requests, profiles/r02/ab_pack)
 #ifndef KETO_PACK
-#define KETO_PACK 0
+#define KETO_PACK 1
 #endif
 constexpr uint32_t kBothMax = 12;      // both sides expand while both pending sums are <= this
 constexpr uint32_t kSeedBothMax = 32;  // seeds pushed eagerly when both seed rows are <= this
@@ -1119,6 +1123,9 @@ template <int HLOG>
 __device__ __forceinline__ int bidi_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
     constexpr int H = 1 << HLOG;
     uint32_t hh = (u * 2654435761u) >> (32 - HLOG);
+#if KETO_PROBE_ROLLED
+#pragma unroll 1
+#endif
     for (int p = 0; p < H; p++, hh = (hh + 1) & (H - 1)) {
         // insert: compare-and-swap first (one LDS round trip per probe, whether the slot
         // is empty, holds u or holds another key)
@@ -1692,30 +1699,53 @@ void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
 // them as validate_kernel does and stores them in HBM for the spill stages.  Replaces
 // the chunk pipeline (load_kernel per chunk + one first-stage launch per chunk on two
 // streams): no exposed first-chunk upload, one launch tail instead of one per chunk.
+// K units per workgroup, run one after the other: the requests of all K are read at the
+// start, so only the first unit waits for PCIe (a read from host memory takes several
+// times an HBM miss and every unit would wait for one).
+template <int K>
 __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
                                                        uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
                                                        unsigned int *spill_count, unsigned long long *stats,
                                                        unsigned long long *first_bad) {
     __shared__ BidiShared<16, 9, 128, 64, 7> S;
-    const uint64_t unit = blockIdx.x;
-    const uint64_t c = unit * 16 + threadIdx.x;
-    uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
-    if (threadIdx.x < 16 && c < n) {
-        r = hr[c];
-        t = ht[c];
-        if ((r != KETOGPU_NODE_NONE && r >= g.Nx) || (t != KETOGPU_NODE_NONE && t >= g.N)) {
-            atomicMin(first_bad, (unsigned long long)c);
-            r = t = KETOGPU_NODE_NONE;
+    uint32_t r[K], t[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
+        r[k] = t[k] = KETOGPU_NODE_NONE;
+        if (threadIdx.x < 16 && c < n) {
+            r[k] = hr[c];
+            t[k] = ht[c];
         }
-        dr[c] = r;
-        dt[c] = t;
     }
-    bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count,
-                                 stats, nullptr);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
+        if (threadIdx.x < 16 && c < n) {
+            if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
+                atomicMin(first_bad, (unsigned long long)c);
+                r[k] = t[k] = KETOGPU_NODE_NONE;
+            }
+            dr[c] = r[k];
+            dt[c] = t[k];
+        }
+    }
+    const uint64_t units = (n + 15) / 16;
+#pragma unroll 1
+    for (int k = 0; k < K; k++) {
+        const uint64_t unit = (uint64_t)blockIdx.x * K + k;
+        if (unit >= units) break;
+        uint32_t rk = r[0], tk = t[0];
+#pragma unroll
+        for (int j = 1; j < K; j++)
+            if (j == k) rk = r[j], tk = t[j];
+        bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out,
+                                     spill_count, stats, nullptr);
+        __syncthreads();
+    }
 }
 
-// zero the per-run outputs and counters in one launch
 // bad (may be null): a host batch's first-invalid-request word, reset to "none" here
 // instead of by a separate memset launch
 __global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t *a, uint64_t na, uint64_t *b, uint64_t nb,
@@ -2368,6 +2398,7 @@ struct ketogpu_engine {
     // pinned requests read in place by one first-stage launch (bidi_host_kernel);
     // KETOGPU_PIPE_MODE=chunks restores the chunk pipeline (load_kernel + a launch per chunk)
     bool pipe_direct = true;
+    int host_units = 2;  // units per workgroup of bidi_host_kernel (KETOGPU_HOST_UNITS: 1, 2 or 4)
     uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
     EmitReq emit_req;                     // host batch: emit launched with the statistics reduction
     unsigned long long *clear_bad = nullptr;  // host batch: d_bad reset by the run's clear launch
@@ -2481,6 +2512,7 @@ struct ketogpu_engine {
         if (const char *pc = getenv("KETOGPU_PIPE_CHUNK"))  // requests per chunk, rounded to 64
             pipe_chunk = std::max<uint64_t>(64, (uint64_t)atoll(pc) / 64 * 64);
         if (const char *pm = getenv("KETOGPU_PIPE_MODE")) pipe_direct = std::string(pm) != "chunks";
+        if (const char *hu = getenv("KETOGPU_HOST_UNITS")) host_units = atoi(hu);
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
@@ -2869,9 +2901,17 @@ struct ketogpu_engine {
                                 st.stats, stamps);
                 } else if (src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, 128, 7, 16, 1}) {
                     // pinned requests: one launch whose units read their requests in place
-                    KLAUNCH(bidi_host_kernel, dim3((unsigned)bunits), dim3(64), 0, stream, g, frec, brec, src->roots,
-                            src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],
-                            st.stats, d_bad);
+#define KETO_HOST_K(K)                                                                                     \
+    KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec,  \
+            src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],   \
+            st.stats, d_bad)
+                    if (host_units == 4)
+                        KETO_HOST_K(4);
+                    else if (host_units == 2)
+                        KETO_HOST_K(2);
+                    else
+                        KETO_HOST_K(1);
+#undef KETO_HOST_K
                 } else {
                     // Host-to-host batch (check_host): the requests arrive in chunks on the
                     // copy stream; each chunk is validated and its units launched as soon as

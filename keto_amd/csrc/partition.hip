@@ -71,7 +71,7 @@ struct PartDev {
     const uint64_t *lb_off;  // [Nil + 1] interior predecessors of owned interior nodes (backward rows)
     const uint32_t *lb_col;
     uint32_t dir;            // round direction: 0 forward, 1 backward
-    uint64_t *vis, *nxt;     // [W][Nil]
+    uint64_t *vis, *nxt;     // [W][Nil] visited bits of the round's requests, new bits of the level
     uint64_t *fe_key, *fe_pre, *fe_mask;
     uint64_t fe_cap;
     uint64_t *touch;
@@ -305,7 +305,20 @@ __global__ __launch_bounds__(kPB) void part_scatter_kernel(PartDev P, const keto
     }
 }
 
-// received (word, u, mask): OR into the owned state, new bits enter the next frontier.
+// KETO_APPLY_READ=1 (default): apply reads vis before its atomic OR and skips records
+// that bring no new bit; 0: every record goes straight to the atomic (one dependent
+// access less per record, one atomic more per redundant record)
+#ifndef KETO_APPLY_READ
+#define KETO_APPLY_READ 1
+#endif
+
+// received (word, u, mask): OR into the owned state, new bits enter the next frontier:
+// they are ORed into nxt[word][u] and the record that finds nxt empty appends the entry,
+// so a (word, u) is expanded once per level with all its new bits (the gather pass copies
+// nxt into the list).  Appending every record's new bits as its own entry instead (no nxt,
+// no gather) measured 0.33 ms faster per 10^6 config #5 requests but lets the entries of
+// one (word, u) multiply along paths that split and merge again (up to 64 per level):
+// rounds of one word overflowed small buffers that the deduplicated form fits.
 // A block takes a tile of kPTile records (kPItems per thread) and makes ONE reservation
 // on the packed frontier counter (count << kCntShift | row-length prefix) and one on the
 // touch counter per tile: a reservation per wave serialised on the shared counter
@@ -332,8 +345,12 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
                 continue;
             }
             const size_t slot = (size_t)r.a * P.Nil + l;
-            const uint64_t nw = r.m & ~P.vis[slot];
+#if KETO_APPLY_READ
+            const uint64_t nw = r.m & ~P.vis[slot];  // skip the atomic when no bit is new
             if (!nw) continue;
+#else
+            const uint64_t nw = r.m;
+#endif
             const uint64_t old = atomicOr((unsigned long long *)&P.vis[slot], (unsigned long long)nw);
             const uint64_t newly = nw & ~old;
             if (!newly) continue;
@@ -397,6 +414,8 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
     }
 }
 
+// forward: owned targets, direct hits (r in rev(t)) and queries (request, interior v in
+// rev(t)).  Backward: owned roots, queries (request, u) for u in fint(r).
 // next level's masks: nxt -> entry list, nxt cleared
 __global__ __launch_bounds__(kPB) void part_gather_kernel(PartDev P, uint64_t b, uint64_t e) {
     const uint64_t i = b + (uint64_t)blockIdx.x * kPB + threadIdx.x;
@@ -407,8 +426,6 @@ __global__ __launch_bounds__(kPB) void part_gather_kernel(PartDev P, uint64_t b,
     P.nxt[slot] = 0;
 }
 
-// forward: owned targets, direct hits (r in rev(t)) and queries (request, interior v in
-// rev(t)).  Backward: owned roots, queries (request, u) for u in fint(r).
 __global__ __launch_bounds__(kPB) void part_pull_emit_kernel(PartDev P) {
     const uint64_t i = (uint64_t)blockIdx.x * kPB + threadIdx.x;
     uint64_t b = 0, e = 0;
@@ -509,6 +526,26 @@ struct ketogpu_part {
     int cur = 0;
     bool dirty = false;  // state may hold bits a sparse reset does not know about
     ketogpu_part_stats stats{};
+    // Two state buffers (vis + the entry keys and touch list the sparse reset reads): a
+    // round runs on buffer vb while the previous round's buffer is cleared on rstream, so
+    // the reset (0.62 ms per 10^6 config #2 requests, random 8-B stores) overlaps the next
+    // round instead of ending every round; begin() makes `stream` wait for its buffer.
+    uint64_t *vis_buf[2] = {nullptr, nullptr}, *key_buf[2] = {nullptr, nullptr}, *touch_buf[2] = {nullptr, nullptr};
+    int vb = 0;
+    hipStream_t rstream = nullptr;
+    hipEvent_t clean_ev[2] = {nullptr, nullptr}, done_ev = nullptr;
+    bool clean_pending[2] = {false, false};
+    void use_buffer(int b) {
+        vb = b;
+        P.vis = vis_buf[b];
+        P.fe_key = key_buf[b];
+        P.touch = touch_buf[b];
+    }
+    // the current buffer's clear (if one is in flight) before `stream` touches it
+    void wait_clean() {
+        if (clean_pending[vb]) PHIP(hipStreamWaitEvent(stream, clean_ev[vb], 0));
+        clean_pending[vb] = false;
+    }
     // measurement pass (ketogpu_part_set_timing): event pairs per launch, resolved at the
     // next host synchronization
     bool timing = false;
@@ -530,22 +567,25 @@ struct ketogpu_part {
     }
     // bracket one launch (fam: KETOGPU_PART_K_*) with events while timing; bytes always
     template <class F>
-    void timed(int fam, uint64_t bytes, F &&launch) {
+    void timed(int fam, uint64_t bytes, F &&launch, hipStream_t on = nullptr) {
         stats.bytes[fam] += bytes;
         if (!timing) {
             launch();
             return;
         }
+        if (!on) on = stream;
         hipEvent_t a = ev(), b = ev();
-        PHIP(hipEventRecord(a, stream));
+        PHIP(hipEventRecord(a, on));
         launch();
-        PHIP(hipEventRecord(b, stream));
+        PHIP(hipEventRecord(b, on));
         pend.push_back({fam, a, b});
     }
     // after a stream synchronization: fold the completed launches' times into the stats
+    // (launches on rstream may still run: their end events are waited for)
     void resolve_timing() {
         for (const Pending &x : pend) {
             float ms = 0;
+            PHIP(hipEventSynchronize(x.b));
             PHIP(hipEventElapsedTime(&ms, x.a, x.b));
             stats.ms[x.fam] += ms;
             stats.launches[x.fam]++;
@@ -559,7 +599,12 @@ struct ketogpu_part {
             (void)hipSetDevice(device);
             (void)hipStreamSynchronize(stream);
         }
+        if (rstream) (void)hipStreamSynchronize(rstream);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
+        for (auto e : clean_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (done_ev) (void)hipEventDestroy(done_ev);
+        if (rstream) (void)hipStreamDestroy(rstream);
         for (void *p : owned) (void)hipFree(p);
         if (h) (void)hipHostFree(h);
         if (stream) (void)hipStreamDestroy(stream);
@@ -598,6 +643,9 @@ struct ketogpu_part {
         if (device < 0 || device >= ndev) throw Error(KETOGPU_EDEVICE, "no such HIP device");
         PHIP(hipSetDevice(device));
         PHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        PHIP(hipStreamCreateWithFlags(&rstream, hipStreamNonBlocking));
+        for (auto &e : clean_ev) PHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        PHIP(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
         auto upv = [&](const auto *p, size_t n) {
             using T = std::remove_const_t<std::remove_pointer_t<decltype(p)>>;
             return upload(std::vector<T>(p, p + n));
@@ -627,10 +675,12 @@ struct ketogpu_part {
         uint64_t budget = o.state_budget_bytes ? o.state_budget_bytes : std::min<uint64_t>(free_b / 4, 64ull << 30);
         budget = std::min<uint64_t>(budget, (uint64_t)free_b / 2);
         uint64_t lists = budget / 4;
-        P.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 32, 1 << 16), kMaxListEntries);
+        // per entry: key, prefix, mask, touch + the second buffer's key and touch
+        P.fe_cap = std::min<uint64_t>(std::max<uint64_t>(lists / 48, 1 << 16), kMaxListEntries);
         P.touch_cap = P.fe_cap;
         P.ocap = o.record_capacity ? o.record_capacity : std::max<uint64_t>(lists / 16, 1 << 16);
-        W = std::max<uint64_t>(1, (budget - std::min(budget, lists + P.ocap * 16)) / (16ull * std::max<uint32_t>(Nil, 1)));
+        // 24 B per (word, node): the two vis buffers and nxt
+        W = std::max<uint64_t>(1, (budget - std::min(budget, lists + P.ocap * 16)) / (24ull * std::max<uint32_t>(Nil, 1)));
         if (o.max_words_per_round) W = std::min<uint64_t>(W, o.max_words_per_round);
         W = std::max<uint64_t>(1, std::min<uint64_t>(W, 1u << 16));
         // Not bounded by fe_cap / (Nil + 64) (the worst case of one (word, node) entry per
@@ -640,14 +690,17 @@ struct ketogpu_part {
         // device_util.hpp) or whose records exceed ocap sets the overflow flag; every rank
         // then aborts the round and retries it with half the requests (PartitionedEngine).
         const size_t state = (size_t)W * std::max<uint32_t>(Nil, 1);
-        P.vis = own(palloc<uint64_t>(state));
-        P.nxt = own(palloc<uint64_t>(state));
-        PHIP(hipMemsetAsync(P.vis, 0, state * 8, stream));
+        for (int b = 0; b < 2; b++) {
+            vis_buf[b] = own(palloc<uint64_t>(state));
+            PHIP(hipMemsetAsync(vis_buf[b], 0, state * 8, stream));
+            key_buf[b] = own(palloc<uint64_t>(P.fe_cap));
+            touch_buf[b] = own(palloc<uint64_t>(P.touch_cap));
+        }
+        use_buffer(0);
+        P.nxt = own(palloc<uint64_t>(state));  // all zero between levels (the gather clears it)
         PHIP(hipMemsetAsync(P.nxt, 0, state * 8, stream));
-        P.fe_key = own(palloc<uint64_t>(P.fe_cap));
         P.fe_pre = own(palloc<uint64_t>(P.fe_cap));
         P.fe_mask = own(palloc<uint64_t>(P.fe_cap));
-        P.touch = own(palloc<uint64_t>(P.touch_cap));
         P.obuf = own(palloc<ketogpu_record>(P.ocap));
         P.ctr = own(palloc<unsigned long long>(8));
         P.overflow = (unsigned int *)(P.ctr + 4);  // in the counter block: one copy reads both
@@ -674,6 +727,7 @@ struct ketogpu_part {
         if (dir != KETOGPU_PART_FORWARD && dir != KETOGPU_PART_BACKWARD)
             throw Error(KETOGPU_EINVAL, "partition: direction must be KETOGPU_PART_FORWARD or _BACKWARD");
         if (dirty) reset(true);
+        wait_clean();
         P.dir = (uint32_t)dir;
         if (n > W * 64) throw Error(KETOGPU_EINVAL, "partition: more requests than one round holds");
         // ids are validated by the seed kernel (a host loop over 10^6 requests cost ~0.5 ms
@@ -809,24 +863,35 @@ struct ketogpu_part {
         return overflow_bits() & 2u ? KETOGPU_EINVAL : KETOGPU_OK;
     }
 
-    // clear the round's state: sparse (recorded entries) unless bits may be unrecorded
+    // Clear the round's state.  dense (or after an overflow, when bits may be unrecorded):
+    // the whole current buffer, synchronously.  Sparse: the recorded entries, on rstream
+    // after the round's last kernel, while the next round runs on the other buffer.
     void reset(bool dense) {
         read_ctr();
         if (dense || overflow_bits()) {
+            wait_clean();
             const size_t state = (size_t)W * std::max<uint32_t>(P.Nil, 1);
             PHIP(hipMemsetAsync(P.vis, 0, state * 8, stream));
             PHIP(hipMemsetAsync(P.nxt, 0, state * 8, stream));
         } else {
             const uint64_t ents = lb + cnt, ntouch = h[2];
+            PHIP(hipEventRecord(done_ev, stream));
+            PHIP(hipStreamWaitEvent(rstream, done_ev, 0));
+            uint64_t *vis = P.vis, *keys = P.fe_key, *touch = P.touch;
+            const uint32_t Nil = P.Nil;
             if (ents)
-                timed(KETOGPU_PART_K_RESET, 16 * ents, [&] {
-                    KLAUNCH(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, stream, P.vis, P.Nil, P.fe_key, ents);
-                });
+                timed(
+                    KETOGPU_PART_K_RESET, 16 * ents,
+                    [&] { KLAUNCH(part_reset_kernel, dim3(pblocks(ents)), dim3(kPB), 0, rstream, vis, Nil, keys, ents); },
+                    rstream);
             if (ntouch)
-                timed(KETOGPU_PART_K_RESET, 16 * ntouch, [&] {
-                    KLAUNCH(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, stream, P.vis, P.Nil, P.touch,
-                            ntouch);
-                });
+                timed(
+                    KETOGPU_PART_K_RESET, 16 * ntouch,
+                    [&] { KLAUNCH(part_reset_kernel, dim3(pblocks(ntouch)), dim3(kPB), 0, rstream, vis, Nil, touch, ntouch); },
+                    rstream);
+            PHIP(hipEventRecord(clean_ev[vb], rstream));
+            clean_pending[vb] = true;
+            use_buffer(vb ^ 1);  // the next round's state
         }
         PHIP(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), stream));
         PHIP(hipStreamSynchronize(stream));

@@ -53,8 +53,16 @@ def _gpu():
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
 
 
+def _pipe_mode(monkeypatch, mode):
+    """direct[K]: pinned requests read in place by one launch, K units per workgroup;
+    chunks: the chunk pipeline"""
+    monkeypatch.setenv("KETOGPU_PIPE_MODE", "chunks" if mode == "chunks" else "direct")
+    if mode.startswith("direct") and mode != "direct":
+        monkeypatch.setenv("KETOGPU_HOST_UNITS", mode[len("direct"):])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "chunks"])
+@pytest.mark.parametrize("mode", ["direct", "direct1", "direct4", "chunks"])
 @pytest.mark.parametrize("chunk", ["4096", "65536", "1048576"])
 def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, monkeypatch):
     """bidi plan, host batches: pinned requests read in place by one first-stage launch
@@ -64,7 +72,7 @@ def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, monkeypatch):
     _, snap, roots, targets, want = rbac
     monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", chunk)
-    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
+    _pipe_mode(monkeypatch, mode)
     eng = check.Engine(snap)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     pr, pt = check.pinned(roots), check.pinned(targets)
@@ -82,13 +90,13 @@ def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "chunks"])
+@pytest.mark.parametrize("mode", ["direct", "direct4", "chunks"])
 def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, monkeypatch):
     _gpu()
     _, snap, roots, targets, want = rbac
     monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", "4096")
-    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
+    _pipe_mode(monkeypatch, mode)
     eng = check.Engine(snap)
     st = snap.stats()
     words = (len(roots) + 63) // 64
@@ -113,14 +121,14 @@ def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["direct", "chunks"])
+@pytest.mark.parametrize("mode", ["direct", "direct4", "chunks"])
 def test_pipelined_call_with_global_path_spills(mode, monkeypatch):
     """a 20000-long chain of subject sets: requests whose search outgrows every LDS table
     (8192 slots at most) finish on the global path after the host-batch first stage"""
     _gpu()
     monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", "8192")
-    monkeypatch.setenv("KETOGPU_PIPE_MODE", mode)
+    _pipe_mode(monkeypatch, mode)
     n = 20000
     rows = [(1, f"g{i}", "m", None, 1, f"g{i + 1}", "m") for i in range(n)]
     rows.append((1, f"g{n}", "m", "alice", None, None, None))

@@ -17,8 +17,9 @@ for round in 1 2; do
       *=*) envset=("$v") ;;
       *) lib="$PWD/keto_amd/variants/libketogpu_$v.so" ;;
     esac
+    # AB_ARGS: extra bench.py arguments (e.g. "--mode partitioned --scale 0.01")
     env "${envset[@]}" KETOGPU_LIB="$lib" timeout -k 10 240 python3 bench.py --no-cpu-baseline --parity sample \
-      --steps 10 --warmup 3 > "$OUT/${v}_$round.json" 2> "$OUT/${v}_$round.err" \
+      --steps 10 --warmup 3 $AB_ARGS > "$OUT/${v}_$round.json" 2> "$OUT/${v}_$round.err" \
       || { echo "$v failed"; tail -5 "$OUT/${v}_$round.err"; exit 1; }
     python3 -c "
 import json,sys; d=json.loads(open('$OUT/${v}_$round.json').read().strip().splitlines()[-1]); r=d['roofline']
