@@ -1702,6 +1702,9 @@ void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
 // K units per workgroup, run one after the other: the requests of all K are read at the
 // start, so only the first unit waits for PCIe (a read from host memory takes several
 // times an HBM miss and every unit would wait for one).
+#ifndef KETO_HOST_PREROWS
+#define KETO_HOST_PREROWS 0
+#endif
 template <int K>
 __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
@@ -1732,16 +1735,30 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
         }
     }
     const uint64_t units = (n + 15) / 16;
+#if KETO_HOST_PREROWS
+    // every unit's seed-row offsets loaded up front too: the later units start without a
+    // dependent HBM round trip
+    BidiSeed sd[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) sd[k] = bidi_load_rows(g, r[k], t[k]);
+#endif
 #pragma unroll 1
     for (int k = 0; k < K; k++) {
         const uint64_t unit = (uint64_t)blockIdx.x * K + k;
         if (unit >= units) break;
+#if KETO_HOST_PREROWS
+        BidiSeed sk = sd[0];
+#pragma unroll
+        for (int j = 1; j < K; j++)
+            if (j == k) sk = sd[j];
+#else
         uint32_t rk = r[0], tk = t[0];
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out,
-                                     spill_count, stats, nullptr);
+        const BidiSeed sk = bidi_load_rows(g, rk, tk);
+#endif
+        bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, sk, allowed, unit, spill_out, spill_count, stats, nullptr);
         __syncthreads();
     }
 }
@@ -2399,6 +2416,8 @@ struct ketogpu_engine {
     // KETOGPU_PIPE_MODE=chunks restores the chunk pipeline (load_kernel + a launch per chunk)
     bool pipe_direct = true;
     int host_units = 2;  // units per workgroup of bidi_host_kernel (KETOGPU_HOST_UNITS: 1, 2 or 4)
+    bool light_events = true;           // host batches: timing events only around the whole call
+    hipEvent_t light_begin = nullptr;   // that call's begin event (run_once -> run_units)
     uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
     EmitReq emit_req;                     // host batch: emit launched with the statistics reduction
     unsigned long long *clear_bad = nullptr;  // host batch: d_bad reset by the run's clear launch
@@ -2513,6 +2532,7 @@ struct ketogpu_engine {
             pipe_chunk = std::max<uint64_t>(64, (uint64_t)atoll(pc) / 64 * 64);
         if (const char *pm = getenv("KETOGPU_PIPE_MODE")) pipe_direct = std::string(pm) != "chunks";
         if (const char *hu = getenv("KETOGPU_HOST_UNITS")) host_units = atoi(hu);
+        if (const char *ea = getenv("KETOGPU_EVENTS")) light_events = std::string(ea) != "all";
         if (s.N >= kDynBase) throw Error(KETOGPU_EINVAL, "snapshot has >= 2^31 nodes");
         const char *mode = getenv("KETOGPU_PATH");  // "global": skip the LDS unit path (tests)
         use_units = !(mode && std::string(mode) == "global");
@@ -2800,7 +2820,9 @@ struct ketogpu_engine {
             cur ^= 1;
             u_prev = sg.u;
         }
-        HIP_CHECK(hipEventRecord(d, stream));
+        // b == nullptr (host batches): no event between the call's kernels (each costs ~6 us of
+        // GPU idle between the launches it separates); one event after the last launch
+        if (b) HIP_CHECK(hipEventRecord(d, stream));
         const size_t ns = stages.size() + 1;
         // the spill counters sit 8 words after the reduced statistics (st.stats
         // layout, kStatsLen): the reduction mirrors both into h_ctr[16..21] and h_ctr + 24
@@ -2814,10 +2836,15 @@ struct ketogpu_engine {
         KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16,
                 12, E);
         if (before_sync) before_sync();
+        if (!b) HIP_CHECK(hipEventRecord(d, stream));
         HIP_CHECK(hipStreamSynchronize(stream));
         unit_end = d;
-        unit_ev.push_back({a, b});
-        unit_ev.push_back({b, d});
+        if (b) {
+            unit_ev.push_back({a, b});
+            unit_ev.push_back({b, d});
+        } else {
+            unit_ev.push_back({a, d});
+        }
         const uint64_t *t = (const uint64_t *)h_ctr + 16;
         rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
         const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
@@ -2893,13 +2920,18 @@ struct ketogpu_engine {
                 // `cascade` (persistent over the previous stage's spilled units, counts read
                 // on the device), then the global path for single requests that exceed the
                 // last table; one host synchronization for counts and statistics
-                hipEvent_t a = ev(), b = ev();
-                HIP_CHECK(hipEventRecord(a, stream));
+                // host batches (src): the run's begin event was recorded ahead of its clear
+                // launch (light_begin) and no event separates the call's kernels
+                const bool direct = src && src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, 128, 7, 16, 1};
+                // (the chunk pipeline's other streams wait for an event after the clear)
+                const bool light = direct && light_begin;
+                hipEvent_t a = light ? light_begin : ev(), b = light ? nullptr : ev();
+                if (!light) HIP_CHECK(hipEventRecord(a, stream));
                 const uint64_t bunits = (q.n + bidi_cfg.u - 1) / bidi_cfg.u;
                 if (!src) {
                     launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                                 st.stats, stamps);
-                } else if (src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, 128, 7, 16, 1}) {
+                } else if (direct) {
                     // pinned requests: one launch whose units read their requests in place
 #define KETO_HOST_K(K)                                                                                     \
     KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec,  \
@@ -2952,7 +2984,7 @@ struct ketogpu_engine {
                     HIP_CHECK(hipEventRecord(j, stream2));
                     HIP_CHECK(hipStreamWaitEvent(stream, j, 0));
                 }
-                HIP_CHECK(hipEventRecord(b, stream));
+                if (b) HIP_CHECK(hipEventRecord(b, stream));
                 return bidi_tail(q, rs, unit_ev, a, b, bunits, before_sync);
             }
             uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
@@ -3195,6 +3227,13 @@ struct ketogpu_engine {
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
         uint64_t words = (q.n + 63) / 64;
+        // host batches: the run's begin event ahead of the clear launch (no event between
+        // the call's kernels, KETOGPU_EVENTS=all restores them)
+        light_begin = nullptr;
+        if (src && light_events) {
+            HIP_CHECK(hipEventRecord(t_begin, stream));
+            light_begin = t_begin;
+        }
         // one launch zeroes results, flags, statistics and spill counters
         KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
                            q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen, clear_bad);
@@ -3203,7 +3242,7 @@ struct ketogpu_engine {
         // (kernel trace of config #2): with the bidi first stage the run starts at that
         // stage's own start event, recorded right after this point.
         const bool bidi_first = use_units && !wave_u && use_v2 && use_bidi && q.n;
-        if (!bidi_first) HIP_CHECK(hipEventRecord(t_begin, stream));
+        if (!bidi_first && !light_begin) HIP_CHECK(hipEventRecord(t_begin, stream));
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
             uint64_t ns = run_units(q, rs, unit_ev, src, before_sync);
