@@ -1702,9 +1702,6 @@ void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
 // K units per workgroup, run one after the other: the requests of all K are read at the
 // start, so only the first unit waits for PCIe (a read from host memory takes several
 // times an HBM miss and every unit would wait for one).
-#ifndef KETO_HOST_PREROWS
-#define KETO_HOST_PREROWS 0
-#endif
 template <int K>
 __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
@@ -1735,29 +1732,17 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
         }
     }
     const uint64_t units = (n + 15) / 16;
-#if KETO_HOST_PREROWS
-    // every unit's seed-row offsets loaded up front too: the later units start without a
-    // dependent HBM round trip
-    BidiSeed sd[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) sd[k] = bidi_load_rows(g, r[k], t[k]);
-#endif
 #pragma unroll 1
     for (int k = 0; k < K; k++) {
         const uint64_t unit = (uint64_t)blockIdx.x * K + k;
         if (unit >= units) break;
-#if KETO_HOST_PREROWS
-        BidiSeed sk = sd[0];
-#pragma unroll
-        for (int j = 1; j < K; j++)
-            if (j == k) sk = sd[j];
-#else
         uint32_t rk = r[0], tk = t[0];
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
+        // (loading every unit's seed-row offsets up front as well measured slower: 1.99
+        // vs 2.10 x 10^9 checks/s, profiles/r02/ab_prerows)
         const BidiSeed sk = bidi_load_rows(g, rk, tk);
-#endif
         bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, sk, allowed, unit, spill_out, spill_count, stats, nullptr);
         __syncthreads();
     }
