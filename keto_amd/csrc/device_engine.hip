@@ -2917,7 +2917,11 @@ struct ketogpu_engine {
                     launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
                                 st.stats, stamps);
                 } else if (direct) {
-                    // pinned requests: one launch whose units read their requests in place
+                    // pinned requests: one launch whose units read their requests in place.
+                    // (Tried: only a share f of the units reading in place while load_kernel
+                    // copied the rest into HBM for a second launch on stream2 — f = 0.25 /
+                    // 0.35 / 0.5: 1.85 / 1.83 / 1.90 vs 2.09 x 10^9 checks/s,
+                    // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec,  \
             src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],   \

@@ -22,6 +22,8 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [
+    # host batches with pinned requests: the first stage reading its requests in place
+    ("bidi_host_kernel (host batches)", r"bidi_host_kernel"),
     # the pipelined host-to-host first stage is its own instantiation (last template
     # argument 1), so a launch per chunk never mixes into the full-batch launch's figures
     ("bidi_kernel<16> (pipelined chunks)", r"bidi_kernel<16, 9, .*, 1>"),
@@ -40,6 +42,9 @@ FAMILIES = [
     ("seed_kernel", r"\bseed_kernel"),
     ("part_expand_kernel", r"part_expand_kernel"),
     ("part_apply_kernel", r"part_apply_kernel"),
+    ("part_gather_kernel", r"part_gather_kernel"),
+    ("part_reset_kernel", r"part_reset_kernel"),
+    ("part_pull_answer_kernel", r"part_pull_answer_kernel"),
 ]
 
 
