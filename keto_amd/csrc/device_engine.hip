@@ -1038,6 +1038,10 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 #ifndef KETO_PACK
 #define KETO_PACK 1
 #endif
+// pending-list entries of the first-stage shape (bidi_kernel<16, 9, KETO_F1, 64, 7>)
+#ifndef KETO_F1
+#define KETO_F1 128
+#endif
 constexpr uint32_t kBothMax = 12;      // both sides expand while both pending sums are <= this
 constexpr uint32_t kSeedBothMax = 32;  // seeds pushed eagerly when both seed rows are <= this
 
@@ -1064,14 +1068,16 @@ struct BidiShared {
     uint32_t e_begin[2 * U], e_deg[2 * U];
 #endif
     uint16_t e_mask[EM];   // request bits of the entries being expanded
-    uint32_t c_pre[BT + 1];
-    uint32_t wave_sum[BT / 64];
+    // block scan (BT > 64: c_pre[BT] total, wave_sum) or owner map (one wave: c_pre[64])
+    uint32_t c_pre[BT > 64 ? BT + 1 : BT];
+    uint32_t wave_sum[BT > 64 ? BT / 64 : 1];
     uint32_t cost[2][U];          // pending degree sums per direction and request
     uint32_t root[U];
     uint32_t sel[2], lookup[2];   // per direction: bits expanded this level / lookup-only bits
     uint32_t sread[2];            // per direction: bits for which a push of a dead-end node is lookup-only
-    uint32_t n_used, n_e, n_p[2], spill, found, active;
-    unsigned long long cnt_rows, cnt_edges, cnt_rev;
+    uint32_t n_used, n_p[2], spill, found, active;
+    // unit statistics (workgroups of several waves; one wave adds its own to the global slots)
+    unsigned long long cnt[BT > 64 ? 3 : 1];
 };
 
 // per-level selection, wave-uniform: open requests, bits expanded per direction, lookup-only
@@ -1424,8 +1430,8 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     for (int i = tid; i < SH::H / 4; i += BT) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
     for (int i = tid; i < SH::H / 2; i += BT) reinterpret_cast<uint4 *>(S.st)[i] = make_uint4(0, 0, 0, 0);
     if (tid == 0) {
-        S.n_used = S.n_e = S.n_p[0] = S.n_p[1] = S.spill = S.found = S.active = 0;
-        S.cnt_rows = S.cnt_edges = S.cnt_rev = 0;
+        S.n_used = S.n_p[0] = S.n_p[1] = S.spill = S.found = S.active = 0;
+        if constexpr (BT > 64) S.cnt[0] = S.cnt[1] = S.cnt[2] = 0;
     }
     if (tid < 2 * U) S.cost[tid / U][tid % U] = 0;
     if (tid < 2) {
@@ -1635,8 +1641,16 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         return;
     }
     if (stamp) stamp[3] = __builtin_amdgcn_s_memtime();
-    wave_stats_add(rows, edges, 0, &S.cnt_rows, &S.cnt_edges, &S.cnt_rev);
-    __syncthreads();
+    if constexpr (BT > 64) {
+        wave_stats_add(rows, edges, 0, &S.cnt[0], &S.cnt[1], &S.cnt[2]);
+        __syncthreads();
+    } else {  // one wave: its sums go straight to the global slots
+#pragma unroll
+        for (int s = 32; s; s >>= 1) {
+            rows += __shfl_down(rows, s, 64);
+            edges += __shfl_down(edges, s, 64);
+        }
+    }
     if (stamp) {
         stamp[4] = stamp[3];
         stamp[5] = n_levels;
@@ -1646,8 +1660,8 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
     if (tid == 0) {
         uint32_t res = S.found & ((1u << U) - 1);
         if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << shift);
-        atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
-        atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
+        atomicAdd(&stat_slot(stats)[0], BT > 64 ? S.cnt[0] : (unsigned long long)rows);
+        atomicAdd(&stat_slot(stats)[1], BT > 64 ? S.cnt[1] : (unsigned long long)edges);
     }
 }
 
@@ -1708,7 +1722,7 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
                                                        uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
                                                        unsigned int *spill_count, unsigned long long *stats,
                                                        unsigned long long *first_bad) {
-    __shared__ BidiShared<16, 9, 128, 64, 7> S;
+    __shared__ BidiShared<16, 9, KETO_F1, 64, 7> S;
     uint32_t r[K], t[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -1743,7 +1757,7 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
         // (loading every unit's seed-row offsets up front as well measured slower: 1.99
         // vs 2.10 x 10^9 checks/s, profiles/r02/ab_prerows)
         const BidiSeed sk = bidi_load_rows(g, rk, tk);
-        bidi_unit<16, 9, 128, 64, 7>(S, g, frec, brec, sk, allowed, unit, spill_out, spill_count, stats, nullptr);
+        bidi_unit<16, 9, KETO_F1, 64, 7>(S, g, frec, brec, sk, allowed, unit, spill_out, spill_count, stats, nullptr);
         __syncthreads();
     }
 }
@@ -2259,14 +2273,14 @@ struct ketogpu_engine {
             return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe;
         }
     };
-    BidiCfg bidi_cfg{9, 64, 128, 7};
+    BidiCfg bidi_cfg{9, 64, KETO_F1, 7};
 
     void launch_bidi(const BidiCfg &c, unsigned grid, unsigned pad, const Batch &q, const uint32_t *parents,
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
-        if (chunked && c == BidiCfg{9, 64, 128, 7, 16, 1}) {  // the default shape's chunk instantiation
-            KLAUNCH((bidi_kernel<16, 9, 128, 64, 7, 1, 1>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
+        if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
+            KLAUNCH((bidi_kernel<16, 9, KETO_F1, 64, 7, 1, 1>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
                     q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp, unit0);
             return;
         }
@@ -2285,6 +2299,9 @@ struct ketogpu_engine {
         KETO_BIDI(9, 128, 64, 6)
         KETO_BIDI(9, 192, 64, 7)
         KETO_BIDI(9, 128, 64, 7)
+#if KETO_F1 != 128
+        KETO_BIDI(9, KETO_F1, 64, 7)
+#endif
         KETO_BIDI(9, 64, 64, 7)
         KETO_BIDI(9, 96, 64, 7)
         KETO_BIDI(8, 128, 64, 7)
@@ -2907,7 +2924,7 @@ struct ketogpu_engine {
                 // last table; one host synchronization for counts and statistics
                 // host batches (src): the run's begin event was recorded ahead of its clear
                 // launch (light_begin) and no event separates the call's kernels
-                const bool direct = src && src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, 128, 7, 16, 1};
+                const bool direct = src && src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, KETO_F1, 7, 16, 1};
                 // (the chunk pipeline's other streams wait for an event after the clear)
                 const bool light = direct && light_begin;
                 hipEvent_t a = light ? light_begin : ev(), b = light ? nullptr : ev();
