@@ -28,5 +28,5 @@ for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
     -d "$OUT/pmc_$tag" -o run -- python3 $B > "$OUT/pmc_$tag.log" 2>&1 \
     || { echo "pmc $C failed"; tail -5 "$OUT/pmc_$tag.log"; exit 1; }
 done
-python3 tools/pmc_traffic.py "$OUT" "$OUT/summary" || exit 1
+python3 tools/pmc_traffic.py "$OUT" "$OUT/summary" --workload "${WORKLOAD:-config2_rbac}" || exit 1
 echo "[profile] done"
