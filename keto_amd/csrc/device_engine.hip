@@ -345,7 +345,11 @@ __global__ __launch_bounds__(kBlock) void hub_mask_kernel(const uint64_t *vis, u
 // closure outgrows the table (or that have a dynamic root) SPILL: 16-request units are
 // re-run as 4-request units, those as single requests, and only single requests whose
 // closure exceeds the table go to the global multi-word engine.
-constexpr int kHashLog = 11;
+// unit_kernel / unit2_kernel LDS table: 2^KETO_U2_HASHLOG slots (build knob for A/B)
+#ifndef KETO_U2_HASHLOG
+#define KETO_U2_HASHLOG 11
+#endif
+constexpr int kHashLog = KETO_U2_HASHLOG;
 constexpr int kHash = 1 << kHashLog;
 constexpr int kHashMax = kHash * 3 / 4;
 constexpr int kChunk = kBlock;
@@ -694,7 +698,13 @@ __global__ __launch_bounds__(256) void patch_rows_kernel(const uint64_t *seg, ui
         }
     }
 }
-constexpr int kFront = 512;  // frontier entries per level (spill beyond)
+// unit2 frontier entries per level (spill beyond).  256 (round 2; 512 before): 25.6 instead
+// of 31 KB of LDS per unit, 6 instead of 5 units per CU for this latency-bound kernel —
+// config #3 at 500M tuples 6.5 -> 7.7 x 10^8 checks/s, 0 spills (Kernels)
+#ifndef KETO_U2_FRONT
+#define KETO_U2_FRONT 256
+#endif
+constexpr int kFront = KETO_U2_FRONT;
 constexpr int kRevCache = 16;
 constexpr int kHubList = 128;  // hubs a unit may reach (spill beyond)
 
