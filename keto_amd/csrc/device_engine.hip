@@ -1048,12 +1048,6 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
 #ifndef KETO_PACK
 #define KETO_PACK 1
 #endif
-// KETO_PUSH1=1: the table word holds visited | EXPANDED bits per direction and "pending"
-// is visited & ~expanded, so a push is ONE 64-bit atomic OR (visited bits, plus expanded
-// bits for lookup-only and dead-end pushes) instead of a visited OR and a second pending OR
-#ifndef KETO_PUSH1
-#define KETO_PUSH1 0
-#endif
 // pending-list entries of the first-stage shape (bidi_kernel<16, 9, KETO_F1, 64, 7>)
 #ifndef KETO_F1
 #define KETO_F1 128
@@ -1235,24 +1229,6 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
     if (bal && lane == __ffsll((unsigned long long)bal) - 1) atomicAdd(&S.n_used, (uint32_t)__popcll(bal));
     bool app = false;
     uint32_t pend = 0;  // requests for which u becomes pending
-#if KETO_PUSH1
-    if (h >= 0) {
-        const int vs = 32 * d;
-        // visited for every bit; expanded too for the bits that must not become pending
-        // (lookup-only requests, dead ends): pending = visited & ~expanded.  The old word
-        // carries the other direction's visited bits (meets, as below) and this direction's
-        // pending bits (a node that had none gets a list entry from this push)
-        const uint32_t E = lk | (deg ? 0u : m);
-        unsigned long long old =
-            atomicOr(&S.st[h], ((unsigned long long)m << vs) | ((unsigned long long)E << (vs + 16)));
-        const uint32_t ov = (uint32_t)(old >> vs) & 0xFFFFu, oe = (uint32_t)(old >> (vs + 16)) & 0xFFFFu;
-        const uint32_t newly = m & ~ov;
-        const uint32_t meet = newly & (uint32_t)(old >> (32 - vs)) & 0xFFFFu;
-        if (meet) atomicOr(&S.found, meet);
-        pend = newly & ~E;  // (meet bits included: found requests drop them at the next take)
-        app = pend && !(ov & ~oe);
-    }
-#else
     if (h >= 0) {
         const int vs = 32 * d;
         // one 64-bit atomic per push: the old word also carries the other direction's
@@ -1268,7 +1244,6 @@ __device__ __forceinline__ void bidi_push(BidiShared<U, HLOG, F, BT, LF> &S, con
             pend = newly;
         }
     }
-#endif
     cost_update<BT>(S, pend, d, deg, false);
     uint32_t idx = lds_append(app, &S.n_p[nxt]);
     if (app) {
@@ -1382,37 +1357,37 @@ __device__ __forceinline__ void bidi_expand(const DevGraph &g, const FRec *frec,
                                             uint64_t &edges) {
     if constexpr (BT == 64) {
         bidi_expand64<U, HLOG, F, BT, LF, SDT>(g, frec, brec, S, L, my_deg, sd, begin, nxt, edges);
-    } else {
-    const uint32_t total = block_scan_sh<BT>(my_deg, S);
-    for (uint32_t eb = 0; eb < total; eb += BT) {
-        uint32_t e = eb + threadIdx.x;
-        bool want = e < total;
-        uint32_t u = 0, deg = 0, bg = 0, m = 0;
-        int d = 0;
-        if (want) {
-            uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
-            while (hi - lo > 1) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (S.c_pre[mid] <= e)
-                    lo = mid;
-                else
-                    hi = mid;
+    } else {  // several waves: block scan + binary search for each edge's entry
+        const uint32_t total = block_scan_sh<BT>(my_deg, S);
+        for (uint32_t eb = 0; eb < total; eb += BT) {
+            uint32_t e = eb + threadIdx.x;
+            bool want = e < total;
+            uint32_t u = 0, deg = 0, bg = 0, m = 0;
+            int d = 0;
+            if (want) {
+                uint32_t lo = 0, hi = k;  // largest j with c_pre[j] <= e
+                while (hi - lo > 1) {
+                    uint32_t mid = (lo + hi) >> 1;
+                    if (S.c_pre[mid] <= e)
+                        lo = mid;
+                    else
+                        hi = mid;
+                }
+                d = (int)((uint32_t)(sd[lo] >> 15) & 1u);
+                m = S.e_mask[lo] & L.active & ~S.found;
+                FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
+                u = rc.node;
+                deg = rc.deg;
+                bg = rc.begin;
+                edges++;
+                if (d && u >= g.Ni) {
+                    bidi_source_meet<U, HLOG, F, BT, LF>(S, u, m);
+                    m = 0;
+                }
+                want = m != 0;
             }
-            d = (int)((uint32_t)(sd[lo] >> 15) & 1u);
-            m = S.e_mask[lo] & L.active & ~S.found;
-            FRec rc = (d ? brec : frec)[(uint64_t)begin[lo] + (e - S.c_pre[lo])];
-            u = rc.node;
-            deg = rc.deg;
-            bg = rc.begin;
-            edges++;
-            if (d && u >= g.Ni) {
-                bidi_source_meet<U, HLOG, F, BT, LF>(S, u, m);
-                m = 0;
-            }
-            want = m != 0;
+            bidi_push<U, HLOG, F, BT, LF>(S, L, want, u, deg, bg, m, d, nxt);
         }
-        bidi_push<U, HLOG, F, BT, LF>(S, L, want, u, deg, bg, m, d, nxt);
-    }
     }
 }
 
@@ -1509,24 +1484,11 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
                     rslot = h;
                 else
                     tslot = h;
-#if KETO_PUSH1
-                // t == r: t is not backward-visited (a meet needs >= 1 edge) and, pending
-                // being visited & ~expanded, cannot be left pending: its reverse row is read
-                // with the eager rows
-                const bool pend = !(eager || (side == 1 && t == r)) && deg;
-                unsigned long long bits = 0;
-                if (side == 0 || t != r)
-                    bits = ((unsigned long long)bit << (32 * side)) |
-                           (pend ? 0ull : (unsigned long long)bit << (32 * side + 16));
-                unsigned long long old = atomicOr(&S.st[h], bits);
-                app = pend && !((uint32_t)(old >> (32 * side)) & ~(uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
-#else
                 const bool pend = !eager && deg;
                 unsigned long long bits = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
                 if (pend) bits |= (unsigned long long)bit << (32 * side + 16);
                 unsigned long long old = atomicOr(&S.st[h], bits);
                 app = pend && !((uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
-#endif
                 if (pend) atomicAdd(&S.cost[side][tid], deg);
             }
             uint32_t idx = lds_append(app, &S.n_p[0]);
@@ -1544,16 +1506,10 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
         }
         if (tid < U) {  // eager rows (zero degree when not eager or not active)
             const bool e = v && eager;
-#if KETO_PUSH1
-            const bool et = v && (eager || t == r);  // (t == r: see the seeds above)
-            if (et && tdeg > 0xFFFFu) S.spill = 1;
-#else
-            const bool et = e;
-#endif
 #if KETO_PACK
             S.p_sdd[1][tid] = (e ? rdeg : 0u) << 16;  // eager degrees <= seed_max (< 65536)
             S.p_begin[1][tid] = (uint32_t)fb;
-            S.p_sdd[1][U + tid] = (1u << 15) | ((et ? tdeg : 0u) << 16);
+            S.p_sdd[1][U + tid] = (1u << 15) | ((e ? tdeg : 0u) << 16);
             S.p_begin[1][U + tid] = (uint32_t)rb;
 #else
             S.e_sd[tid] = 0;
@@ -1561,7 +1517,7 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             S.e_deg[tid] = e ? rdeg : 0;
             S.e_sd[U + tid] = (uint16_t)(1u << 15);
             S.e_begin[U + tid] = (uint32_t)rb;
-            S.e_deg[U + tid] = et ? tdeg : 0;
+            S.e_deg[U + tid] = e ? tdeg : 0;
 #endif
         }
         if (tid < 2 * U) S.e_mask[tid] = (uint16_t)(1u << (tid % U));
@@ -1600,16 +1556,9 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
             const int j = tid & 15;
             const bool fc = a && !cf, bc = a && !cb;
             // seed rows still unread (only needed when a side is closed)
-#if KETO_PUSH1
-            const unsigned long long wr = a ? S.st[rslot] : 0ull, wt = a ? S.st[tslot] : 0ull;
-            const bool rpend = a && ((wr >> j) & ~(wr >> (16 + j)) & 1ull);
-            const bool rp = bc && rpend;
-            const bool tpend = a && ((wt >> (32 + j)) & ~(wt >> (48 + j)) & 1ull);
-#else
             const bool rpend = a && ((S.st[rslot] >> (16 + j)) & 1ull);
             const bool rp = bc && rpend;
             const bool tpend = a && ((S.st[tslot] >> (48 + j)) & 1ull);
-#endif
             const bool tp = fc && tpend;
             const bool closed = (fc && !tp) || (bc && !rp) || (fc && bc);
             const bool open = a && !closed;
@@ -1658,20 +1607,11 @@ __device__ __forceinline__ void bidi_unit(BidiShared<U, HLOG, F, BT, LF> &S, con
 #endif
                 bg = S.p_begin[cur][i];
                 const uint32_t d = sd >> 15, s = sd & 0x7FFFu;
-#if KETO_PUSH1
-                const unsigned long long w64 = S.st[s];
-                const uint32_t pb = (uint32_t)(w64 >> (32 * d)) & ~(uint32_t)(w64 >> (32 * d + 16)) & 0xFFFFu;
-#else
                 const uint32_t pb = (uint32_t)(S.st[s] >> (32 * d + 16)) & 0xFFFFu;
-#endif
                 take = pb & (d ? L.sel[1] : L.sel[0]);
                 rest = pb & act2 & ~take;
                 clr = pb & ~rest;
-#if KETO_PUSH1
-                if (clr) atomicOr(&S.st[s], (unsigned long long)clr << (32 * d + 16));  // expanded
-#else
                 if (clr) atomicAnd(&S.st[s], ~((unsigned long long)clr << (32 * d + 16)));
-#endif
                 S.e_mask[tid] = (uint16_t)take;
             }
             cost_update<BT>(S, clr, (int)(sd >> 15), dg, true);
