@@ -51,6 +51,12 @@ namespace {
 constexpr int kPB = 256;
 constexpr int kPItems = 4;
 constexpr int kPTile = kPB * kPItems;
+// records per thread of part_apply_kernel (build knob for A/B)
+#ifndef KETO_APPLY_ITEMS
+#define KETO_APPLY_ITEMS 4
+#endif
+constexpr int kAItems = KETO_APPLY_ITEMS;
+constexpr int kATile = kPB * kAItems;
 constexpr uint32_t kMaxWorld = 64;
 
 // Owner of global node id v (the shard layout, shard.cpp): inside each class range —
@@ -328,12 +334,12 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
     __shared__ uint64_t s_wsum[kPB / 64][2];  // per wave: packed append total, touch count
     __shared__ unsigned long long s_base[2];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * kPTile; t0 < n; t0 += (uint64_t)gridDim.x * kPTile) {
-        uint64_t key[kPItems], deg[kPItems];
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kATile; t0 < n; t0 += (uint64_t)gridDim.x * kATile) {
+        uint64_t key[kAItems], deg[kAItems];
         uint32_t app = 0, touched = 0;  // bit it: item it appends / is a vis-only entry
         uint64_t val = 0, tcnt = 0;
 #pragma unroll
-        for (int it = 0; it < kPItems; it++) {
+        for (int it = 0; it < kAItems; it++) {
             const uint64_t i = t0 + (uint64_t)it * kPB + threadIdx.x;
             key[it] = 0;
             deg[it] = 0;
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(kPB) void part_apply_kernel(PartDev P, const ketogp
         uint64_t pos = s_base[0] + incl - val, tpos = s_base[1] + tincl - tcnt;
         for (int k = 0; k < wv; k++) pos += s_wsum[k][0], tpos += s_wsum[k][1];
 #pragma unroll
-        for (int it = 0; it < kPItems; it++) {
+        for (int it = 0; it < kAItems; it++) {
             if ((app >> it) & 1u) {
                 const uint64_t idx = out_base + (pos >> kCntShift);
                 if (idx < P.fe_cap) {
@@ -808,7 +814,7 @@ struct ketogpu_part {
         const uint64_t base = lb + cnt;
         if (n)
             timed(KETOGPU_PART_K_APPLY, 32 * n, [&] {
-                KLAUNCH(part_apply_kernel, dim3((unsigned)std::min<uint64_t>((n + kPTile - 1) / kPTile, 8192)),
+                KLAUNCH(part_apply_kernel, dim3((unsigned)std::min<uint64_t>((n + kATile - 1) / kATile, 8192)),
                         dim3(kPB), 0, stream, P, recv, n, base, &P.ctr[nxt]);
             });
         read_ctr();
