@@ -179,6 +179,8 @@ int ketogpu_snapshot_set_namespaces(const ketogpu_snapshot *base, const ketogpu_
 #define KETOGPU_WRITE_AMBIGUOUS 5  /* shared Subject.String() keys (R4) */
 #define KETOGPU_WRITE_FULL 6       /* a touched row has no free slot left */
 #define KETOGPU_WRITE_RESERVE 7    /* no reserved node id left for a new subject */
+#define KETOGPU_WRITE_FANOUT 8     /* a record count change would re-upload more rows than
+                                      KETOGPU_WRITE_FANOUT_MAX (env, default 65536) */
 typedef struct {
     int32_t applied;          /* 1: written in place; 0: unchanged, see reason */
     int32_t reason;           /* KETOGPU_WRITE_* */

@@ -19,7 +19,7 @@ ORDER_NULLS_LAST = 2  # Postgres row order (include/ketogpu.h KETOGPU_ORDER_NULL
 ORDERS = {"sqlite": 0, "mysql-bin": 0, "cockroach": 0, "postgres": ORDER_NULLS_LAST}
 BUILD_WRITABLE = 4  # rows with free slots: ketogpu_snapshot_write patches in place
 WRITE_REASONS = {0: "applied", 1: "not_writable", 2: "wildcard", 3: "poison", 4: "class", 5: "ambiguous",
-                 6: "full", 7: "reserve"}
+                 6: "full", 7: "reserve", 8: "fanout"}
 NODE_UNION, NODE_LEAF = 0, 1
 
 

@@ -2231,10 +2231,11 @@ struct ketogpu_queries {
     }
 };
 
-// pinned buffers handed out by ketogpu_host_alloc: base -> (bytes, device view)
+// pinned buffers handed out by ketogpu_host_alloc: base -> (bytes, the view of every
+// device that has read it; filled on first use with hipHostGetDevicePointer on that device)
 struct PinnedRange {
     size_t bytes;
-    uintptr_t dev;
+    std::map<int, uintptr_t> dev;  // device -> its view (0: the device cannot map it)
 };
 static std::mutex g_pinned_mu;
 static std::map<uintptr_t, PinnedRange> g_pinned;
@@ -2450,7 +2451,7 @@ struct ketogpu_engine {
     // upload of the packed rows and one scatter launch; called under the snapshot's shared
     // lock before every traversal.
     uint64_t synced_version = 0;
-    size_t patch_pos = 0;
+    uint64_t patch_pos = 0;  // absolute position in the snapshot's patch log
     // what edge records carry about the node they point at: its forward row's interior
     // successors and its reverse row's interior predecessors.  In a writable layout only the
     // real entries count (they come first; the free slots after them are never read through
@@ -2469,7 +2470,10 @@ struct ketogpu_engine {
         if (!s.writable || synced_version == s.version) return 0;
         HIP_CHECK(hipSetDevice(device));
         std::vector<uint32_t> fr, rr;
-        for (size_t i = patch_pos; i < s.patches.size(); i++) (s.patches[i].rev ? rr : fr).push_back(s.patches[i].node);
+        for (uint64_t i = patch_pos; i < s.patch_end(); i++) {
+            const Snapshot::Patch &pt = s.patches[i - s.patch_base];
+            (pt.rev ? rr : fr).push_back(pt.node);
+        }
         for (auto *v : {&fr, &rr}) {
             std::sort(v->begin(), v->end());
             v->erase(std::unique(v->begin(), v->end()), v->end());
@@ -2507,16 +2511,19 @@ struct ketogpu_engine {
             for (void *p : {(void *)d_seg, (void *)d_cols, (void *)d_recs}) (void)hipFree(p);
         }
         g.N = s.N;
-        patch_pos = s.patches.size();
+        patch_pos = s.patch_end();
+        s.reader_at(this, patch_pos);
         synced_version = s.version;
         return nseg;
     }
 
     ~ketogpu_engine() {
-        if (stream) {
-            (void)hipSetDevice(device);
-            (void)hipStreamSynchronize(stream);
-        }
+        if (snap) snap->reader_gone(this);
+        // every stream of the engine drains before anything it may read or write is freed
+        // (the chunk pipeline's copies run on copy_stream and its launches on stream2)
+        (void)hipSetDevice(device);
+        for (hipStream_t x : {stream, stream2, copy_stream})
+            if (x) (void)hipStreamSynchronize(x);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         for (void *p : owned) (void)hipFree(p);
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
@@ -3354,13 +3361,26 @@ struct ketogpu_engine {
     // (pageable memory goes through DMA copies).
     const uint32_t *device_view(const uint32_t *p, bool query = true) {
         if (!p) return nullptr;
-        {  // buffers of ketogpu_host_alloc: known without a runtime query (~10 us per call)
+        {  // buffers of ketogpu_host_alloc (portable + mapped): the view of THIS device,
+           // known without a runtime query (~10 us per call) after its first use here
             std::lock_guard<std::mutex> lk(g_pinned_mu);
             auto it = g_pinned.upper_bound((uintptr_t)p);
             if (it != g_pinned.begin()) {
                 --it;
                 const uintptr_t off = (uintptr_t)p - it->first;
-                if (off < it->second.bytes && it->second.dev) return (const uint32_t *)(it->second.dev + off);
+                if (off < it->second.bytes) {
+                    auto d = it->second.dev.find(device);
+                    if (d == it->second.dev.end()) {
+                        void *v = nullptr;  // the caller has made `device` current
+                        if (hipHostGetDevicePointer(&v, (void *)it->first, 0) != hipSuccess) {
+                            (void)hipGetLastError();
+                            v = nullptr;
+                        }
+                        d = it->second.dev.emplace(device, (uintptr_t)v).first;
+                    }
+                    if (d->second) return (const uint32_t *)(d->second + off);
+                    return nullptr;  // not mappable here: DMA path
+                }
             }
         }
         if (!query) return nullptr;
@@ -3532,7 +3552,8 @@ int ketogpu_engine_new(const ketogpu_snapshot *s, const ketogpu_engine_opts *opt
     std::shared_lock<std::shared_mutex> rd(snap.mu);
     e->init(snap, opts);
     e->synced_version = snap.version;  // built from the current rows
-    e->patch_pos = snap.patches.size();
+    e->patch_pos = snap.patch_end();
+    snap.reader_at(e.get(), e->patch_pos);
     *out = e.release();
     API_END
 }
@@ -3587,14 +3608,11 @@ int ketogpu_host_alloc(size_t bytes, void **out) {
     if (!out) throw Error(KETOGPU_EINVAL, "null argument");
     *out = nullptr;
     const size_t n = std::max<size_t>(bytes, 1);
-    HIP_CHECK(hipHostMalloc(out, n, hipHostMallocDefault));
-    void *dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, *out, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        dev = nullptr;
-    }
+    // portable: pinned for every device of the process (a MultiEngine reads one batch
+    // buffer from all of them); mapped: each device reads it in place through its own view
+    HIP_CHECK(hipHostMalloc(out, n, hipHostMallocPortable | hipHostMallocMapped));
     std::lock_guard<std::mutex> lk(g_pinned_mu);
-    g_pinned[(uintptr_t)*out] = PinnedRange{n, (uintptr_t)dev};
+    g_pinned[(uintptr_t)*out] = PinnedRange{n, {}};
     API_END
 }
 

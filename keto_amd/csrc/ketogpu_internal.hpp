@@ -12,9 +12,13 @@
 //     state only covers interior nodes (DESIGN.md "Data layout in HBM").
 #pragma once
 
+#include <algorithm>
+#include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
 #include <string>
@@ -188,6 +192,32 @@ struct Snapshot {
         uint32_t node;
     };
     std::vector<Patch> patches;         // device rows changed, in write order (engines replay)
+    uint64_t patch_base = 0;            // patches trimmed off the front (absolute index of patches[0])
+    // engines over this snapshot -> the absolute patch position each has replayed up to;
+    // a write trims the log below the smallest (an engine must be freed before its snapshot)
+    mutable std::mutex readers_mu;
+    mutable std::map<const void *, uint64_t> readers;
+    void reader_at(const void *who, uint64_t pos) const {
+        std::lock_guard<std::mutex> lk(readers_mu);
+        readers[who] = pos;
+    }
+    void reader_gone(const void *who) const {
+        std::lock_guard<std::mutex> lk(readers_mu);
+        readers.erase(who);
+    }
+    uint64_t patch_end() const { return patch_base + patches.size(); }
+    // under the exclusive write lock: drop what every engine has replayed
+    void trim_patches() {
+        uint64_t lo = patch_end();
+        {
+            std::lock_guard<std::mutex> lk(readers_mu);
+            for (auto &kv : readers) lo = std::min(lo, kv.second);
+        }
+        if (lo > patch_base) {
+            patches.erase(patches.begin(), patches.begin() + (ptrdiff_t)(lo - patch_base));
+            patch_base = lo;
+        }
+    }
     mutable std::shared_mutex mu;       // writes exclusive; engine, resolve and expand calls shared
 
     // ---- helpers

@@ -18,6 +18,7 @@
 // capacities never change between rebuilds, so no record outside a touched row changes.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -408,7 +409,7 @@ struct Writer {
     // final content of one device row region [b, e) whose free slots hold `pad`; the real
     // entries are the sorted prefix below `pad`
     static bool rewrite(std::vector<uint32_t> &col, uint64_t b, uint64_t e, uint32_t pad, std::vector<uint32_t> add,
-                        std::vector<uint32_t> rem, bool commit) {
+                        std::vector<uint32_t> rem, bool commit, size_t *real_after = nullptr) {
         std::vector<uint32_t> cur;
         for (uint64_t i = b; i < e && col[i] != pad; i++) cur.push_back(col[i]);
         std::sort(add.begin(), add.end());
@@ -416,6 +417,7 @@ struct Writer {
         std::vector<uint32_t> tmp, out;
         std::set_difference(cur.begin(), cur.end(), rem.begin(), rem.end(), std::back_inserter(tmp));
         std::set_union(tmp.begin(), tmp.end(), add.begin(), add.end(), std::back_inserter(out));
+        if (real_after) *real_after = out.size();
         if (out.size() > e - b) return false;
         if (commit) {
             std::copy(out.begin(), out.end(), col.begin() + b);
@@ -430,20 +432,30 @@ struct Writer {
     }
     std::vector<uint32_t> fcount_changed, icount_changed;  // nodes whose record fields changed
 
+    // Rows re-uploaded because a record's count field changed (commit's second pass): one
+    // nested-group insert into a hub group would re-upload the forward row of every one of
+    // its (millions of) predecessors, so past this budget the write is refused
+    // (KETOGPU_WRITE_FANOUT) and VersionedEngine rebuilds instead.
+    static uint64_t fanout_budget() {
+        const char *v = getenv("KETOGPU_WRITE_FANOUT_MAX");
+        return v ? strtoull(v, nullptr, 10) : (uint64_t)1 << 16;
+    }
+
     // check (commit = false) or apply (commit = true) the device row edits
     uint64_t device(bool commit) {
         auto id = [&](uint32_t s) { return (s & kNew) ? S.N + (s & ~kNew) : s; };
-        uint64_t rows = 0;
+        uint64_t rows = 0, fanout = 0;
         for (auto &[v, ed] : fwd) {
             const uint32_t before = real(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df);
-            if (!rewrite(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df, ed.add, ed.rem, commit))
+            size_t after = 0;
+            if (!rewrite(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df, ed.add, ed.rem, commit, &after))
                 throw Refuse{KETOGPU_WRITE_FULL};
-            if (commit) {
-                S.patches.push_back({0, v});
-                // only an interior node is pointed at by forward records
-                if (v < S.Ni && real(S.fint_col, S.fint_off[v], S.fint_off[v + 1], S.Df) != before)
-                    fcount_changed.push_back(v);
+            // only an interior node is pointed at by forward records
+            if (v < S.Ni && after != before) {
+                fanout += S.rev_off[v + 1] - S.rev_off[v];
+                if (commit) fcount_changed.push_back(v);
             }
+            if (commit) S.patches.push_back({0, v});
             rows++;
         }
         for (auto &[s0, ed] : rev) {
@@ -457,8 +469,13 @@ struct Writer {
                 uint64_t m = b;
                 while (m < e && S.rev_col[m] < S.Ni) m++;
                 const uint32_t before = real(S.rev_col, b, m, S.Dbi);
-                ok = rewrite(S.rev_col, b, m, S.Dbi, ai, ri, commit) && rewrite(S.rev_col, m, e, S.Dbo, ao, ro, commit);
-                if (ok && commit && real(S.rev_col, b, m, S.Dbi) != before) icount_changed.push_back(u);
+                size_t after = 0;
+                ok = rewrite(S.rev_col, b, m, S.Dbi, ai, ri, commit, &after) &&
+                     rewrite(S.rev_col, m, e, S.Dbo, ao, ro, commit);
+                if (ok && after != before) {
+                    fanout += S.node_row[u].len;
+                    if (commit) icount_changed.push_back(u);
+                }
             } else {
                 std::vector<uint32_t> add(ai), rem(ri);
                 add.insert(add.end(), ao.begin(), ao.end());
@@ -469,6 +486,7 @@ struct Writer {
             if (commit) S.patches.push_back({1, u});
             rows++;
         }
+        if (!commit && fanout > fanout_budget()) throw Refuse{KETOGPU_WRITE_FANOUT};
         return rows;
     }
 
@@ -551,6 +569,7 @@ struct Writer {
         for (auto &[v, ed] : fwd) st.num_interior_edges += ed.add.size() - ed.rem.size();
         for (auto &[s, ed] : rev) st.num_rev_edges += ed.add.size() - ed.rem.size();
         S.version++;
+        S.trim_patches();  // the log keeps only what some engine has not replayed yet
         res.applied = 1;
         res.reason = KETOGPU_WRITE_APPLIED;
         res.rows_inserted = n_ins;

@@ -25,8 +25,21 @@ reports which path the last transaction took and its cost.
 import threading
 import time
 
+from . import _lib as L
 from . import check, expand, persistence
 from .relationtuple import InternalRelationTuple, NilSubject
+
+
+class _Failed:
+    """stands in for the check engine after a committed write could reach no device copy"""
+
+    def __init__(self, sync_err, rebuild_err):
+        self.why = f"sync failed ({sync_err}); rebuild failed ({rebuild_err})"
+
+    def __getattr__(self, name):
+        def fail(*a, **k):
+            raise L.KetoError(L.EDEVICE, "no engine holds the last committed write: " + self.why)
+        return fail
 
 
 class VersionedEngine:
@@ -63,9 +76,18 @@ class VersionedEngine:
             t0 = time.perf_counter()
             res = snap.write(ins, dele)  # reason "not_writable" on a snapshot without free slots
             if res["applied"]:
-                sync_ms, rows = eng.sync()  # the patched device rows, before returning
-                self.last_write = dict(res, path="in_place", sync_ms=sync_ms, synced_rows=rows,
-                                       ms=(time.perf_counter() - t0) * 1e3)
+                # the write is in the shared host snapshot from here on: it is committed
+                # whatever happens to the device copy, so a failed sync must not turn into
+                # a failed transaction (TransactRelationTuples is all-or-nothing)
+                try:
+                    sync_ms, rows = eng.sync()  # the patched device rows, before returning
+                except L.KetoError as err:
+                    self._recover(snap, err)
+                    self.last_write = dict(res, path="in_place+rebuild", sync_error=str(err),
+                                           ms=(time.perf_counter() - t0) * 1e3)
+                else:
+                    self.last_write = dict(res, path="in_place", sync_ms=sync_ms, synced_rows=rows,
+                                           ms=(time.perf_counter() - t0) * 1e3)
             else:
                 self._install(snap.apply(ins, dele))
                 self.last_write = {"applied": False, "reason": res["reason"], "path": "rebuild",
@@ -73,6 +95,17 @@ class VersionedEngine:
             self.version += 1
             return self.version
 
+    def _recover(self, snap, err):
+        """the device sync of a committed in-place write failed: serve the written snapshot
+        from a freshly built engine (a full upload of its rows).  If that fails too, the
+        engine is left FAILED: every later read raises instead of answering from a device
+        copy that lacks the committed write."""
+        try:
+            self._install(snap.apply((), ()))
+        except L.KetoError as err2:
+            self._state = (snap, _Failed(err, err2), expand.Engine(snap))
+            raise L.KetoError(err2.code, f"write committed, but no engine holds it: sync failed ({err}), "
+                                         f"rebuild failed ({err2}); checks raise until the next write") from err2
 
     def reload_namespaces(self, namespaces):
         """Keto's KeyNamespaces reload (internal/driver/config/provider.go:87-110): the next

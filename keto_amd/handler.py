@@ -86,7 +86,9 @@ def tuple_from_json(d):
     """JSON body of POST /check: {namespace, object, relation, subject_id | subject_set}"""
     if not isinstance(d, dict):
         raise BadRequest("Unable to decode JSON payload: expected an object")
-    if "subject_id" in d and "subject_set" in d:
+    # the reference decodes into *string / *SubjectSet (definitions.go:316-325): a key
+    # holding null is the same as an absent key
+    if d.get("subject_id") is not None and d.get("subject_set") is not None:
         raise BadRequest("exactly one of subject_set or subject_id has to be provided")
     ns, obj, rel = (_json_string(d, k) for k in ("namespace", "object", "relation"))
     subject = None
@@ -197,7 +199,8 @@ class Handler:
         try:
             depth = go_parse_int(raw)  # strconv.ParseInt(s, 0, 0)
         except ValueError as e:
-            return self._error(400, f'strconv.ParseInt: parsing "{raw}": {e}')
+            # Go's Query().Get gives "" for a missing key; strconv quotes with escapes
+            return self._error(400, f"strconv.ParseInt: parsing {json.dumps(raw or '')}: {e}")
         # ketogpu_expand takes an int32: every depth beyond any tree's height acts the same
         depth = max(-1, min(depth, 2**31 - 1))
         subject = SubjectSet(_get(q, "namespace") or "", _get(q, "object") or "", _get(q, "relation") or "")

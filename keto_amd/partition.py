@@ -507,6 +507,13 @@ class PartitionedEngine:
         if (status == L.EINVAL).any():
             from .relationtuple import NilSubject
             raise NilSubject("subject is not allowed to be nil")
+        # a wildcard root (R5: empty namespace/object/relation, relationtuples.go:218-236)
+        # matches every group it filters to; the shard has no node for that union, and the
+        # reference may answer True there, so it is refused rather than answered False
+        bad = np.flatnonzero(self.comm.allreduce_array(status.astype(np.int64), "max") == L.ENOTFOUND)
+        if len(bad):
+            raise L.KetoError(L.EINVAL, f"partitioned engine: {len(bad)} requests have wildcard roots (first index "
+                                        f"{int(bad[0])}); evaluate them with the whole-graph engine")
         return self.check_ids(roots, targets)
 
     def _shrink(self, d, m):

@@ -165,3 +165,47 @@ def test_versioned_engine_reads_its_writes():
         want = randgraph.oracle_store(namespaces, cur).check_batch(reqs)
         got = ve.check_many([rt.InternalRelationTuple(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs])
         assert got == [bool(x) for x in want], step
+
+
+def test_failed_sync_after_in_place_write_still_commits(monkeypatch):
+    """an in-place write is in the shared snapshot before the engine's device
+    sync; a sync that raises must not turn into a failed transaction.  The engine is
+    rebuilt over the written snapshot (version bumped, path reported); when the rebuild
+    fails as well, reads raise instead of answering without the committed write."""
+    from keto_amd import freshness
+
+    built = []
+
+    class StubEngine:  # the device engine's interface, on CPU
+        fail_sync = True
+        fail_new = False
+
+        def __init__(self, snapshot, device=0, **kw):
+            if StubEngine.fail_new:
+                raise L.KetoError(L.EDEVICE, "stub: no device")
+            self.snapshot = snapshot
+            built.append(snapshot)
+
+        def sync(self):
+            if StubEngine.fail_sync:
+                raise L.KetoError(L.EDEVICE, "stub: sync failed")
+            return 0.0, 0
+
+        def check_many(self, tuples):
+            return [False] * len(tuples)
+
+    monkeypatch.setattr(freshness.check, "Engine", StubEngine)
+    rows = [(1, "g", "member", "u1", None, None, None), (1, "d", "viewer", None, 1, "g", "member")]
+    ve = freshness.VersionedEngine(Snapshot.from_rows([("n", 1)], rows, writable=True))
+    t = rt.InternalRelationTuple("n", "g", "member", rt.SubjectID("u2"))
+    assert ve.transact(insert=[t]) == 1
+    assert ve.last_write["path"] == "in_place+rebuild" and "sync failed" in ve.last_write["sync_error"]
+    assert len(built) == 2 and built[-1].stats()["num_rows"] == 3  # rebuilt over the written rows
+    StubEngine.fail_new = True
+    t3 = rt.InternalRelationTuple("n", "g", "member", rt.SubjectID("u3"))
+    # the newest engine syncs fine; make the sync fail again and the rebuild fail too
+    with pytest.raises(L.KetoError, match="write committed"):
+        ve.transact(insert=[t3])
+    assert ve.snapshot.stats()["num_rows"] == 4  # the write is committed in the snapshot
+    with pytest.raises(L.KetoError, match="no engine holds"):
+        ve.check_many([t3])

@@ -43,6 +43,12 @@ def test_json_tuple_rejects_non_string_fields():
             tuple_from_json(bad)
     t = tuple_from_json({"namespace": "n", "object": None, "relation": "r", "subject_set": {"namespace": "a"}})
     assert t == rt.InternalRelationTuple("n", "", "r", rt.SubjectSet("a", "", ""))
+    # *string / *SubjectSet decoding: a key holding null counts as absent (definitions.go:316-325)
+    t = tuple_from_json({"namespace": "n", "object": "o", "relation": "r", "subject_id": "u", "subject_set": None})
+    assert t == rt.InternalRelationTuple("n", "o", "r", rt.SubjectID("u"))
+    with pytest.raises(BadRequest, match="exactly one"):
+        tuple_from_json({"namespace": "n", "object": "o", "relation": "r", "subject_id": "u",
+                         "subject_set": {"namespace": "a"}})
     h = Handler(None, None)  # both routes answer the type error before any engine call
     assert h.post_check(b'{"namespace":"n","object":1,"relation":"r","subject_id":"s"}')[0] == 400
     assert h.post_check(b'{"namespace":"n","object":"o","relation":"r","subject_set":5}')[0] == 400
@@ -59,6 +65,9 @@ def test_max_depth_parses_like_strconv_parseint():
     for s in ("", " 3", "3 ", "08", "0x", "1__0", "_1", "1_", "0b2", "+-1", "9223372036854775808", "1e3", "٣"):
         with pytest.raises(ValueError):
             go_parse_int(s)
+    # a missing max-depth reads as "" (r.URL.Query().Get), quoted like strconv.Quote
+    code, body = Handler(None, None).get_expand("namespace=n")
+    assert code == 400 and 'parsing ""' in str(body)
 
 
 @pytest.fixture

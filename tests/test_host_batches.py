@@ -191,3 +191,28 @@ def test_multi_engine_matches_oracle(rbac):
     with pytest.raises(L.KetoError) as e:
         check.MultiEngine(snap, [0, 0])
     assert e.value.code == L.EINVAL
+
+
+@pytest.mark.gpu
+def test_pinned_subrange_pointers_every_engine(rbac):
+    """requests in ketogpu_host_alloc buffers (portable + mapped) passed as pointers into the
+    middle of the allocation — at an odd request offset, so every device range starts
+    inside it — through Engine and MultiEngine, against the oracle; each device reads
+    through its own view of the buffer"""
+    _gpu()
+    _, snap, roots, targets, want = rbac
+    off, n = 37, len(roots)
+    pr, pt = check.PinnedBuffer(n + off + 5), check.PinnedBuffer(n + off + 5)
+    pr.array[:] = 0xFFFFFFFF
+    pt.array[:] = 0xFFFFFFFF
+    pr.array[off:off + n], pt.array[off:off + n] = roots, targets
+    words = (n + 63) // 64
+    out = check.PinnedBuffer(words + 3, np.uint64)
+    ndev = L.lib().ketogpu_device_count()
+    engines = [check.Engine(snap), check.MultiEngine(snap, list(range(ndev)))]
+    for eng in engines:
+        for k in (0, 1, 2):  # a fresh registry view on the first call, cached after
+            out.array[:] = 0
+            eng.check_ids_raw(pr.p.value + 4 * off, pt.p.value + 4 * off, n, out.p.value + 8 * 3)
+            np.testing.assert_array_equal(check.unpack_bits(out.array[3:3 + words].copy(), n), want)
+            assert not out.array[:3].any()

@@ -318,3 +318,20 @@ def test_partition_device_two_ranks_share_gpu():
     for g in got:
         np.testing.assert_array_equal(g, want)
     assert all(r[0] > 0 for r in rec)
+
+
+def test_wildcard_root_is_refused_not_answered_false():
+    """ketogpu_shard_resolve_batch marks a wildcard root (R5) ENOTFOUND; the
+    reference can answer True there (the union of the groups it filters to), so the
+    partitioned engine raises instead of answering False"""
+    from keto_amd.partition import PartitionedEngine
+    from tests.part_cpu import CpuPartition
+    namespaces, rows, reqs = _case(66)
+    sh = _load(namespaces, rows)
+    eng = PartitionedEngine(sh, local=CpuPartition(sh.view(), words=3), direction="forward")
+    ns, o, r, s = reqs[0]
+    with pytest.raises(L.KetoError, match="wildcard") as e:
+        eng.check_requests(persistence.request_columns(reqs[:5] + [(ns, "", r, s)]))
+    assert e.value.code == L.EINVAL
+    np.testing.assert_array_equal(eng.check_requests(persistence.request_columns(reqs)),
+                                  _want(namespaces, rows, reqs))

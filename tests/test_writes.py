@@ -255,3 +255,25 @@ def test_versioned_engine_writes_in_place_and_reads_them():
             want_tree = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, 3)
             assert got == want_tree, (step, ns, o, r)
     assert paths.count("in_place") >= 5 and "rebuild" in paths, paths
+
+
+def test_hub_fanout_is_refused_past_the_budget(monkeypatch):
+    """a nested-group insert into a group that many documents reference changes
+    the group's interior-successor count, which every predecessor's forward records carry;
+    past KETOGPU_WRITE_FANOUT_MAX re-uploaded rows the write is refused (the engine
+    rebuilds instead) and the snapshot is unchanged"""
+    ns = [("g", 1), ("d", 2)]
+    rows = [(1, "hub", "member", None, 1, "s0", "member"), (1, "s0", "member", "u0", None, None, None),
+            (1, "s0", "member", None, 1, "s1", "member"),  # s1 is interior already
+            (1, "s1", "member", "u1", None, None, None), (1, "s1", "member", None, 1, "s2", "member"),
+            (1, "s2", "member", "u2", None, None, None)]
+    rows += [(2, f"doc{k}", "viewer", None, 1, "hub", "member") for k in range(40)]
+    ins = [(1, "hub", "member", None, 1, "s1", "member")]  # hub's interior successors 1 -> 2
+    w = Snapshot.from_rows(ns, rows, sort=True, writable=True)
+    monkeypatch.setenv("KETOGPU_WRITE_FANOUT_MAX", "10")
+    res = w.write(ins, [])
+    assert not res["applied"] and res["reason"] == "fanout"
+    assert w.version() == 0
+    monkeypatch.setenv("KETOGPU_WRITE_FANOUT_MAX", "1000")
+    res = w.write(ins, [])
+    assert res["applied"] and res["device_rows"] >= 40
