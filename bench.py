@@ -384,7 +384,7 @@ def main_partitioned(a, rank, world, local):
                "dtype": "u32 ids / u64 bitmasks (integer)",
                "data": "synthetic: config #5 RBAC-shape stream generator (keto_amd/csrc/synth.cpp ks_c5), seed 0x4B45544F",
                "config": {"workload": f"config5_partitioned_x{f:g}", **sizes, "checks": n_req,
-                          "mode": "hash-partitioned graph (partition-aware loader), per-level all-to-all",
+                          "mode": "hash-partitioned graph (partition-aware loader), native per-level exchange",
                           "parallelism": f"partition x{world}"},
                "roofline": roof, "cpu_baseline": cpu, "parity": parity,
                "load": {"seconds": round(t_load, 1), "rows": sst["rows"], "rows_per_s": round(sst["rows"] / t_load, 1),
@@ -396,7 +396,9 @@ def main_partitioned(a, rank, world, local):
                "partition": {k: v for k, v in st.items() if k != "kernels"},
                "direction": {0: "forward", 1: "backward"}.get(eng.direction, "undecided"),
                "direction_trials_ns_per_check": {{0: "forward", 1: "backward"}[k]: v for k, v in eng._trial.items()},
-               "exchange": {"records": int(eng.records), "levels": int(eng.levels), "retries": int(eng.retries)},
+               "exchange": dict(eng.stats(), driver="native: ketogpu_part_check_ids (part_round.cpp), "
+                                "RCCL grouped send/recv + all-gather" if world > 1 else
+                                "native: ketogpu_part_check_ids (part_round.cpp), world 1: no exchange"),
                "timed_pass_s": round(t_timed, 4)}
         print(json.dumps(out), flush=True)
     barrier(world)

@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 5 /* 5: writable snapshots (in-place writes, engine sync);
+#define KETOGPU_ABI_VERSION 6 /* 6: partitioned rounds behind the C ABI (comm, part_engine);
+                                 5: writable snapshots (in-place writes, engine sync);
                                  4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
 
 #define KETOGPU_OK 0
@@ -450,6 +451,12 @@ int ketogpu_shard_apply(ketogpu_shard *s, const uint32_t *ids, uint64_t n);
 uint64_t ketogpu_shard_claim_count(const ketogpu_shard *s);
 int ketogpu_shard_claims(const ketogpu_shard *s, uint64_t *pairs, uint64_t capacity, uint64_t *counts);
 int ketogpu_shard_check_claims(ketogpu_shard *s, const uint64_t *pairs, uint64_t n, uint64_t *ambiguous);
+/* The whole exchange above in one collective call over a communicator (below: RCCL or a
+ * transport; NULL = a single rank), every step's status agreed by all ranks: counts ->
+ * set_layout -> queries/answer/apply -> claims/check_claims.  KETOGPU_ECOLLISION: every
+ * rank reloads with another salt; KETOGPU_EINVAL: shared Subject.String() keys (R4). */
+struct ketogpu_comm;
+int ketogpu_shard_exchange(ketogpu_shard *s, struct ketogpu_comm *comm);
 /* ketogpu_resolve_batch for a shard: ids of the requests' roots and targets this rank owns,
  * KETOGPU_NODE_NOT_OWNED for the others (the owner's answer is the one that counts);
  * status ENOTFOUND for wildcard roots (not evaluated partitioned), EINVAL nil subjects */
@@ -554,6 +561,103 @@ int ketogpu_part_stats_get(const ketogpu_part *p, ketogpu_part_stats *out);
 /* on: every kernel launch of the partition is bracketed by hipEvents on its stream (a
  * measurement pass; each event costs a few microseconds of GPU idle) */
 int ketogpu_part_set_timing(ketogpu_part *p, int32_t on);
+
+/* --------------------------------------------- partitioned mode: whole rounds */
+/* The same rounds as above with the exchange inside the library, so a Go host drives a
+ * hash-partitioned PermissionEngine through ONE call per batch, like ketogpu_check_ids
+ * (the engine is built once per process, internal/driver/registry_default.go:158-163;
+ * SubjectIsAllowed's recursion, internal/check/engine.go:33-95, spread over ranks).
+ *
+ * A communicator joins the ranks of one partitioned network (one process per GPU):
+ *   RCCL over xGMI  rank 0: ketogpu_comm_unique_id(id); broadcast id to every rank out of
+ *                   band (a Go host: its own channel; tests: torch.distributed); then every
+ *                   rank ketogpu_comm_new(id, rank, world, device) (ncclCommInitRank,
+ *                   /opt/rocm/include/rccl/rccl.h:220).  Records are exchanged from device
+ *                   memory on the partition's stream: grouped ncclSend/ncclRecv per peer
+ *                   (rccl.h:700-725), counts and statuses by ncclAllGather.
+ *   a transport     ketogpu_comm_from_transport(vtable): the caller moves host bytes (a Go
+ *                   transport; the CPU tests use torch.distributed gloo).
+ * Per BFS level every rank makes one small all-gather (each rank's per-destination record
+ * counts plus its step status — a step that failed anywhere fails the round everywhere,
+ * and a level where no rank sends anything ends the closure: no depth cutoff, R2) and one
+ * all-to-all of the records; a round ends with one all-gather of the ranks' hit bits (the
+ * answer is their OR).  Every rank calls ketogpu_part_check_ids with the same requests and
+ * gets the full answer.  Rounds whose buffers overflow are retried with half the requests
+ * on every rank; KETOGPU_PART_AUTO times one round in each direction (max over ranks, so
+ * every rank decides alike) and keeps the faster. */
+typedef struct ketogpu_comm ketogpu_comm;
+#define KETOGPU_COMM_ID_BYTES 128
+int ketogpu_comm_unique_id(uint8_t id[KETOGPU_COMM_ID_BYTES]);
+int ketogpu_comm_new(const uint8_t id[KETOGPU_COMM_ID_BYTES], int32_t rank, int32_t world, int32_t device,
+                     ketogpu_comm **out);
+#define KETOGPU_REDUCE_MIN 0
+#define KETOGPU_REDUCE_MAX 1
+/* host-memory transport; every callback returns 0 on success.  Collective: every rank
+ * calls the same callbacks in the same order. */
+typedef struct {
+    void *ctx;
+    int32_t rank, world;
+    /* every rank's `bytes` -> recv (world * bytes, rank order) */
+    int (*allgather)(void *ctx, const void *send, void *recv, uint64_t bytes);
+    /* send grouped by destination (send_bytes[world]) -> recv grouped by source
+       (recv_bytes[world], known to the caller) */
+    int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv,
+                     const uint64_t *recv_bytes);
+    /* n u32 values reduced elementwise in place (KETOGPU_REDUCE_MIN / _MAX) */
+    int (*allreduce_u32)(void *ctx, uint32_t *buf, uint64_t n, int32_t op);
+} ketogpu_transport;
+int ketogpu_comm_from_transport(const ketogpu_transport *t, ketogpu_comm **out);
+void ketogpu_comm_free(ketogpu_comm *c);
+int ketogpu_comm_rank(const ketogpu_comm *c);
+int ketogpu_comm_world(const ketogpu_comm *c);
+
+/* ketogpu_shard_resolve_batch combined over the ranks (the owners' answers win):
+ * status ENOTFOUND = a wildcard root (R5), which the partitioned engine does not evaluate;
+ * EINVAL = nil subject.  comm NULL: a single rank. */
+int ketogpu_part_resolve_batch(const ketogpu_shard *s, ketogpu_comm *c, const ketogpu_request_batch *reqs,
+                               uint32_t *roots, uint32_t *targets, int32_t *status);
+
+typedef struct ketogpu_part_engine ketogpu_part_engine;
+#define KETOGPU_PART_AUTO (-1)
+typedef struct {
+    int32_t direction;        /* KETOGPU_PART_FORWARD, _BACKWARD or _AUTO                  */
+    uint64_t record_capacity; /* records per exchange buffer; 0 = the partition's own      */
+} ketogpu_part_engine_opts;
+/* comm NULL: world 1 without any exchange (records stay where the kernels wrote them).
+ * The engine borrows p and c (free it first). */
+int ketogpu_part_engine_new(ketogpu_part *p, ketogpu_comm *c, const ketogpu_part_engine_opts *opts,
+                            ketogpu_part_engine **out);
+/* one batch: every rank passes the same requests (host memory), n any size; allowed_bits
+ * ceil(n/64) words */
+int ketogpu_part_check_ids(ketogpu_part_engine *e, const uint32_t *roots, const uint32_t *targets, size_t n,
+                           uint64_t *allowed_bits);
+typedef struct {
+    int32_t direction;          /* the kept direction (KETOGPU_PART_AUTO before any round) */
+    uint64_t trial_ns[2];       /* auto: ns per request of each direction's trial round     */
+    uint64_t rounds, levels;    /* rounds run (trials and retries included), BFS levels     */
+    uint64_t records_sent, records_received, retries, collectives;
+    double exchange_ms;         /* host wall time inside collectives                        */
+} ketogpu_part_engine_stats;
+int ketogpu_part_engine_stats_get(const ketogpu_part_engine *e, ketogpu_part_engine_stats *out);
+void ketogpu_part_engine_free(ketogpu_part_engine *e);
+
+/* Test hook: the same driver over caller-provided steps in host memory (the CPU tests
+ * play a rank's device steps with them, tests/part_cpu.py; the product passes a
+ * ketogpu_part).  Callbacks mirror ketogpu_part_begin_dir / _emit (pull = 0) /
+ * _pull_emit (pull = 1) / _apply / _expand / _pull_answer / _end / _abort. */
+typedef struct {
+    void *ctx;
+    uint64_t round_words;
+    int (*begin)(void *ctx, const uint32_t *roots, const uint32_t *targets, uint64_t n, int32_t direction);
+    int (*emit)(void *ctx, int32_t pull, ketogpu_record *send, uint64_t capacity, uint64_t *counts);
+    int (*apply)(void *ctx, const ketogpu_record *recv, uint64_t n, uint64_t *frontier);
+    int (*expand)(void *ctx);
+    int (*pull_answer)(void *ctx, const ketogpu_record *recv, uint64_t n);
+    int (*end)(void *ctx, uint64_t *allowed_bits);
+    int (*abort)(void *ctx);
+} ketogpu_part_steps;
+int ketogpu_part_engine_new_steps(const ketogpu_part_steps *steps, ketogpu_comm *c,
+                                  const ketogpu_part_engine_opts *opts, ketogpu_part_engine **out);
 
 /* ------------------------------------------------------------------ expand */
 /* BuildTree(subject, rest_depth).  *out = NULL is the nil tree (JSON null).

@@ -189,6 +189,51 @@ class PartStats(C.Structure):
         return d
 
 
+class PartEngineOpts(C.Structure):
+    _fields_ = [("direction", C.c_int32), ("record_capacity", C.c_uint64)]
+
+
+class PartEngineStats(C.Structure):
+    _fields_ = [("direction", C.c_int32), ("trial_ns", C.c_uint64 * 2)] + [(n, C.c_uint64) for n in (
+        "rounds", "levels", "records_sent", "records_received", "retries", "collectives")] + [
+        ("exchange_ms", C.c_double)]
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_}
+        d["trial_ns"] = [int(x) for x in self.trial_ns]
+        return d
+
+
+PART_AUTO = -1
+REDUCE_MIN, REDUCE_MAX = 0, 1
+COMM_ID_BYTES = 128
+# include/ketogpu.h ketogpu_transport callbacks (host memory; 0 = success)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
+                           C.POINTER(C.c_uint64))
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint64, C.c_int32)
+
+
+class Transport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("rank", C.c_int32), ("world", C.c_int32), ("allgather", ALLGATHER_FN),
+                ("alltoallv", ALLTOALLV_FN), ("allreduce_u32", ALLREDUCE_FN)]
+
+
+# include/ketogpu.h ketogpu_part_steps callbacks (test hook)
+BEGIN_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint64, C.c_int32)
+EMIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64))
+APPLY_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64))
+STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)
+PULL_ANSWER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64)
+END_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64))
+
+
+class PartSteps(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("round_words", C.c_uint64), ("begin", BEGIN_FN), ("emit", EMIT_FN),
+                ("apply", APPLY_FN), ("expand", STEP_FN), ("pull_answer", PULL_ANSWER_FN), ("end", END_FN),
+                ("abort", STEP_FN)]
+
+
 # every symbol declared in include/ketogpu.h, with its ctypes signature
 vp, i32, u32, sz = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
 SIGNATURES = {
@@ -249,6 +294,7 @@ SIGNATURES = {
     "ketogpu_shard_claims": (C.c_int, [vp, vp, C.c_uint64, vp]),
     "ketogpu_shard_check_claims": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ketogpu_shard_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
+    "ketogpu_shard_exchange": (C.c_int, [vp, vp]),
     "ketogpu_shard_stats_get": (C.c_int, [vp, C.POINTER(ShardStats)]),
     "ketogpu_shard_view": (C.c_int, [vp, C.POINTER(ShardGraph)]),
     "ketogpu_part_owner": (C.c_uint32, [vp, u32]),
@@ -267,6 +313,18 @@ SIGNATURES = {
     "ketogpu_part_sync": (C.c_int, [vp]),
     "ketogpu_part_stats_get": (C.c_int, [vp, C.POINTER(PartStats)]),
     "ketogpu_part_set_timing": (C.c_int, [vp, C.c_int32]),
+    "ketogpu_comm_unique_id": (C.c_int, [vp]),
+    "ketogpu_comm_new": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int32, C.POINTER(vp)]),
+    "ketogpu_comm_from_transport": (C.c_int, [C.POINTER(Transport), C.POINTER(vp)]),
+    "ketogpu_comm_free": (None, [vp]),
+    "ketogpu_comm_rank": (C.c_int, [vp]),
+    "ketogpu_comm_world": (C.c_int, [vp]),
+    "ketogpu_part_resolve_batch": (C.c_int, [vp, vp, C.POINTER(RequestBatch), vp, vp, vp]),
+    "ketogpu_part_engine_new": (C.c_int, [vp, vp, C.POINTER(PartEngineOpts), C.POINTER(vp)]),
+    "ketogpu_part_engine_new_steps": (C.c_int, [C.POINTER(PartSteps), vp, C.POINTER(PartEngineOpts), C.POINTER(vp)]),
+    "ketogpu_part_check_ids": (C.c_int, [vp, vp, vp, sz, vp]),
+    "ketogpu_part_engine_stats_get": (C.c_int, [vp, C.POINTER(PartEngineStats)]),
+    "ketogpu_part_engine_free": (None, [vp]),
 }
 
 _lib = None

@@ -42,6 +42,7 @@
 
 #include "device_util.hpp"
 #include "ketogpu_internal.hpp"
+#include "part_round.hpp"
 
 using namespace ketogpu;
 using namespace kdev;
@@ -761,7 +762,7 @@ struct ketogpu_part {
             for (uint32_t g = 0; g < world; g++) counts[g] = 0;
             return overflow_bits() & 4u ? KETOGPU_EINVAL : KETOGPU_ENOMEM;
         }
-        if (n && world == 1) {  // one destination: the records are already grouped
+        if (n && world == 1 && !exchange_pack) {  // one destination: the records are already grouped
             // no copy: the caller hands `send` straight back to apply (its own records),
             // which then reads them where the kernels wrote them (obuf_send, apply)
             counts[0] = n;
@@ -796,6 +797,8 @@ struct ketogpu_part {
         return KETOGPU_OK;
     }
 
+    // an exchange reads `send` (a communicator at world 1): the records are copied there
+    bool exchange_pack = false;
     // world 1: the records of the last emit, left in obuf (pack); applying the caller's
     // `send` buffer then means applying obuf.  obuf is rewritten only by the next seed /
     // expand / pull_emit, all after this apply on the same stream.
@@ -913,6 +916,47 @@ struct ketogpu_part {
         reset(false);
     }
 };
+
+// ------------------------------------------------- steps of the native round driver
+// (part_round.cpp): the C entry points below, so every step keeps its lock and its error
+// reporting
+namespace ketogpu {
+namespace {
+struct DeviceSteps : Steps {
+    ketogpu_part *p;
+    explicit DeviceSteps(ketogpu_part *q) : p(q) {
+        device = true;
+        dev = q->device;
+        stream = q->stream;
+    }
+    uint64_t round_words() override { return p->W; }
+    uint64_t record_capacity() override { return p->P.ocap; }
+    int begin(const uint32_t *r, const uint32_t *t, uint64_t n, int dir) override {
+        return ketogpu_part_begin_dir(p, r, t, n, dir);
+    }
+    int emit(int pull, ketogpu_record *send, uint64_t cap, uint64_t *counts) override {
+        return pull ? ketogpu_part_pull_emit(p, send, cap, counts) : ketogpu_part_emit(p, send, cap, counts);
+    }
+    int apply(const ketogpu_record *recv, uint64_t n, uint64_t *frontier) override {
+        return ketogpu_part_apply(p, recv, n, frontier);
+    }
+    int expand() override { return ketogpu_part_expand(p); }
+    int pull_answer(const ketogpu_record *recv, uint64_t n) override { return ketogpu_part_pull_answer(p, recv, n); }
+    int end(uint64_t *bits) override { return ketogpu_part_end(p, bits); }
+    int abort() override { return ketogpu_part_abort(p); }
+    void sync() override { (void)ketogpu_part_sync(p); }
+    void set_exchange(bool on) override {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->exchange_pack = on;
+    }
+    std::string error() override {
+        const char *e = ketogpu_last_error();
+        return e ? e : "";
+    }
+};
+}  // namespace
+std::unique_ptr<Steps> device_steps(ketogpu_part *p) { return std::make_unique<DeviceSteps>(p); }
+}  // namespace ketogpu
 
 // ------------------------------------------------------------------- C ABI
 #define PAPI_BEGIN try {

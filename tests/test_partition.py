@@ -150,6 +150,55 @@ def _worker(rank, world, port, seed, out_dir, device_steps, direction="auto"):
         dist.destroy_process_group()
 
 
+def _fail_worker(rank, world, port, out_dir):
+    """rank 1's apply fails on its second call: every rank must raise (no rank is left
+    waiting in a collective), and the next batch must be answered normally"""
+    import torch.distributed as dist
+    from keto_amd.partition import PartitionedEngine
+    from tests.part_cpu import CpuPartition
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Failing(CpuPartition):
+        armed = True
+
+        def apply(self, recv, n, frontier):
+            if self.rank == 1 and self.armed and self.calls["apply"] == 2:
+                self.armed = False
+                return L.EINVAL
+            return super().apply(recv, n, frontier)
+    try:
+        namespaces, rows, reqs = _case(67)
+        sh = _load(namespaces, rows)
+        eng = PartitionedEngine(sh, local=Failing(sh.view(), words=4), direction="forward")
+        cols = persistence.request_columns(reqs)
+        try:
+            eng.check_requests(cols)
+            code, msg = 0, ""
+        except L.KetoError as e:
+            code, msg = e.code, str(e)
+        got = eng.check_requests(cols)
+        np.save(os.path.join(out_dir, f"rank{rank}.npy"), got)
+        with open(os.path.join(out_dir, f"err{rank}.txt"), "w") as f:
+            f.write(f"{code}\n{msg}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_step_failure_on_one_rank_fails_every_rank():
+    namespaces, rows, reqs = _case(67)
+    want = _want(namespaces, rows, reqs)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_fail_worker, args=(2, 29680, d), nprocs=2, join=True, start_method="spawn")
+        errs = [open(os.path.join(d, f"err{r}.txt")).read().split("\n", 1) for r in range(2)]
+        got = [np.load(os.path.join(d, f"rank{r}.npy")) for r in range(2)]
+    assert [int(e[0]) for e in errs] == [L.EINVAL, L.EINVAL]
+    assert "apply" in errs[1][1] and "another rank" in errs[0][1]
+    for g in got:
+        np.testing.assert_array_equal(g, want)
+
+
 def _run_ranks(world, seed, device_steps, port, direction="auto"):
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(world, port, seed, d, device_steps, direction), nprocs=world, join=True,
@@ -335,3 +384,33 @@ def test_wildcard_root_is_refused_not_answered_false():
     assert e.value.code == L.EINVAL
     np.testing.assert_array_equal(eng.check_requests(persistence.request_columns(reqs)),
                                   _want(namespaces, rows, reqs))
+
+
+@pytest.mark.gpu
+def test_partition_device_rccl_world1_matches_oracle():
+    """the native round over a real RCCL communicator (nranks = 1: the records go through
+    grouped ncclSend/ncclRecv to itself, counts and bits through ncclAllGather), the id
+    exchange and request resolution over it too, every answer against the oracle"""
+    from keto_amd import synth
+    from keto_amd.partition import NativeComm, PartitionedEngine, Shard
+    if L.lib().ketogpu_device_count() < 1:
+        pytest.fail("no HIP device visible")
+    w = synth.config5(users=50000, groups=5000, docs=20000, tuples=400_000, checks=12000, seed=29)
+    from oracle import oracle as O
+    st = O.Store(w.namespaces, 100)
+    for cols in w.batches(1 << 16):
+        st.add_columnar(cols)
+    want = st.finalize(presorted=True).check_batch(w.requests(range(w.n_checks)), nthreads=8).astype(bool)
+    comm = NativeComm(device=0, kind="rccl")
+    sh = Shard.load(w.namespaces, lambda: w.batches(1 << 16), native_comm=comm)
+    roots, targets, status = sh.resolve_batch(w.request_batch(), comm)
+    assert not status.any()
+    for direction in ("forward", "backward", "auto"):
+        eng = PartitionedEngine(sh, device=0, direction=direction, comm=comm, record_capacity=1 << 20)
+        np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+        st = eng.stats()
+        assert st["collectives"] > 2 * st["levels"] and st["records_sent"] == st["records_received"] > 0
+    # small buffers: overflowing rounds are retried with fewer requests over RCCL too
+    eng = PartitionedEngine(sh, device=0, direction="backward", comm=comm, record_capacity=4096)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    assert eng.retries > 0
