@@ -188,3 +188,99 @@ def store_from_case(case):
     for t in case["tuples"]:
         st.add_tuple(t)
     return st.finalize()
+
+
+# ----------------------------------------------------------------- keto_sql (B2)
+_SQL_PATH = os.path.join(_HERE, "build", "libketo_sql.so")
+_sql = None
+
+
+def sql_lib():
+    global _sql
+    if _sql is None:
+        if not os.path.exists(_SQL_PATH):
+            build()
+        L = C.CDLL(_SQL_PATH)
+        vp = C.c_void_p
+        L.ks_db_create.restype = vp
+        L.ks_db_create.argtypes = [C.c_char_p, C.c_int]
+        L.ks_db_add_namespace.argtypes = [vp, C.c_int32, C.c_char_p]
+        L.ks_db_add_rows_columnar.argtypes = [vp, C.c_size_t] + [vp] * 14
+        L.ks_db_finish.argtypes = [vp]
+        L.ks_db_free.argtypes = [vp]
+        L.ks_check_batch.argtypes = [vp, C.c_size_t] + [vp] * 8 + [C.c_int, C.c_double, vp, vp,
+                                                                    C.POINTER(C.c_size_t), C.POINTER(C.c_longlong)]
+        _sql = L
+    return _sql
+
+
+SKIPPED = -9
+
+
+class SqlStore:
+    """keto_relation_tuples in a real SQLite file read through the reference's queries
+    (oracle/keto_sql.c: COUNT + ORDER BY/LIMIT/OFFSET per page per expansion), one
+    connection per worker thread.  BASELINE.md B2."""
+
+    def __init__(self, namespaces, page_size=100, path=None):
+        self.L = sql_lib()
+        if path is None:
+            d = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+            path = os.path.join(d, f"keto_sql_{os.getpid()}_{id(self)}.db")
+        self.path = path
+        self.h = self.L.ks_db_create(_b(path), page_size)
+        if not self.h:
+            raise OracleError(EINVAL)
+        for name, nid in namespaces:
+            self.L.ks_db_add_namespace(self.h, nid, _b(name))
+
+    def add_columnar(self, cols):
+        p = lambda a: None if a is None else a.ctypes.data
+        rc = self.L.ks_db_add_rows_columnar(
+            self.h, len(cols["namespace_id"]), p(cols["namespace_id"]), p(cols["object_data"]), p(cols["object_off"]),
+            p(cols["relation_data"]), p(cols["relation_off"]), p(cols["subject_kind"]), p(cols["subject_id_data"]),
+            p(cols["subject_id_off"]), p(cols["ss_namespace_id"]), p(cols["ss_object_data"]),
+            p(cols["ss_object_off"]), p(cols["ss_relation_data"]), p(cols["ss_relation_off"]),
+            p(cols.get("commit_time")))
+        if rc:
+            raise OracleError(rc)
+
+    def finish(self):
+        rc = self.L.ks_db_finish(self.h)
+        if rc:
+            raise OracleError(rc)
+        return self
+
+    def check_batch(self, reqs, nthreads=1, seconds=0.0):
+        """reqs: [(ns, obj, rel, subject dict)] -> (allowed bool array, answered mask, SQL
+        statements issued); requests past the time budget are not answered"""
+        import numpy as np
+        n = len(reqs)
+        keep = []
+
+        def arr(vals):
+            a = (C.c_char_p * n)(*[_b(v if v is not None else "") for v in vals])
+            keep.append(a)
+            return a
+
+        subj = [subject_args(r[3]) for r in reqs]
+        kinds = (C.c_int * n)(*[s[0] for s in subj])
+        allowed = np.zeros(n, dtype=np.uint8)
+        status = np.zeros(n, dtype=np.int32)
+        done, queries = C.c_size_t(), C.c_longlong()
+        self.L.ks_check_batch(self.h, n, arr([r[0] for r in reqs]), arr([r[1] for r in reqs]),
+                              arr([r[2] for r in reqs]), kinds, arr([s[1] for s in subj]), arr([s[2] for s in subj]),
+                              arr([s[3] for s in subj]), arr([s[4] for s in subj]), nthreads, seconds,
+                              allowed.ctypes.data, status.ctypes.data, C.byref(done), C.byref(queries))
+        bad = status[(status != 0) & (status != SKIPPED)]
+        if len(bad):
+            raise OracleError(int(bad[0]))
+        return allowed.astype(bool), status == 0, int(queries.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ks_db_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
