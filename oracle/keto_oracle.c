@@ -11,6 +11,7 @@
 #include "keto_oracle.h"
 
 #include <pthread.h>
+#include <time.h>
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -457,7 +458,15 @@ typedef struct {
     const ko_subj *req;
     char *kbuf;
     size_t kcap;
+    double deadline; /* CLOCK_MONOTONIC seconds; 0 = none (ko_check_batch_budget) */
+    unsigned tick;
 } chk_ctx;
+
+static double mono_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
 
 static int check_one_further(chk_ctx *c, kset *visited, const ko_query *q);
 
@@ -494,6 +503,8 @@ static int subject_is_allowed(chk_ctx *c, kset *visited, const ko_page *rels) {
 
 /* checkOneIndirectionFurther (internal/check/engine.go:69-91) */
 static int check_one_further(chk_ctx *c, kset *visited, const ko_query *q) {
+    /* a per-request time budget (test harness only: the reference has none) */
+    if (c->deadline > 0 && !(++c->tick & 255) && mono_s() > c->deadline) return KO_ETIMEOUT;
     ko_page pg = {0};
     int rc = 0;
     for (int page = 1;; page++) {
@@ -536,21 +547,27 @@ static int make_subj(int kind, const char *sid, const char *sns, const char *sob
     return KO_EINVAL; /* nil subject: relationtuple.ErrNilSubject */
 }
 
-int ko_check(const ko_store *s, const char *ns, const char *obj, const char *rel, int subject_kind,
-             const char *subject_id, const char *ss_ns, const char *ss_obj, const char *ss_rel,
-             int *allowed) {
+static int check_budget(const ko_store *s, const char *ns, const char *obj, const char *rel, int subject_kind,
+                        const char *subject_id, const char *ss_ns, const char *ss_obj, const char *ss_rel,
+                        double seconds, int *allowed) {
     *allowed = 0;
     if (!s->finalized) return KO_EINVAL;
     ko_subj req;
     int e = make_subj(subject_kind, subject_id, ss_ns, ss_obj, ss_rel, &req);
     if (e) return e;
-    chk_ctx c = {s, &req, NULL, 0};
+    chk_ctx c = {s, &req, NULL, 0, seconds > 0 ? mono_s() + seconds : 0, 0};
     ko_query q = {ns ? ns : "", obj ? obj : "", rel ? rel : ""};
     int r = check_one_further(&c, NULL, &q); /* SubjectIsAllowed, engine.go:93-95 */
     free(c.kbuf);
     if (r < 0) return r;
     *allowed = r;
     return KO_OK;
+}
+
+int ko_check(const ko_store *s, const char *ns, const char *obj, const char *rel, int subject_kind,
+             const char *subject_id, const char *ss_ns, const char *ss_obj, const char *ss_rel,
+             int *allowed) {
+    return check_budget(s, ns, obj, rel, subject_kind, subject_id, ss_ns, ss_obj, ss_rel, 0, allowed);
 }
 
 typedef struct {
@@ -561,6 +578,7 @@ typedef struct {
     const int *kind;
     uint8_t *allowed;
     int *status;
+    double budget; /* seconds per request, 0 = none */
     atomic_size_t next;
 } batch_job;
 
@@ -570,9 +588,9 @@ static void *batch_worker(void *arg) {
         size_t i = atomic_fetch_add(&j->next, 1);
         if (i >= j->n) break;
         int a = 0;
-        j->status[i] = ko_check(j->s, j->ns[i], j->obj[i], j->rel[i], j->kind[i], j->sid ? j->sid[i] : NULL,
-                                j->sns ? j->sns[i] : NULL, j->sobj ? j->sobj[i] : NULL,
-                                j->srel ? j->srel[i] : NULL, &a);
+        j->status[i] = check_budget(j->s, j->ns[i], j->obj[i], j->rel[i], j->kind[i], j->sid ? j->sid[i] : NULL,
+                                    j->sns ? j->sns[i] : NULL, j->sobj ? j->sobj[i] : NULL,
+                                    j->srel ? j->srel[i] : NULL, j->budget, &a);
         j->allowed[i] = (uint8_t)a;
     }
     return NULL;
@@ -582,8 +600,17 @@ int ko_check_batch(const ko_store *s, size_t n, const char *const *ns, const cha
                    const char *const *rel, const int *subject_kind, const char *const *subject_id,
                    const char *const *ss_ns, const char *const *ss_obj, const char *const *ss_rel,
                    int nthreads, uint8_t *allowed, int *status) {
+    return ko_check_batch_budget(s, n, ns, obj, rel, subject_kind, subject_id, ss_ns, ss_obj, ss_rel, nthreads, 0,
+                                 allowed, status);
+}
+
+int ko_check_batch_budget(const ko_store *s, size_t n, const char *const *ns, const char *const *obj,
+                          const char *const *rel, const int *subject_kind, const char *const *subject_id,
+                          const char *const *ss_ns, const char *const *ss_obj, const char *const *ss_rel,
+                          int nthreads, double seconds_per_request, uint8_t *allowed, int *status) {
     batch_job j;
     memset(&j, 0, sizeof j);
+    j.budget = seconds_per_request;
     j.s = s; j.n = n; j.ns = ns; j.obj = obj; j.rel = rel; j.sid = subject_id; j.sns = ss_ns;
     j.sobj = ss_obj; j.srel = ss_rel; j.kind = subject_kind; j.allowed = allowed; j.status = status;
     atomic_init(&j.next, 0);

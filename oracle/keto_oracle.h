@@ -40,6 +40,7 @@ extern "C" {
 #define KO_ENOTFOUND (-1) /* herodot.ErrNotFound                      */
 #define KO_EINVAL (-2)    /* malformed input / nil subject            */
 #define KO_ENOMEM (-3)
+#define KO_ETIMEOUT (-4)  /* ko_check_batch_budget: the request's time budget ran out */
 
 #define KO_SUBJECT_ID 0
 #define KO_SUBJECT_SET 1
@@ -81,6 +82,13 @@ int ko_check_batch(const ko_store *s, size_t n, const char *const *ns, const cha
                    const char *const *rel, const int *subject_kind, const char *const *subject_id,
                    const char *const *ss_ns, const char *const *ss_obj, const char *const *ss_rel,
                    int nthreads, uint8_t *allowed, int *status);
+
+/* ko_check_batch with a time budget per request (the full-size pins: a negative check of
+ * a power-law graph walks ~10^6 groups); status KO_ETIMEOUT for the requests that ran out */
+int ko_check_batch_budget(const ko_store *s, size_t n, const char *const *ns, const char *const *obj,
+                          const char *const *rel, const int *subject_kind, const char *const *subject_id,
+                          const char *const *ss_ns, const char *const *ss_obj, const char *const *ss_rel,
+                          int nthreads, double seconds_per_request, uint8_t *allowed, int *status);
 
 /* BuildTree; *json receives the tree as the reference's JSON (or "null"); free with ko_free */
 int ko_expand(const ko_store *s, int subject_kind, const char *subject_id, const char *ss_ns,

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libketo_oracle.so")
 _lib = None
 
-OK, ENOTFOUND, EINVAL, ENOMEM = 0, -1, -2, -3
+OK, ENOTFOUND, EINVAL, ENOMEM, ETIMEOUT = 0, -1, -2, -3, -4
 SUBJECT_ID, SUBJECT_SET, SUBJECT_NIL = 0, 1, -1
 
 
@@ -40,6 +40,8 @@ def lib():
         L.ko_num_rows.restype = C.c_size_t
         L.ko_check.argtypes = [vp, cp, cp, cp, C.c_int, cp, cp, cp, cp, C.POINTER(C.c_int)]
         L.ko_check_batch.argtypes = [vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp]
+        L.ko_check_batch_budget.argtypes = [vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_double,
+                                            vp, vp]
         L.ko_expand.argtypes = [vp, C.c_int, cp, cp, cp, cp, C.c_int, C.POINTER(C.c_void_p)]
         L.ko_get_page.argtypes = [vp, cp, cp, cp, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
         L.ko_free.argtypes = [vp]
@@ -163,6 +165,31 @@ class Store:
             raise OracleError(int(status[status != 0][0]))
         return allowed.astype(bool)
 
+    def check_batch_budget(self, reqs, nthreads=1, seconds=60.0):
+        """check_batch with a time budget per request -> (allowed, completed mask): a
+        request whose DFS runs out of time is reported, not answered"""
+        import numpy as np
+        n = len(reqs)
+        keep = []
+
+        def arr(vals):
+            a = (C.c_char_p * max(n, 1))(*[_b(v) for v in vals])
+            keep.append(a)
+            return a
+
+        subj = [subject_args(r[3]) for r in reqs]
+        kinds = (C.c_int * max(n, 1))(*[s[0] for s in subj])
+        allowed = np.zeros(max(n, 1), dtype=np.uint8)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        self.L.ko_check_batch_budget(self.h, n, arr([r[0] for r in reqs]), arr([r[1] for r in reqs]),
+                                     arr([r[2] for r in reqs]), kinds, arr([s[1] for s in subj]),
+                                     arr([s[2] for s in subj]), arr([s[3] for s in subj]), arr([s[4] for s in subj]),
+                                     nthreads, seconds, allowed.ctypes.data, status.ctypes.data)
+        bad = status[:n][(status[:n] != OK) & (status[:n] != ETIMEOUT)]
+        if len(bad):
+            raise OracleError(int(bad[0]))
+        return allowed[:n].astype(bool), status[:n] == OK
+
     def expand(self, subject, max_depth):
         kind, sid, sns, sobj, srel = subject_args(subject)
         out = C.c_void_p()
@@ -280,6 +307,94 @@ class SqlStore:
     def close(self):
         if getattr(self, "h", None):
             self.L.ks_db_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+# ------------------------------------------------------------ r2_check (scale pins)
+_R2_PATH = os.path.join(_HERE, "build", "libr2_check.so")
+_r2 = None
+
+
+def r2_lib():
+    global _r2
+    if _r2 is None:
+        if not os.path.exists(_R2_PATH):
+            build()
+        L = C.CDLL(_R2_PATH)
+        vp = C.c_void_p
+        L.kr_new.restype = vp
+        L.kr_new.argtypes = [vp, vp, C.c_size_t]
+        L.kr_add_requests.argtypes = [vp, C.c_size_t] + [vp] * 8
+        L.kr_add_rows_columnar.argtypes = [vp, C.c_size_t] + [vp] * 13
+        L.kr_finish.argtypes = [vp]
+        L.kr_check.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_uint64)]
+        L.kr_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.kr_error.restype = C.c_char_p
+        L.kr_error.argtypes = [vp]
+        L.kr_free.argtypes = [vp]
+        _r2 = L
+    return _r2
+
+
+class R2Checker:
+    """allowed(r, t) <=> r in P(t) or P(t) ∩ X(r) != {} over the raw rows (oracle/r2_check.c):
+    an independent check for graphs the reference DFS cannot finish.  Requests first, then
+    the row stream, then check()."""
+
+    def __init__(self, namespaces, reqs):
+        self.L = r2_lib()
+        ids = (C.c_int32 * max(len(namespaces), 1))(*[i for _, i in namespaces])
+        names = (C.c_char_p * max(len(namespaces), 1))(*[_b(n) for n, _ in namespaces])
+        self.h = self.L.kr_new(ids, names, len(namespaces))
+        n = self.n = len(reqs)
+        keep = self._keep = []
+
+        def arr(vals):
+            a = (C.c_char_p * max(n, 1))(*[_b(v if v is not None else "") for v in vals])
+            keep.append(a)
+            return a
+        subj = [subject_args(r[3]) for r in reqs]
+        kinds = (C.c_int * max(n, 1))(*[s[0] for s in subj])
+        keep.append(kinds)
+        self.L.kr_add_requests(self.h, n, arr([r[0] for r in reqs]), arr([r[1] for r in reqs]),
+                               arr([r[2] for r in reqs]), kinds, arr([s[1] for s in subj]), arr([s[2] for s in subj]),
+                               arr([s[3] for s in subj]), arr([s[4] for s in subj]))
+
+    def add_columnar(self, cols):
+        p = lambda a: None if a is None else a.ctypes.data
+        rc = self.L.kr_add_rows_columnar(
+            self.h, len(cols["namespace_id"]), p(cols["namespace_id"]), p(cols["object_data"]), p(cols["object_off"]),
+            p(cols["relation_data"]), p(cols["relation_off"]), p(cols["subject_kind"]), p(cols["subject_id_data"]),
+            p(cols["subject_id_off"]), p(cols["ss_namespace_id"]), p(cols["ss_object_data"]),
+            p(cols["ss_object_off"]), p(cols["ss_relation_data"]), p(cols["ss_relation_off"]))
+        if rc:
+            raise OracleError(rc) from RuntimeError(self.L.kr_error(self.h).decode())
+        return self
+
+    def check(self, nthreads=1):
+        """-> (allowed bool array, in-scope mask)"""
+        import numpy as np
+        rc = self.L.kr_finish(self.h)
+        if rc:
+            raise OracleError(rc)
+        allowed = np.zeros(max(self.n, 1), dtype=np.uint8)
+        status = np.zeros(max(self.n, 1), dtype=np.int32)
+        visits = C.c_uint64()
+        self.L.kr_check(self.h, nthreads, allowed.ctypes.data, status.ctypes.data, C.byref(visits))
+        self.edge_visits = visits.value
+        return allowed[:self.n].astype(bool), status[:self.n] == 0
+
+    def stats(self):
+        nodes, edges = C.c_uint64(), C.c_uint64()
+        self.L.kr_stats(self.h, C.byref(nodes), C.byref(edges))
+        return {"set_nodes": nodes.value, "set_edges": edges.value}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.kr_free(self.h)
             self.h = None
 
     def __del__(self):

@@ -7,10 +7,12 @@ HBM-resident requests are timed exactly as bench.py times them.
     python tools/bench_scale.py --workload folders --tuples 500000000
     python tools/bench_scale.py --workload social --tuples 1000000000
 
-The CPU oracle cannot hold these graphs next to the engine, so correctness is checked by
-(1) every constructed positive must be allowed and (2) a 100k-request sample must agree
-bit-for-bit with a second engine on the same snapshot that runs the other first stage
-(bidi vs forward-only unit2: bidirectional meet vs closure + reverse pull).
+Correctness at full size: (1) every constructed positive must be allowed, (2) a uniform
+sample must equal oracle/r2_check.c — an independent checker of the R2 formula over the raw
+rows that shares no code with libketogpu (--r2-sample, default 20k) — (3) a sample must
+equal the reference DFS restatement oracle/keto_oracle.c where it finishes within its
+per-request budget (--oracle-sample; its completions and timeouts are reported), and (4) a
+sample must agree with a second engine on the same snapshot running the other first stage.
 A heartbeat line every 30 s keeps long host phases visibly alive.
 """
 import argparse
@@ -93,6 +95,11 @@ def main():
                         "trees of those roots diffed against the oracle's BuildTree")
     p.add_argument("--oracle-seconds", type=float, default=300.0,
                    help="bound on the oracle's check time: the sample is cut to what fits (reported)")
+    p.add_argument("--oracle-request-seconds", type=float, default=20.0,
+                   help="time budget per oracle request: a DFS that outlives it is counted, not waited for")
+    p.add_argument("--r2-sample", type=int, default=20000,
+                   help="uniform requests diffed against oracle/r2_check.c, the independent checker of the R2 "
+                        "formula over the raw rows (no code shared with libketogpu); 0 = off")
     p.add_argument("--expand-sample", type=int, default=None,
                    help="BuildTree roots timed per max-depth (default 200 for folders, config #3's expand; "
                         "0 elsewhere: power-law groups expand into trees of millions of members)")
@@ -134,6 +141,25 @@ def main():
         log(f"oracle store in {time.time() - t0:.1f}s")
         oidx = np.random.default_rng(5).permutation(w.n_checks)[:a.oracle_sample]
         oreqs = w.requests(oidx)
+    r2 = None
+    if a.r2_sample:  # its own interning and adjacency of the raw rows, before they are dropped
+        PHASE[0] = "building the R2 checker"
+        from oracle import oracle as O
+        t0 = time.time()
+        ridx = np.random.default_rng(7).permutation(w.n_checks)[:a.r2_sample]
+        r2c = O.R2Checker(w.namespaces, w.requests(ridx))
+        r2c.add_columnar(w.columns)
+        r2_build = time.time() - t0
+        t0 = time.time()
+        threads = min(16, os.cpu_count() or 1)
+        r2_want, r2_ok = r2c.check(nthreads=threads)
+        r2 = {"against": "oracle/r2_check.c (independent R2 checker: own interning, adjacency and bitset BFS over "
+                         "the raw rows; pinned against keto_oracle.c in tests/test_oracle.py)",
+              "sample": int(r2_ok.sum()), "requested": int(len(ridx)), "build_s": round(r2_build, 1),
+              "check_s": round(time.time() - t0, 1), "threads": threads, **r2c.stats(),
+              "edge_visits": int(r2c.edge_visits)}
+        r2c.close()
+        log(f"R2 checker: {r2}")
     del w  # the rows are no longer needed
     PHASE[0] = "uploading the device graph"
     t0 = time.time()
@@ -163,25 +189,32 @@ def main():
     ref = ref_eng.check_ids(roots[idx], targets[idx])
     xmism = int((ref != got[idx]).sum())
     log(f"cross-check against the {other} engine: {xmism} mismatches of {len(idx)}")
+    if r2 is not None:
+        r2["mismatches"] = int((r2_want[r2_ok] != got[ridx][r2_ok]).sum())
+        log(f"R2 checker parity: {r2['mismatches']} mismatches of {r2['sample']}")
     # a first result line now: a run cut short in the oracle phase still reports the timing
     print(json.dumps({"workload": f"{a.workload}_{a.tuples}", "phase": "timed", "checks": len(roots),
                       "checks_per_s": round(len(roots) * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 4),
                       "plan": check_plan(rs["plan"]), "positives_denied": int((pos & ~got.astype(bool)).sum()),
-                      "cross_check": {"sample": int(len(idx)), "mismatches": xmism}}), flush=True)
+                      "cross_check": {"sample": int(len(idx)), "mismatches": xmism}, "r2_check": r2}), flush=True)
     oracle = None
     if orc is not None:
         PHASE[0] = "oracle sample"
         threads = min(16, os.cpu_count() or 1)
         t0 = time.perf_counter()
-        want, done = [], 0
-        for k in range(0, len(oreqs), threads):  # bounded: one check per thread between budget checks
-            want.append(orc.check_batch(oreqs[k:k + threads], nthreads=threads))
-            done += len(want[-1])
+        mism = done = timed_out = tried = 0
+        step = 4 * threads
+        for k in range(0, len(oreqs), step):  # chunks under a per-request budget: nothing runs unbounded
+            want, ok = orc.check_batch_budget(oreqs[k:k + step], nthreads=threads, seconds=a.oracle_request_seconds)
+            sel = oidx[k:k + step]
+            mism += int((want[ok] != got[sel][ok]).sum())
+            done += int(ok.sum())
+            timed_out += int((~ok).sum())
+            tried += len(sel)
             if time.perf_counter() - t0 > a.oracle_seconds:
                 break
-        want = np.concatenate(want) if want else np.zeros(0, bool)
-        mism = int((want != got[oidx[:done]]).sum())
         oracle = {"against": "oracle/keto_oracle.c", "sample": int(done), "requested": int(len(oidx)),
+                  "tried": int(tried), "timed_out": int(timed_out), "request_budget_s": a.oracle_request_seconds,
                   "mismatches": mism, "seconds": round(time.perf_counter() - t0, 1), "threads": threads,
                   "oracle_checks_per_s": round(done / (time.perf_counter() - t0), 1)}
         log(f"oracle: {oracle}")
@@ -215,7 +248,8 @@ def main():
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),
            "cross_check": {"sample": int(len(idx)), "mismatches": xmism,
                            "against": f"{other} engine without the hub index, same snapshot"},
-           "parity": oracle if oracle is not None else ({"skipped": oracle_skipped} if oracle_skipped else None),
+           "parity": {"r2_check": r2, "oracle": oracle if oracle is not None else
+                      ({"skipped": oracle_skipped} if oracle_skipped else None)},
            "peak_rss_gb": round(rss_gb(), 1),
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
