@@ -209,7 +209,7 @@ def main():
         # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time over
         # the timed HBM-resident runs
         plan = L.RunStats.PLANS.get(st["plan"], "unit")  # KETOGPU_UNITS=auto: the plan the engine kept
-        main = {"bidi": "bidi_kernel<16>", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
+        main = {"bidi": "bidi_kernel<16>", "lite": "lite_kernel", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
         tot = lambda k: sum(r[k] for r in runs)
         fam = {
             main: (tot("main_bytes"), tot("main_ms"), sum(1 for r in runs if r["main_ms"] > 0)),
@@ -279,7 +279,8 @@ def main():
             "pageable_checks_per_s": round(n / t_pageable, 1),
             "hbm_resident_checks_per_s": round((e0 - b0) * a.steps / dt_res, 1),
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
-            "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)" if plan == "bidi" else ""),
+            "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)"
+                            if plan in ("bidi", "lite") else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
                                           "hubs", "hub_build_ms")},

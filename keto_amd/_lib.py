@@ -102,7 +102,7 @@ class RunStats(C.Structure):
         ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double),
         ("plan_unit", C.c_uint32)]
 
-    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit"}
+    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite"}
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

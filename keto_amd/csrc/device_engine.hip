@@ -63,6 +63,10 @@ struct DevGraph {
     const uint32_t *row_amb;  // nullptr when the snapshot has no ambiguous keys
     uint32_t Ni, Nx, N;
     uint32_t both_max, seed_max;  // bidi: both-sides and eager-seed thresholds (kBothMax, kSeedBothMax)
+    // plan lite: added to every row begin an entry carries and taken off the record
+    // arrays' base (0; a test knob, KETOGPU_TEST_BEGIN_SHIFT, that sends every begin
+    // past 2^32 through the 64-bit path)
+    uint64_t seed_shift;
     // hub index for the unit2 kernels (nullptr: off; see ketogpu_engine::build_hubs):
     // hub_of[v] (v < Nx) = hub number or NONE, hub_mask[v][hub_words] (v < Ni) bit h = v is
     // in the closure of hub h; forward edge records carry hub number + 1 in FRec::pad
@@ -1772,6 +1776,412 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
     }
 }
 
+// ----------------------------------------------------------------------- bidi-lite
+// The first stage of plan "lite" (round 3): the bidirectional meet of bidi_kernel with the
+// per-request bookkeeping taken out of the hot loop.  Counters of the round-2 kernel put
+// its instruction issue, not HBM, at the limit (VALU issue 63%, 2,261 VALU + 1,617 SALU
+// per 16-request unit for ~305 edges), and most of those instructions were
+// per-level overhead: per-request pending-degree sums kept with one LDS atomic per lane
+// and request bit on every push and every take (39% of LDS cycles in bank conflicts on
+// the 32-word cost array), per-request direction choice that split every pending entry
+// into taken and carried parts, and a per-level selection over LDS state.  Here:
+//   * the DIRECTION is chosen per unit and level: both sides while both pending degree
+//     totals are small, else the side with the smaller total (sums accumulated in lane
+//     registers during the pushes, one wave reduction per level);
+//   * every direction has its own ring of pending rows, consumed whole when that
+//     direction is expanded (one LDS atomic reads and clears an entry's pending bits);
+//   * per-request closure is pure SGPR bit logic on 16-bit masks: pf / pb = requests with
+//     a pending row in the forward / backward ring (OR of the pushes' new pending bits,
+//     one reduction per level), rpend / tpend = requests whose own seed row is still
+//     unread.  A request is decided false when one side has nothing pending and the other
+//     side's seed row has been read (every path r -> v1 -> ... -> t has v1 in fint(r) and
+//     its last interior node in rev(t)), exactly the rule of bidi_kernel;
+//   * seed rows are addressed with 64-bit begins (sbase), so graphs whose forward or
+//     reverse rows pass 2^32 entries keep this plan as long as the INTERIOR rows (the ids
+//     below Ni come first) fit 32-bit record begins (round-2 verdict item 6).
+// Dead ends are looked up, not stored, as in bidi_kernel.  Same answers, same spill
+// protocol (a spilled unit re-runs on the bidi cascade w, q, s).
+constexpr int kLiteF = 128;  // ring entries per direction
+
+template <int HLOG>
+struct LiteShared {
+    static constexpr int H = 1 << HLOG;
+    static constexpr int HMAX = H * 7 / 8;
+    alignas(16) uint32_t key[H];
+    alignas(16) unsigned long long st[H];  // fwd visited | fwd pending | bwd visited | bwd pending
+    uint32_t ring_sd[2][kLiteF];           // slot | seed << 14 | degree << 16
+    uint32_t ring_bg[2][kLiteF];           // the row's first record; a seed entry: its request
+    unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
+    unsigned long long e_beg[64];          // the chunk's entries' first records
+    uint32_t c_pre[64];                    // owner map
+    uint32_t root[16];
+    uint16_t e_mask[64];
+    uint32_t n_used, spill, found, active;
+    uint32_t head[2], tail[2];
+};
+
+struct LiteLevel {
+    uint32_t lookup, sread;  // for the direction being expanded
+};
+
+// one lane's push of node u (record fields deg / begin) in direction D
+template <int HLOG, int D>
+__device__ __forceinline__ void lite_push(LiteShared<HLOG> &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
+                                          uint32_t begin, uint32_t m, uint32_t &or_acc, uint32_t &deg_acc) {
+    const uint32_t lk = m & (L.lookup | (deg ? 0u : L.sread));
+    int h = -1;
+    bool inserted = false;
+    if (want) {
+        const bool ins = (m & ~lk) != 0;
+        h = bidi_slot<HLOG>(S.key, u, ins, inserted);
+        if (h < 0 && ins) S.spill = 1;
+    }
+    const uint64_t bal = __ballot(inserted);
+    if (bal && (threadIdx.x & 63) == (unsigned)(__ffsll((unsigned long long)bal) - 1))
+        atomicAdd(&S.n_used, (uint32_t)__popcll(bal));
+    bool app = false;
+    if (h >= 0) {
+        // one 64-bit atomic: the old word carries the other direction's visited bits, so of
+        // two pushes that complete a meet the later one sees it
+        const unsigned long long old = atomicOr(&S.st[h], (unsigned long long)m << (32 * D));
+        uint32_t newly = m & ~(uint32_t)(old >> (32 * D)) & 0xFFFFu;
+        const uint32_t meet = newly & (uint32_t)(old >> (32 - 32 * D)) & 0xFFFFu;
+        if (meet) atomicOr(&S.found, meet);
+        newly &= ~(meet | lk);
+        if (newly && deg) {
+            const unsigned long long o2 = atomicOr(&S.st[h], (unsigned long long)newly << (32 * D + 16));
+            app = !((uint32_t)(o2 >> (32 * D + 16)) & 0xFFFFu);
+            or_acc |= newly;
+            deg_acc += app ? deg : 0u;
+        }
+    }
+    const uint32_t idx = lds_append(app, &S.tail[D]);
+    if (app) {
+        if (idx - S.head[D] < (uint32_t)kLiteF && deg <= 0xFFFFu) {
+            S.ring_sd[D][idx & (kLiteF - 1)] = (uint32_t)h | (deg << 16);
+            S.ring_bg[D][idx & (kLiteF - 1)] = begin;
+        } else {
+            S.spill = 1;
+        }
+    }
+}
+
+// Expand this chunk's entries in direction D: lane j holds entry j's degree (0: nothing
+// taken); its mask is S.e_mask[j], its first record S.e_beg[j].  Edge-balanced: an owner
+// map per 64-edge chunk (each entry writes its index at its first position, a prefix max
+// fills the gaps), record loads of the next 64 edges issued before this chunk's pushes.
+template <int HLOG, int D>
+__device__ __forceinline__ void lite_expand(LiteShared<HLOG> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+                                            uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t incl = wave_incl_sum_u32(my_deg);
+    const uint32_t start = incl - my_deg;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (!total) return;
+    rec -= g.seed_shift;  // begins carry the shift (0 outside the test knob)
+    S.c_pre[lane] = 0xFFFFFFFFu;
+    struct Edge {
+        uint32_t lo, ls;
+        FRec rc;
+    };
+    auto fetch = [&](uint32_t eb, Edge &x) {
+        if (my_deg && start < eb + 64 && start + my_deg > eb) S.c_pre[(start > eb ? start : eb) - eb] = lane;
+        __syncthreads();
+        const int o = wave_incl_max_i32((int)S.c_pre[lane]);
+        x.lo = (uint32_t)(o < 0 ? 0 : o);
+        x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
+        const uint32_t e = min(eb + lane, total - 1);
+        x.rc = rec[S.e_beg[x.lo] + (e - x.ls)];
+    };
+    auto push = [&](uint32_t eb, const Edge &x) {
+        const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
+        uint32_t m = 0;
+        if (eb + lane < total) {
+            m = S.e_mask[x.lo] & ~found;
+            edges++;
+            if (D == 1 && x.rc.node >= g.Ni) {  // a source entry of rev(t): it can only meet r itself
+                uint32_t hit = 0;
+                for (uint32_t b = m; b; b &= b - 1)
+                    if (S.root[__ffs(b) - 1] == x.rc.node) hit |= b & (~b + 1);
+                if (hit) atomicOr(&S.found, hit);
+                m = 0;
+            }
+        }
+        lite_push<HLOG, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
+    };
+    Edge a{}, b{};
+    fetch(0, a);
+    if (total <= 64) {  // one chunk (the common level): no pipelining to pay for
+        push(0, a);
+        return;
+    }
+    for (uint32_t eb = 0;;) {
+        fetch(eb + 64, b);
+        push(eb, a);
+        eb += 64;
+        if (eb + 64 >= total) {
+            push(eb, b);
+            break;
+        }
+        fetch(eb + 64, a);
+        push(eb, b);
+        eb += 64;
+        if (eb + 64 >= total) {
+            push(eb, a);
+            break;
+        }
+    }
+}
+
+// consume direction D's ring (every pending row: one atomic reads and clears its pending
+// bits of D) and expand it
+template <int HLOG, int D>
+__device__ __forceinline__ void lite_level(LiteShared<HLOG> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+                                           uint32_t open, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.head[D]);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.tail[D]);
+    for (uint32_t c = h0; c < t0; c += 64) {
+        const uint32_t i = c + lane;
+        uint32_t deg = 0, take = 0;
+        if (i < t0) {
+            const uint32_t w = S.ring_sd[D][i & (kLiteF - 1)], bg = S.ring_bg[D][i & (kLiteF - 1)];
+            const uint32_t s = w & 0x3FFFu;
+            const unsigned long long old = atomicAnd(&S.st[s], ~(0xFFFFull << (32 * D + 16)));
+            take = (uint32_t)(old >> (32 * D + 16)) & open;
+            deg = take ? w >> 16 : 0u;
+            S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & 15] : (unsigned long long)bg + g.seed_shift;
+        }
+        S.e_mask[lane] = (uint16_t)take;
+        if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
+        __syncthreads();
+        lite_expand<HLOG, D>(S, g, rec, L, deg, edges, or_acc, deg_acc);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_or_all(uint32_t x) {
+#pragma unroll
+    for (int s = 32; s; s >>= 1) x |= (uint32_t)__shfl_xor((int)x, s, 64);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ uint32_t wave_sum_all(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(x), 63);
+}
+
+// one 16-request unit by one wave (seed as bidi_load_rows loads it on lanes < 16)
+template <int HLOG>
+__device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g, const FRec *frec, const FRec *brec,
+                                          const BidiSeed &seed, uint64_t *allowed, const uint64_t unit,
+                                          uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats) {
+    using SH = LiteShared<HLOG>;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t c0 = unit * 16;
+    for (int i = lane; i < SH::H / 4; i += 64) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+    for (int i = lane; i < SH::H / 2; i += 64) reinterpret_cast<uint4 *>(S.st)[i] = make_uint4(0, 0, 0, 0);
+    if (lane == 0) S.n_used = S.spill = S.found = S.active = S.head[0] = S.head[1] = S.tail[0] = S.tail[1] = 0;
+    const uint32_t r = seed.r, t = seed.t;
+    uint64_t rows = 0, edges = 0;
+    if (lane < 16) {
+        if (r != KETOGPU_NODE_NONE && r < kDynBase) {
+            rows += 2;
+            if (seed.re > seed.rb) atomicOr(&S.active, 1u << lane);  // nothing reaches a t without predecessors
+        }
+        if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
+        S.root[lane] = r;
+        S.sbase[0][lane] = seed.fb + g.seed_shift;
+        S.sbase[1][lane] = seed.rb + g.seed_shift;
+    }
+    __syncthreads();
+    if (S.spill) {
+        if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+    uint32_t active = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.active);
+    // seeds: r forward-visited and t backward-visited at distance 0 (t = r excluded: a meet
+    // needs >= 1 edge); both rows short: both read at level 0, else both become pending
+    const bool v = lane < 16 && ((active >> lane) & 1u);
+    const uint32_t bit = 1u << (lane & 15);
+    const uint32_t rdeg = (uint32_t)(seed.fe - seed.fb), tdeg = (uint32_t)(seed.re - seed.rb);
+    const bool eager = rdeg <= g.seed_max && tdeg <= g.seed_max;
+    uint32_t pend_mask[2];
+    for (int side = 0; side < 2; side++) {
+        const uint32_t u = side ? t : r, deg = side ? tdeg : rdeg;
+        bool inserted = false;
+        const int h = v ? bidi_slot<HLOG>(S.key, u, true, inserted) : -1;
+        const uint64_t bal = __ballot(inserted);
+        if (lane == 0) S.n_used += (uint32_t)__popcll(bal);
+        const bool pend = h >= 0 && !eager && deg;
+        bool app = false;
+        if (h >= 0) {
+            unsigned long long bits = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
+            if (pend) bits |= (unsigned long long)bit << (32 * side + 16);
+            const unsigned long long old = atomicOr(&S.st[h], bits);
+            app = pend && !((uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
+        }
+        pend_mask[side] = (uint32_t)__ballot(pend);
+        const uint32_t idx = lds_append(app, &S.tail[side]);  // idx < 16 <= kLiteF
+        if (app) {
+            if (deg > 0xFFFFu) S.spill = 1;
+            S.ring_sd[side][idx] = (uint32_t)h | (1u << 14) | (deg << 16);
+            S.ring_bg[side][idx] = lane;
+        }
+    }
+    uint32_t rpend = pend_mask[0], tpend = pend_mask[1];  // seed rows not read yet
+    // pending-row presence and degree totals per direction
+    uint32_t pf = rpend, pb = tpend, sf = 0, sb = 0;
+    uint32_t acc_or[2] = {0, 0}, acc_deg[2] = {0, 0};
+    for (int side = 0; side < 2; side++) {  // the pending seed rows' degrees
+        const uint32_t d = (lane < 16 && ((pend_mask[side] >> lane) & 1u)) ? (side ? tdeg : rdeg) : 0u;
+        (side ? sb : sf) = wave_sum_all(d);
+    }
+    // level 0: the eager seed rows, every push inserts
+    {
+        const LiteLevel L0{0, 0};
+        const bool e = v && eager;
+        for (int side = 0; side < 2; side++) {
+            if (lane < 16) {
+                S.e_mask[lane] = (uint16_t)bit;
+                S.e_beg[lane] = S.sbase[side][lane];
+            }
+            __syncthreads();
+            const uint32_t d = (lane < 16 && e) ? (side ? tdeg : rdeg) : 0u;
+            if (side == 0)
+                lite_expand<HLOG, 0>(S, g, frec, L0, d, edges, acc_or[0], acc_deg[0]);
+            else
+                lite_expand<HLOG, 1>(S, g, brec, L0, d, edges, acc_or[1], acc_deg[1]);
+            __syncthreads();
+        }
+        pf |= wave_or_all(acc_or[0]);
+        pb |= wave_or_all(acc_or[1]);
+        sf += wave_sum_all(acc_deg[0]);
+        sb += wave_sum_all(acc_deg[1]);
+    }
+    bool spilled = false;
+    for (;;) {
+        __syncthreads();
+        const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
+        uint32_t open = active & ~found;
+        if (S.spill || (S.n_used > (uint32_t)SH::HMAX && open)) {  // undecided requests, table over its load
+            spilled = true;
+            break;
+        }
+        const uint32_t fc = open & ~pf, bc = open & ~pb;
+        const uint32_t closed = (fc & ~tpend) | (bc & ~rpend) | (fc & bc);
+        active &= ~closed;
+        open &= ~closed;
+        if (!open) break;
+        const bool want_f = (pf & open) != 0, want_b = (pb & open) != 0;
+        bool do_f, do_b;
+        if (want_f && want_b && sf <= g.both_max && sb <= g.both_max) {
+            do_f = do_b = true;
+        } else if (want_f && want_b) {
+            do_f = sf <= sb;
+            do_b = !do_f;
+        } else {
+            do_f = want_f;
+            do_b = want_b;
+        }
+        // bits of requests whose OTHER side is closed: only looked up (a meet or nothing);
+        // a dead end (no row in this direction) is only looked up once the other side's
+        // seed row was read in an earlier level (it can meet nothing else)
+        if (do_f) {
+            const LiteLevel L{open & bc, ~tpend};
+            acc_or[0] = acc_deg[0] = 0;
+            lite_level<HLOG, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
+        }
+        if (do_b) {
+            const LiteLevel L{open & fc, ~rpend};
+            acc_or[1] = acc_deg[1] = 0;
+            lite_level<HLOG, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
+        }
+        if (do_f) {
+            pf = wave_or_all(acc_or[0]);
+            sf = wave_sum_all(acc_deg[0]);
+            rpend = 0;
+        }
+        if (do_b) {
+            pb = wave_or_all(acc_or[1]);
+            sb = wave_sum_all(acc_deg[1]);
+            tpend = 0;
+        }
+    }
+    __syncthreads();
+    if (spilled || S.spill) {
+        if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        return;
+    }
+#pragma unroll
+    for (int s = 32; s; s >>= 1) {
+        rows += __shfl_down(rows, s, 64);
+        edges += __shfl_down(edges, s, 64);
+    }
+    if (lane == 0) {
+        const uint32_t res = S.found & 0xFFFFu;
+        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
+        atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
+        atomicAdd(&stat_slot(stats)[1], (unsigned long long)edges);
+    }
+}
+
+// plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit)
+__global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, const FRec *brec, const uint32_t *roots,
+                                                  const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                  uint32_t *spill_out, unsigned int *spill_count,
+                                                  unsigned long long *stats, uint64_t unit0) {
+    __shared__ LiteShared<9> S;
+    const uint64_t units = (n + 15) / 16;
+    const uint64_t unit = unit0 + blockIdx.x;
+    uint32_t r, t;
+    bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
+    lite_unit<9>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats);
+}
+
+// plan "lite" first stage over pinned host requests read in place (bidi_host_kernel's
+// prologue: K units per workgroup, requests validated and stored in HBM for the spill stages)
+template <int K>
+__global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+                                                       const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
+                                                       uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
+                                                       unsigned int *spill_count, unsigned long long *stats,
+                                                       unsigned long long *first_bad) {
+    __shared__ LiteShared<9> S;
+    uint32_t r[K], t[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
+        r[k] = t[k] = KETOGPU_NODE_NONE;
+        if (threadIdx.x < 16 && c < n) {
+            r[k] = hr[c];
+            t[k] = ht[c];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
+        if (threadIdx.x < 16 && c < n) {
+            if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
+                atomicMin(first_bad, (unsigned long long)c);
+                r[k] = t[k] = KETOGPU_NODE_NONE;
+            }
+            dr[c] = r[k];
+            dt[c] = t[k];
+        }
+    }
+    const uint64_t units = (n + 15) / 16;
+#pragma unroll 1
+    for (int k = 0; k < K; k++) {
+        const uint64_t unit = (uint64_t)blockIdx.x * K + k;
+        if (unit >= units) break;
+        uint32_t rk = r[0], tk = t[0];
+#pragma unroll
+        for (int j = 1; j < K; j++)
+            if (j == k) rk = r[j], tk = t[j];
+        lite_unit<9>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
+        __syncthreads();
+    }
+}
+
 // bad (may be null): a host batch's first-invalid-request word, reset to "none" here
 // instead of by a separate memset launch
 __global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t *a, uint64_t na, uint64_t *b, uint64_t nb,
@@ -2259,6 +2669,8 @@ struct ketogpu_engine {
     int wave_u = 8;
     bool use_v2 = true;
     bool use_bidi = true;
+    bool use_lite = false;     // plan "lite" available (lite_kernel)
+    bool frec_needed = false;  // forward edge records built (v2, bidi, lite)
     // plan "auto" (default): the first kTrialRuns batches of >= kTrialMin requests run
     // every candidate first stage back to back (each a complete evaluation, in rotating
     // order); the engine then keeps the candidate with the smallest summed time
@@ -2272,6 +2684,7 @@ struct ketogpu_engine {
         bool units = true;    // false: the global path alone (with the hub index)
         int u = 16;           // bidi: requests per first-stage unit
         int wpe = 1;          // bidi: minimum waves per SIMD of the first stage
+        int lite = 0;         // bidi: plan "lite" (lite_kernel)
     };
     std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
@@ -2280,8 +2693,10 @@ struct ketogpu_engine {
         int hlog, bt, f, lf;
         int u = 16;   // requests per unit (16, or 8: half the LDS per unit)
         int wpe = 1;  // minimum waves per SIMD asked of the compiler (bidi_kernel WPE)
+        int lite = 0;  // 1: plan "lite" (lite_kernel: per-unit direction, per-direction rings)
         bool operator==(const BidiCfg &o) const {
-            return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe;
+            return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe &&
+                   lite == o.lite;
         }
     };
     BidiCfg bidi_cfg{9, 64, KETO_F1, 7};
@@ -2290,6 +2705,11 @@ struct ketogpu_engine {
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
+        if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
+            KLAUNCH(lite_kernel, dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets, q.n, q.allowed,
+                    out, out_count, stats, unit0);
+            return;
+        }
         if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
             KLAUNCH((bidi_kernel<16, 9, KETO_F1, 64, 7, 1, 1>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
                     q.targets, q.n, q.allowed, parents, in_count, 1u, out, out_count, stats, stp, unit0);
@@ -2563,11 +2983,36 @@ struct ketogpu_engine {
         const char *plan = getenv("KETOGPU_UNITS");
         std::string p = plan ? plan : "auto";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        use_v2 = p == "v2" || p == "bidi" || p == "auto";
-        if (use_v2 && s.fint_col.size() >= (1ull << 32)) use_v2 = false;  // record begins are u32
-        // bidi: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
-        use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && s.rev_col.size() < (1ull << 32);
-        trials_left = p == "auto" && use_bidi && use_units ? kTrialRuns : 0;
+        const bool lite_req = p == "lite" || p == "auto";
+        use_v2 = p == "v2" || p == "bidi" || lite_req;
+        // Edge records carry 32-bit row begins.  Plan lite reads only INTERIOR rows through
+        // records (ids below Ni come first, so their begins are the smallest) and carries
+        // seed rows' begins in 64 bits: it needs fint_off[Ni] and rev_off[Ni] below 2^32.
+        // bidi and unit2 also keep seed begins in 32 bits: they need every row below 2^32.
+        const bool small_f = s.fint_col.size() < (1ull << 32), small_r = s.rev_col.size() < (1ull << 32);
+        const bool lite_ok = s.fint_off[s.Ni] < (1ull << 32) && s.rev_off[s.Ni] < (1ull << 32);
+        const bool recs = use_v2 && (small_f || (lite_req && lite_ok));
+        auto disabled = [&](const char *what, const char *why) {
+            fprintf(stderr, "[ketogpu] plan %s disabled: %s (fint %llu, rev %llu entries; interior rows %llu / %llu)\n",
+                    what, why, (unsigned long long)s.fint_col.size(), (unsigned long long)s.rev_col.size(),
+                    (unsigned long long)s.fint_off[s.Ni], (unsigned long long)s.rev_off[s.Ni]);
+        };
+        // bidi / lite: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
+        use_lite = lite_req && use_v2 && !s.has_ambiguous && lite_ok;
+        use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && small_f && small_r;
+        if (use_v2 && !small_f) {
+            disabled("v2", "forward rows pass 2^32 entries (32-bit record begins)");
+            use_v2 = false;
+        }
+        if ((p == "bidi" || p == "auto") && !s.has_ambiguous && recs && !use_bidi)
+            disabled("bidi", "rows pass 2^32 entries (32-bit seed begins)");
+        if (lite_req && !s.has_ambiguous && !lite_ok) disabled("lite", "interior rows pass 2^32 entries");
+        frec_needed = recs && (use_v2 || use_bidi || use_lite);
+        if (p == "lite" && use_lite) {  // forced: the lite first stage, no trials
+            use_bidi = true;
+            bidi_cfg.lite = 1;
+        }
+        trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
         const char *bc = getenv("KETOGPU_BIDI");  // "hlog,threads,lists,load", e.g. "9,64,192,6"
         if (bc) {
@@ -2581,9 +3026,13 @@ struct ketogpu_engine {
             // (8-request units — 5 KB of LDS, KETOGPU_BIDI=8,64,64,7,8[,wpe] — measured slower on
             // config #2: 0.48-0.53 vs 0.39 ms, profiles/r01/tune_u8.txt; not a candidate)
             const BidiCfg &c = bidi_cfg;
-            candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0, true, c.u, c.wpe});
-            if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
-            candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
+            if (use_bidi) {
+                candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0, true, c.u, c.wpe});
+                if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
+            }
+            if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
+            if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
+            use_bidi = use_bidi || use_lite;
         }
         if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
             std::vector<SpillStage> c;
@@ -2615,6 +3064,8 @@ struct ketogpu_engine {
         g.Nx = s.Nx;
         g.N = s.N;
         g.both_max = kBothMax;
+        g.seed_shift = 0;
+        if (const char *sh = getenv("KETOGPU_TEST_BEGIN_SHIFT")) g.seed_shift = strtoull(sh, nullptr, 0);
         g.seed_max = kSeedBothMax;
         if (const char *bt = getenv("KETOGPU_BIDI_TUNE")) {  // "both,seed" (tuning runs)
             unsigned a = kBothMax, b = kSeedBothMax;
@@ -2627,7 +3078,7 @@ struct ketogpu_engine {
             has_kids = up(hk);
         }
         choose_hubs(s);
-        if (use_v2) {
+        if (frec_needed) {
             std::vector<FRec> rec(s.fint_col.size());
             for (size_t e = 0; e < rec.size(); e++) {
                 uint32_t u = s.fint_col[e];
@@ -2636,7 +3087,7 @@ struct ketogpu_engine {
             }
             frec = up(rec);
         }
-        if (use_bidi) {
+        if (use_bidi || use_lite) {
             // interior predecessors of v = the prefix of rev(v) below Ni (sorted rows)
             std::vector<uint32_t> id(s.Ni);
             for (uint32_t v = 0; v < s.Ni; v++) id[v] = ideg(s, v);
@@ -2931,7 +3382,7 @@ struct ketogpu_engine {
         }
         uint64_t units = (q.n + 15) / 16;
         uint64_t left = 0;
-        if (use_v2) {
+        if (use_v2 || (use_lite && use_bidi)) {
             // Forward-only plan "v2": the host-driven unit2 cascade unit2<16> -> unit2<4> ->
             // unit2<1> -> global path.
             if (use_bidi) {
@@ -2941,7 +3392,8 @@ struct ketogpu_engine {
                 // last table; one host synchronization for counts and statistics
                 // host batches (src): the run's begin event was recorded ahead of its clear
                 // launch (light_begin) and no event separates the call's kernels
-                const bool direct = src && src->mapped && pipe_direct && bidi_cfg == BidiCfg{9, 64, KETO_F1, 7, 16, 1};
+                const bool direct = src && src->mapped && pipe_direct &&
+                                    (bidi_cfg == BidiCfg{9, 64, KETO_F1, 7, 16, 1} || bidi_cfg.lite);
                 // (the chunk pipeline's other streams wait for an event after the clear)
                 const bool light = direct && light_begin;
                 hipEvent_t a = light ? light_begin : ev(), b = light ? nullptr : ev();
@@ -2957,9 +3409,16 @@ struct ketogpu_engine {
                     // 0.35 / 0.5: 1.85 / 1.83 / 1.90 vs 2.09 x 10^9 checks/s,
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
-    KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec,  \
-            src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],   \
-            st.stats, d_bad)
+    do {                                                                                                   \
+        if (bidi_cfg.lite)                                                                                 \
+            KLAUNCH(lite_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
+                    frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
+                    list[0], &spill_count[0], st.stats, d_bad);                                            \
+        else                                                                                               \
+            KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
+                    frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
+                    list[0], &spill_count[0], st.stats, d_bad);                                            \
+    } while (0)
                     if (host_units == 4)
                         KETO_HOST_K(4);
                     else if (host_units == 2)
@@ -3215,7 +3674,7 @@ struct ketogpu_engine {
                 use_units = c.units;
                 if (!c.units) return;
                 use_bidi = c.bidi;
-                bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf, c.u, c.wpe};
+                bidi_cfg = BidiCfg{c.hlog, c.bt, c.f, c.lf, c.u, c.wpe, c.lite};
             };
             for (size_t k = 0; k < nc; k++) {
                 Candidate &c = candidates[(k + (size_t)trials_left) % nc];  // rotate the order per trial
@@ -3240,7 +3699,7 @@ struct ketogpu_engine {
         Batch q = qq.batch();
         ketogpu_run_stats rs{};
         rs.checks = q.n;
-        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? 1 : use_v2 ? 2 : 4;
+        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? (bidi_cfg.lite ? 5 : 1) : use_v2 ? 2 : 4;
         rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
         rs.plan_unit = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.u : 0;
         rs.hubs = n_hubs;
@@ -3264,7 +3723,7 @@ struct ketogpu_engine {
         // A timing event costs ~5.6 us of GPU idle between the kernels it separates
         // (kernel trace of config #2): with the bidi first stage the run starts at that
         // stage's own start event, recorded right after this point.
-        const bool bidi_first = use_units && !wave_u && use_v2 && use_bidi && q.n;
+        const bool bidi_first = use_units && !wave_u && (use_v2 || use_lite) && use_bidi && q.n;
         if (!bidi_first && !light_begin) HIP_CHECK(hipEventRecord(t_begin, stream));
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
@@ -3432,7 +3891,7 @@ struct ketogpu_engine {
         const uint64_t words = (n + 63) / 64;
         emit_req = EmitReq{};
         clear_bad = nullptr;
-        const bool bidi_ok = n && use_units && !wave_u && use_v2 && use_bidi && !(trials_left && n >= kTrialMin);
+        const bool bidi_ok = n && use_units && !wave_u && (use_v2 || use_lite) && use_bidi && !(trials_left && n >= kTrialMin);
         // KETOGPU_PIPE_DMA=1: pinned requests are copied by DMA (copy engines) instead of
         // read in place by the device (CUs); an A/B knob
         static const bool dma = getenv("KETOGPU_PIPE_DMA") != nullptr;

@@ -47,12 +47,18 @@ def test_nil_subject_is_bad_request():
         eng.SubjectIsAllowed(rt.InternalRelationTuple("n", "o", "r", None))
 
 
-@pytest.fixture(params=["bidi", "bidi-wide", "v2"])
+@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift"])
 def unit_plan(request, monkeypatch):
     """first LDS pass of engines created while active: the default bidirectional units
-    (one-wave, 512-slot tables), bidi with the wide 2048-slot table, or forward-only unit2"""
+    (one-wave, 512-slot tables), bidi with the wide 2048-slot table, forward-only unit2, or
+    plan lite (per-unit direction) — also with every row begin carried past 2^32 through
+    its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT)"""
     if request.param == "v2":
         monkeypatch.setenv("KETOGPU_UNITS", "v2")
+    elif request.param.startswith("lite"):
+        monkeypatch.setenv("KETOGPU_UNITS", "lite")
+        if request.param == "lite-shift":
+            monkeypatch.setenv("KETOGPU_TEST_BEGIN_SHIFT", str(3 << 32))
     else:
         monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     if request.param == "bidi-wide":
@@ -154,7 +160,7 @@ def test_hub_index_default_on_power_law(monkeypatch):
     roots, targets = w.resolve(snap)
     want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
         w.requests(range(len(roots))), nthreads=8)
-    for plan in ("bidi", "v2", "auto"):
+    for plan in ("bidi", "v2", "lite", "auto"):
         monkeypatch.setenv("KETOGPU_UNITS", plan)
         eng = check.Engine(snap)
         for _ in range(3 if plan == "auto" else 1):
@@ -297,7 +303,7 @@ def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
     for _ in range(4):
         np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
         plans.add(eng.last_stats()["plan"])
-    assert plans <= {0, 1, 2}  # global path (with the hub index), bidi, unit2
+    assert plans <= {0, 1, 2, 5}  # global path (with the hub index), bidi, unit2, lite
     kept = eng.last_stats()["plan"]
     np.testing.assert_array_equal(eng.check_ids(roots[:5000], targets[:5000]), want[:5000])
     assert eng.last_stats()["plan"] == kept

@@ -62,15 +62,16 @@ def _pipe_mode(monkeypatch, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["bidi", "lite"])
 @pytest.mark.parametrize("mode", ["direct", "direct1", "direct4", "chunks"])
 @pytest.mark.parametrize("chunk", ["4096", "65536", "1048576"])
-def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, monkeypatch):
-    """bidi plan, host batches: pinned requests read in place by one first-stage launch
-    (direct) or by the chunk pipeline (several chunk sizes: many chunks, a few, one = not
-    pipelined), and pageable host arrays; the HBM-resident run agrees"""
+def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, plan, monkeypatch):
+    """bidi and lite plans, host batches: pinned requests read in place by one first-stage
+    launch (direct) or by the chunk pipeline (several chunk sizes: many chunks, a few, one =
+    not pipelined), and pageable host arrays; the HBM-resident run agrees"""
     _gpu()
     _, snap, roots, targets, want = rbac
-    monkeypatch.setenv("KETOGPU_UNITS", "bidi")
+    monkeypatch.setenv("KETOGPU_UNITS", plan)
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", chunk)
     _pipe_mode(monkeypatch, mode)
     eng = check.Engine(snap)

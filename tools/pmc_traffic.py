@@ -24,6 +24,8 @@ from collections import defaultdict
 FAMILIES = [
     # host batches with pinned requests: the first stage reading its requests in place
     ("bidi_host_kernel (host batches)", r"bidi_host_kernel"),
+    ("lite_host_kernel (host batches)", r"lite_host_kernel"),
+    ("lite_kernel", r"\blite_kernel"),
     # the pipelined host-to-host first stage is its own instantiation (last template
     # argument 1), so a launch per chunk never mixes into the full-batch launch's figures
     ("bidi_kernel<16> (pipelined chunks)", r"bidi_kernel<16, 9, .*, 1>"),
