@@ -1801,16 +1801,16 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
 //     below Ni come first) fit 32-bit record begins (round-2 verdict item 6).
 // Dead ends are looked up, not stored, as in bidi_kernel.  Same answers, same spill
 // protocol (a spilled unit re-runs on the bidi cascade w, q, s).
-constexpr int kLiteF = 128;  // ring entries per direction
+constexpr int kLiteF = 128;  // ring entries per direction (default shape)
 
-template <int HLOG>
+template <int HLOG, int F>
 struct LiteShared {
     static constexpr int H = 1 << HLOG;
     static constexpr int HMAX = H * 7 / 8;
     alignas(16) uint32_t key[H];
     alignas(16) unsigned long long st[H];  // fwd visited | fwd pending | bwd visited | bwd pending
-    uint32_t ring_sd[2][kLiteF];           // slot | seed << 14 | degree << 16
-    uint32_t ring_bg[2][kLiteF];           // the row's first record; a seed entry: its request
+    uint32_t ring_sd[2][F];           // slot | seed << 14 | degree << 16
+    uint32_t ring_bg[2][F];           // the row's first record; a seed entry: its request
     unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
     unsigned long long e_beg[64];          // the chunk's entries' first records
     uint32_t c_pre[64];                    // owner map
@@ -1825,8 +1825,8 @@ struct LiteLevel {
 };
 
 // one lane's push of node u (record fields deg / begin) in direction D
-template <int HLOG, int D>
-__device__ __forceinline__ void lite_push(LiteShared<HLOG> &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
+template <int HLOG, int F, int D>
+__device__ __forceinline__ void lite_push(LiteShared<HLOG, F> &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
                                           uint32_t begin, uint32_t m, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lk = m & (L.lookup | (deg ? 0u : L.sread));
     int h = -1;
@@ -1857,9 +1857,9 @@ __device__ __forceinline__ void lite_push(LiteShared<HLOG> &S, const LiteLevel &
     }
     const uint32_t idx = lds_append(app, &S.tail[D]);
     if (app) {
-        if (idx - S.head[D] < (uint32_t)kLiteF && deg <= 0xFFFFu) {
-            S.ring_sd[D][idx & (kLiteF - 1)] = (uint32_t)h | (deg << 16);
-            S.ring_bg[D][idx & (kLiteF - 1)] = begin;
+        if (idx - S.head[D] < (uint32_t)F && deg <= 0xFFFFu) {
+            S.ring_sd[D][idx % F] = (uint32_t)h | (deg << 16);
+            S.ring_bg[D][idx % F] = begin;
         } else {
             S.spill = 1;
         }
@@ -1870,8 +1870,8 @@ __device__ __forceinline__ void lite_push(LiteShared<HLOG> &S, const LiteLevel &
 // taken); its mask is S.e_mask[j], its first record S.e_beg[j].  Edge-balanced: an owner
 // map per 64-edge chunk (each entry writes its index at its first position, a prefix max
 // fills the gaps), record loads of the next 64 edges issued before this chunk's pushes.
-template <int HLOG, int D>
-__device__ __forceinline__ void lite_expand(LiteShared<HLOG> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+template <int HLOG, int F, int D>
+__device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                             uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
@@ -1907,7 +1907,7 @@ __device__ __forceinline__ void lite_expand(LiteShared<HLOG> &S, const DevGraph 
                 m = 0;
             }
         }
-        lite_push<HLOG, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
+        lite_push<HLOG, F, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
     };
     Edge a{}, b{};
     fetch(0, a);
@@ -1935,8 +1935,8 @@ __device__ __forceinline__ void lite_expand(LiteShared<HLOG> &S, const DevGraph 
 
 // consume direction D's ring (every pending row: one atomic reads and clears its pending
 // bits of D) and expand it
-template <int HLOG, int D>
-__device__ __forceinline__ void lite_level(LiteShared<HLOG> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+template <int HLOG, int F, int D>
+__device__ __forceinline__ void lite_level(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                            uint32_t open, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lane = threadIdx.x;
     const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.head[D]);
@@ -1945,7 +1945,7 @@ __device__ __forceinline__ void lite_level(LiteShared<HLOG> &S, const DevGraph &
         const uint32_t i = c + lane;
         uint32_t deg = 0, take = 0;
         if (i < t0) {
-            const uint32_t w = S.ring_sd[D][i & (kLiteF - 1)], bg = S.ring_bg[D][i & (kLiteF - 1)];
+            const uint32_t w = S.ring_sd[D][i % F], bg = S.ring_bg[D][i % F];
             const uint32_t s = w & 0x3FFFu;
             const unsigned long long old = atomicAnd(&S.st[s], ~(0xFFFFull << (32 * D + 16)));
             take = (uint32_t)(old >> (32 * D + 16)) & open;
@@ -1955,7 +1955,7 @@ __device__ __forceinline__ void lite_level(LiteShared<HLOG> &S, const DevGraph &
         S.e_mask[lane] = (uint16_t)take;
         if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
         __syncthreads();
-        lite_expand<HLOG, D>(S, g, rec, L, deg, edges, or_acc, deg_acc);
+        lite_expand<HLOG, F, D>(S, g, rec, L, deg, edges, or_acc, deg_acc);
         __syncthreads();
     }
 }
@@ -1970,12 +1970,14 @@ __device__ __forceinline__ uint32_t wave_sum_all(uint32_t x) {
 }
 
 // one 16-request unit by one wave (seed as bidi_load_rows loads it on lanes < 16)
-template <int HLOG>
-__device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g, const FRec *frec, const FRec *brec,
+template <int HLOG, int F>
+__device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *frec, const FRec *brec,
                                           const BidiSeed &seed, uint64_t *allowed, const uint64_t unit,
-                                          uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats) {
-    using SH = LiteShared<HLOG>;
+                                          uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats,
+                                          unsigned long long *stamp = nullptr) {
+    using SH = LiteShared<HLOG, F>;
     const uint32_t lane = threadIdx.x;
+    if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t c0 = unit * 16;
     for (int i = lane; i < SH::H / 4; i += 64) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
     for (int i = lane; i < SH::H / 2; i += 64) reinterpret_cast<uint4 *>(S.st)[i] = make_uint4(0, 0, 0, 0);
@@ -2020,7 +2022,7 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
             app = pend && !((uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
         }
         pend_mask[side] = (uint32_t)__ballot(pend);
-        const uint32_t idx = lds_append(app, &S.tail[side]);  // idx < 16 <= kLiteF
+        const uint32_t idx = lds_append(app, &S.tail[side]);  // idx < 16 <= F
         if (app) {
             if (deg > 0xFFFFu) S.spill = 1;
             S.ring_sd[side][idx] = (uint32_t)h | (1u << 14) | (deg << 16);
@@ -2035,11 +2037,15 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
         const uint32_t d = (lane < 16 && ((pend_mask[side] >> lane) & 1u)) ? (side ? tdeg : rdeg) : 0u;
         (side ? sb : sf) = wave_sum_all(d);
     }
-    // level 0: the eager seed rows, every push inserts
+    if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
+    // level 0: the eager seed rows.  rev(t) first (every push inserts), then fint(r): by
+    // then t's row is complete, so a forward dead end (a group with no interior successor:
+    // most of a document's grants) can only meet t or an entry of rev(t) and is looked up,
+    // not stored
     {
-        const LiteLevel L0{0, 0};
         const bool e = v && eager;
-        for (int side = 0; side < 2; side++) {
+        const uint32_t eager_mask = (uint32_t)__ballot(e) & 0xFFFFu;
+        for (int side = 1; side >= 0; side--) {
             if (lane < 16) {
                 S.e_mask[lane] = (uint16_t)bit;
                 S.e_beg[lane] = S.sbase[side][lane];
@@ -2047,9 +2053,9 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
             __syncthreads();
             const uint32_t d = (lane < 16 && e) ? (side ? tdeg : rdeg) : 0u;
             if (side == 0)
-                lite_expand<HLOG, 0>(S, g, frec, L0, d, edges, acc_or[0], acc_deg[0]);
+                lite_expand<HLOG, F, 0>(S, g, frec, LiteLevel{0, eager_mask}, d, edges, acc_or[0], acc_deg[0]);
             else
-                lite_expand<HLOG, 1>(S, g, brec, L0, d, edges, acc_or[1], acc_deg[1]);
+                lite_expand<HLOG, F, 1>(S, g, brec, LiteLevel{0, 0}, d, edges, acc_or[1], acc_deg[1]);
             __syncthreads();
         }
         pf |= wave_or_all(acc_or[0]);
@@ -2057,7 +2063,9 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
         sf += wave_sum_all(acc_deg[0]);
         sb += wave_sum_all(acc_deg[1]);
     }
+    if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     bool spilled = false;
+    uint32_t n_levels = 0;
     for (;;) {
         __syncthreads();
         const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
@@ -2085,15 +2093,16 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
         // bits of requests whose OTHER side is closed: only looked up (a meet or nothing);
         // a dead end (no row in this direction) is only looked up once the other side's
         // seed row was read in an earlier level (it can meet nothing else)
+        n_levels++;
         if (do_f) {
             const LiteLevel L{open & bc, ~tpend};
             acc_or[0] = acc_deg[0] = 0;
-            lite_level<HLOG, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
+            lite_level<HLOG, F, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
         }
         if (do_b) {
             const LiteLevel L{open & fc, ~rpend};
             acc_or[1] = acc_deg[1] = 0;
-            lite_level<HLOG, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
+            lite_level<HLOG, F, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
         }
         if (do_f) {
             pf = wave_or_all(acc_or[0]);
@@ -2111,6 +2120,12 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
         if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
         return;
     }
+    if (stamp) {  // KETOGPU_STAMPS=1: phase cycles, levels and table load per unit (report_stamps)
+        stamp[3] = stamp[4] = __builtin_amdgcn_s_memtime();
+        stamp[5] = n_levels;
+        stamp[6] = S.n_used;
+        stamp[7] = 1;
+    }
 #pragma unroll
     for (int s = 32; s; s >>= 1) {
         rows += __shfl_down(rows, s, 64);
@@ -2125,27 +2140,31 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG> &S, const DevGraph &g
 }
 
 // plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit)
+template <int HLOG, int F>
 __global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, const FRec *brec, const uint32_t *roots,
                                                   const uint32_t *targets, uint64_t n, uint64_t *allowed,
                                                   uint32_t *spill_out, unsigned int *spill_count,
-                                                  unsigned long long *stats, uint64_t unit0) {
-    __shared__ LiteShared<9> S;
+                                                  unsigned long long *stats, uint64_t unit0,
+                                                  unsigned long long *stamps) {
+    __shared__ LiteShared<HLOG, F> S;
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
-    lite_unit<9>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats);
+    unsigned long long *stamp =
+        (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
+    lite_unit<HLOG, F>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats, stamp);
 }
 
 // plan "lite" first stage over pinned host requests read in place (bidi_host_kernel's
 // prologue: K units per workgroup, requests validated and stored in HBM for the spill stages)
-template <int K>
+template <int K, int HLOG = 9, int F = kLiteF>
 __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
                                                        uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
                                                        unsigned int *spill_count, unsigned long long *stats,
                                                        unsigned long long *first_bad) {
-    __shared__ LiteShared<9> S;
+    __shared__ LiteShared<HLOG, F> S;
     uint32_t r[K], t[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -2177,7 +2196,7 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        lite_unit<9>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
+        lite_unit<HLOG, F>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
         __syncthreads();
     }
 }
@@ -2706,8 +2725,12 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
-            KLAUNCH(lite_kernel, dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets, q.n, q.allowed,
-                    out, out_count, stats, unit0);
+            if (c.hlog == 8)
+                KLAUNCH((lite_kernel<8, 96>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets,
+                        q.n, q.allowed, out, out_count, stats, unit0, stp);
+            else
+                KLAUNCH((lite_kernel<9, kLiteF>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
+                        q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
             return;
         }
         if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
@@ -3011,6 +3034,11 @@ struct ketogpu_engine {
         if (p == "lite" && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
             bidi_cfg.lite = 1;
+            bidi_cfg.f = kLiteF;
+            if (const char *ls = getenv("KETOGPU_LITE"); ls && atoi(ls) == 8) {  // "8": 256-slot tables, 96-entry rings
+                bidi_cfg.hlog = 8;
+                bidi_cfg.f = 96;
+            }
         }
         trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
@@ -3410,7 +3438,11 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite)                                                                                 \
+        if (bidi_cfg.lite && bidi_cfg.hlog == 8)                                                           \
+            KLAUNCH((lite_host_kernel<K, 8, 96>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
+                    g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,   \
+                    list[0], &spill_count[0], st.stats, d_bad);                                            \
+        else if (bidi_cfg.lite)                                                                            \
             KLAUNCH(lite_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
                     frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
                     list[0], &spill_count[0], st.stats, d_bad);                                            \
