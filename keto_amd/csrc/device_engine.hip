@@ -1814,6 +1814,7 @@ struct LiteShared {
     unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
     unsigned long long e_beg[64];          // the chunk's entries' first records
     uint32_t c_pre[64];                    // owner map
+    uint32_t c_pre2[64];                   // owner map of the prefetched forward seed rows (level 0)
     uint32_t root[16];
     uint16_t e_mask[64];
     uint32_t n_used, spill, found, active;
@@ -1867,37 +1868,55 @@ __device__ __forceinline__ void lite_push(LiteShared<HLOG, F> &S, const LiteLeve
 }
 
 // Expand this chunk's entries in direction D: lane j holds entry j's degree (0: nothing
-// taken); its mask is S.e_mask[j], its first record S.e_beg[j].  Edge-balanced: an owner
-// map per 64-edge chunk (each entry writes its index at its first position, a prefix max
-// fills the gaps), record loads of the next 64 edges issued before this chunk's pushes.
-template <int HLOG, int F, int D>
+// taken); its mask is S.e_mask[j] (SEED: bit j), its first record S.e_beg[j] (SEED: the
+// seed row's, S.sbase[D][j]).  Edge-balanced: an owner map per 64-edge chunk in `own`
+// (each entry writes its index at its first position, a prefix max fills the gaps), record
+// loads of the next 64 edges issued before this chunk's pushes.  `pre`: chunk 0 was
+// already fetched by lite_fetch0 (with the same `own`), so its loads overlapped other work.
+struct LiteEdge {
+    uint32_t lo, ls;
+    FRec rc;
+};
+
+template <int HLOG, int F, int D, bool SEED>
+__device__ __forceinline__ void lite_fetch(LiteShared<HLOG, F> &S, const FRec *rec, uint32_t *own, uint32_t my_deg,
+                                           uint32_t start, uint32_t total, uint32_t eb, LiteEdge &x) {
+    const uint32_t lane = threadIdx.x;
+    if (my_deg && start < eb + 64 && start + my_deg > eb) own[(start > eb ? start : eb) - eb] = lane;
+    __syncthreads();
+    const int o = wave_incl_max_i32((int)own[lane]);
+    x.lo = (uint32_t)(o < 0 ? 0 : o);
+    x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
+    const uint32_t e = min(eb + lane, total - 1);
+    const unsigned long long b0 = SEED ? S.sbase[D][x.lo & 15] : S.e_beg[x.lo];
+    x.rc = rec[b0 + (e - x.ls)];
+}
+
+// chunk 0 of an expansion: owner map and record loads only (lite_expand with `pre` pushes it)
+template <int HLOG, int F, int D, bool SEED>
+__device__ __forceinline__ void lite_fetch0(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, uint32_t *own,
+                                            uint32_t my_deg, LiteEdge &x) {
+    const uint32_t incl = wave_incl_sum_u32(my_deg);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    own[threadIdx.x] = 0xFFFFFFFFu;
+    if (total) lite_fetch<HLOG, F, D, SEED>(S, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, x);
+}
+
+template <int HLOG, int F, int D, bool SEED = false>
 __device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
-                                            uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
+                                            uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc,
+                                            uint32_t *own, const LiteEdge *pre = nullptr) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (!total) return;
     rec -= g.seed_shift;  // begins carry the shift (0 outside the test knob)
-    S.c_pre[lane] = 0xFFFFFFFFu;
-    struct Edge {
-        uint32_t lo, ls;
-        FRec rc;
-    };
-    auto fetch = [&](uint32_t eb, Edge &x) {
-        if (my_deg && start < eb + 64 && start + my_deg > eb) S.c_pre[(start > eb ? start : eb) - eb] = lane;
-        __syncthreads();
-        const int o = wave_incl_max_i32((int)S.c_pre[lane]);
-        x.lo = (uint32_t)(o < 0 ? 0 : o);
-        x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
-        const uint32_t e = min(eb + lane, total - 1);
-        x.rc = rec[S.e_beg[x.lo] + (e - x.ls)];
-    };
-    auto push = [&](uint32_t eb, const Edge &x) {
+    auto push = [&](uint32_t eb, const LiteEdge &x) {
         const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
         uint32_t m = 0;
         if (eb + lane < total) {
-            m = S.e_mask[x.lo] & ~found;
+            m = (SEED ? (1u << (x.lo & 15)) : (uint32_t)S.e_mask[x.lo]) & ~found;
             edges++;
             if (D == 1 && x.rc.node >= g.Ni) {  // a source entry of rev(t): it can only meet r itself
                 uint32_t hit = 0;
@@ -1909,21 +1928,26 @@ __device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGra
         }
         lite_push<HLOG, F, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
     };
-    Edge a{}, b{};
-    fetch(0, a);
+    LiteEdge a{}, b{};
+    if (pre) {
+        a = *pre;
+    } else {
+        own[lane] = 0xFFFFFFFFu;
+        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, 0, a);
+    }
     if (total <= 64) {  // one chunk (the common level): no pipelining to pay for
         push(0, a);
         return;
     }
     for (uint32_t eb = 0;;) {
-        fetch(eb + 64, b);
+        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, b);
         push(eb, a);
         eb += 64;
         if (eb + 64 >= total) {
             push(eb, b);
             break;
         }
-        fetch(eb + 64, a);
+        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, a);
         push(eb, b);
         eb += 64;
         if (eb + 64 >= total) {
@@ -1955,7 +1979,7 @@ __device__ __forceinline__ void lite_level(LiteShared<HLOG, F> &S, const DevGrap
         S.e_mask[lane] = (uint16_t)take;
         if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
         __syncthreads();
-        lite_expand<HLOG, F, D>(S, g, rec, L, deg, edges, or_acc, deg_acc);
+        lite_expand<HLOG, F, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre);
         __syncthreads();
     }
 }
@@ -2045,19 +2069,16 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
     {
         const bool e = v && eager;
         const uint32_t eager_mask = (uint32_t)__ballot(e) & 0xFFFFu;
-        for (int side = 1; side >= 0; side--) {
-            if (lane < 16) {
-                S.e_mask[lane] = (uint16_t)bit;
-                S.e_beg[lane] = S.sbase[side][lane];
-            }
-            __syncthreads();
-            const uint32_t d = (lane < 16 && e) ? (side ? tdeg : rdeg) : 0u;
-            if (side == 0)
-                lite_expand<HLOG, F, 0>(S, g, frec, LiteLevel{0, eager_mask}, d, edges, acc_or[0], acc_deg[0]);
-            else
-                lite_expand<HLOG, F, 1>(S, g, brec, LiteLevel{0, 0}, d, edges, acc_or[1], acc_deg[1]);
-            __syncthreads();
-        }
+        const uint32_t df = (lane < 16 && e) ? rdeg : 0u, db = (lane < 16 && e) ? tdeg : 0u;
+        // the forward rows' first 64 records are loaded before the backward pushes, so
+        // the two dependent expansions of level 0 wait for HBM once
+        LiteEdge f0{};
+        lite_fetch0<HLOG, F, 0, true>(S, g, frec, S.c_pre2, df, f0);
+        lite_expand<HLOG, F, 1, true>(S, g, brec, LiteLevel{0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
+        __syncthreads();
+        lite_expand<HLOG, F, 0, true>(S, g, frec, LiteLevel{0, eager_mask}, df, edges, acc_or[0], acc_deg[0],
+                                      S.c_pre2, &f0);
+        __syncthreads();
         pf |= wave_or_all(acc_or[0]);
         pb |= wave_or_all(acc_or[1]);
         sf += wave_sum_all(acc_deg[0]);
@@ -2065,11 +2086,13 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
     }
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     bool spilled = false;
-    uint32_t n_levels = 0;
+    uint32_t n_levels = 0, ring_max[2] = {0, 0};
     for (;;) {
         __syncthreads();
         const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
         uint32_t open = active & ~found;
+        if (stamp)
+            for (int d = 0; d < 2; d++) ring_max[d] = max(ring_max[d], S.tail[d] - S.head[d]);
         if (S.spill || (S.n_used > (uint32_t)SH::HMAX && open)) {  // undecided requests, table over its load
             spilled = true;
             break;
@@ -2125,6 +2148,8 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
         stamp[5] = n_levels;
         stamp[6] = S.n_used;
         stamp[7] = 1;
+        stamp[12] = ring_max[0];
+        stamp[13] = ring_max[1];
     }
 #pragma unroll
     for (int s = 32; s; s >>= 1) {
@@ -2825,7 +2850,7 @@ struct ketogpu_engine {
         std::vector<unsigned long long> h((size_t)65536 * 16);
         HIP_CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
         double ph[4] = {0, 0, 0, 0}, lv = 0, used = 0, lp[4] = {0, 0, 0, 0};
-        std::vector<double> tot;
+        std::vector<double> tot, slots, ring[2];
         for (size_t b = 0; b < 65536; b++) {
             const unsigned long long *s = &h[b * 16];
             if (s[7] != 1) continue;
@@ -2833,7 +2858,17 @@ struct ketogpu_engine {
             for (int k = 0; k < 4; k++) lp[k] += (double)s[8 + k];
             lv += (double)s[5];
             used += (double)s[6];
+            slots.push_back((double)s[6]);
+            for (int d = 0; d < 2; d++) ring[d].push_back((double)s[12 + d]);
             tot.push_back((double)(s[4] - s[0]));
+        }
+        if (!slots.empty()) {  // table load and (lite) ring occupancy: p50 / p99 / max per unit
+            for (auto *v : {&slots, &ring[0], &ring[1]}) std::sort(v->begin(), v->end());
+            auto q = [](const std::vector<double> &v, double f) { return v[(size_t)(f * (double)(v.size() - 1))]; };
+            fprintf(stderr, "[stamps] slots p50 %.0f p99 %.0f max %.0f | rings fwd p50 %.0f p99 %.0f max %.0f, "
+                            "bwd p50 %.0f p99 %.0f max %.0f\n",
+                    q(slots, 0.5), q(slots, 0.99), slots.back(), q(ring[0], 0.5), q(ring[0], 0.99), ring[0].back(),
+                    q(ring[1], 0.5), q(ring[1], 0.99), ring[1].back());
         }
         if (tot.empty()) return;
         std::sort(tot.begin(), tot.end());

@@ -14,7 +14,7 @@ for round in 1 2; do
     envset=()
     case "$v" in
       base) ;;
-      *=*) envset=("$v") ;;
+      *=*) read -r -a envset <<< "$v" ;;
       *) lib="$PWD/keto_amd/variants/libketogpu_$v.so" ;;
     esac
     # AB_ARGS: extra bench.py arguments (e.g. "--mode partitioned --scale 0.01")
