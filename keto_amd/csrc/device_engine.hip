@@ -1801,40 +1801,69 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
 //     below Ni come first) fit 32-bit record begins (round-2 verdict item 6).
 // Dead ends are looked up, not stored, as in bidi_kernel.  Same answers, same spill
 // protocol (a spilled unit re-runs on the bidi cascade w, q, s).
-constexpr int kLiteF = 128;  // ring entries per direction (default shape)
+constexpr int kLiteF = 128;  // ring entries per direction (wide shape)
+// the two table shapes: "wide" 512 slots, 128-entry rings; "slim" (default) 384 slots,
+// 64 forward / 128 backward ring entries — 7.4 instead of 9.7 KB of LDS, 21 instead of 16
+// units per CU (config #2: slots p99 230, rings p99 35 / 72 per unit, KETOGPU_STAMPS)
+template <int H, int FF, int FB> struct LiteShared;
 
-template <int HLOG, int F>
+template <int H_, int FF_, int FB_>
 struct LiteShared {
-    static constexpr int H = 1 << HLOG;
-    static constexpr int HMAX = H * 7 / 8;
+    static constexpr int H = H_;             // table slots (not necessarily a power of two)
+    static constexpr int HMAX = H * 7 / 8;   // load limit: a unit spills beyond it
+    static constexpr int FF = FF_, FB = FB_; // ring entries, forward / backward
     alignas(16) uint32_t key[H];
     alignas(16) unsigned long long st[H];  // fwd visited | fwd pending | bwd visited | bwd pending
-    uint32_t ring_sd[2][F];           // slot | seed << 14 | degree << 16
-    uint32_t ring_bg[2][F];           // the row's first record; a seed entry: its request
+    uint32_t ring_sd[FF + FB];             // slot | seed << 14 | degree << 16 (forward ring, then backward)
+    uint32_t ring_bg[FF + FB];             // the row's first record; a seed entry: its request
     unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
-    unsigned long long e_beg[64];          // the chunk's entries' first records
+    uint32_t e_beg[64];                    // the chunk's entries' first records (a seed entry: its request)
     uint32_t c_pre[64];                    // owner map
     uint32_t c_pre2[64];                   // owner map of the prefetched forward seed rows (level 0)
     uint32_t root[16];
     uint16_t e_mask[64];
     uint32_t n_used, spill, found, active;
     uint32_t head[2], tail[2];
+    template <int D>
+    static constexpr int ring_size() { return D ? FB : FF; }
+    template <int D>
+    __device__ __forceinline__ uint32_t &sd(uint32_t i) { return ring_sd[(D ? FF : 0) + i % (D ? FB : FF)]; }
+    template <int D>
+    __device__ __forceinline__ uint32_t &bg(uint32_t i) { return ring_bg[(D ? FF : 0) + i % (D ? FB : FF)]; }
 };
+
+// find (insert == false) or find-or-insert u in a table of H slots (any H); -1 when absent
+// (or the table is full)
+template <int H>
+__device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
+    uint32_t hh = (uint32_t)(((uint64_t)(u * 2654435761u) * (uint64_t)H) >> 32);
+    for (int p = 0; p < H; p++) {
+        const uint32_t kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
+        if (kv == kEmpty) {
+            if (!insert) return -1;
+            inserted = true;
+            return (int)hh;
+        }
+        if (kv == u) return (int)hh;
+        hh = hh + 1 == (uint32_t)H ? 0u : hh + 1;
+    }
+    return -1;
+}
 
 struct LiteLevel {
     uint32_t lookup, sread;  // for the direction being expanded
 };
 
 // one lane's push of node u (record fields deg / begin) in direction D
-template <int HLOG, int F, int D>
-__device__ __forceinline__ void lite_push(LiteShared<HLOG, F> &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
+template <class SH, int D>
+__device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
                                           uint32_t begin, uint32_t m, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lk = m & (L.lookup | (deg ? 0u : L.sread));
     int h = -1;
     bool inserted = false;
     if (want) {
         const bool ins = (m & ~lk) != 0;
-        h = bidi_slot<HLOG>(S.key, u, ins, inserted);
+        h = lite_slot<SH::H>(S.key, u, ins, inserted);
         if (h < 0 && ins) S.spill = 1;
     }
     const uint64_t bal = __ballot(inserted);
@@ -1858,9 +1887,9 @@ __device__ __forceinline__ void lite_push(LiteShared<HLOG, F> &S, const LiteLeve
     }
     const uint32_t idx = lds_append(app, &S.tail[D]);
     if (app) {
-        if (idx - S.head[D] < (uint32_t)F && deg <= 0xFFFFu) {
-            S.ring_sd[D][idx % F] = (uint32_t)h | (deg << 16);
-            S.ring_bg[D][idx % F] = begin;
+        if (idx - S.head[D] < (uint32_t)SH::template ring_size<D>() && deg <= 0xFFFFu) {
+            S.template sd<D>(idx) = (uint32_t)h | (deg << 16);
+            S.template bg<D>(idx) = begin;
         } else {
             S.spill = 1;
         }
@@ -1878,9 +1907,9 @@ struct LiteEdge {
     FRec rc;
 };
 
-template <int HLOG, int F, int D, bool SEED>
-__device__ __forceinline__ void lite_fetch(LiteShared<HLOG, F> &S, const FRec *rec, uint32_t *own, uint32_t my_deg,
-                                           uint32_t start, uint32_t total, uint32_t eb, LiteEdge &x) {
+template <class SH, int D, bool SEED>
+__device__ __forceinline__ void lite_fetch(SH &S, const DevGraph &g, const FRec *rec, uint32_t *own, uint32_t my_deg,
+                                           uint32_t start, uint32_t total, uint32_t eb, uint64_t seeds, LiteEdge &x) {
     const uint32_t lane = threadIdx.x;
     if (my_deg && start < eb + 64 && start + my_deg > eb) own[(start > eb ? start : eb) - eb] = lane;
     __syncthreads();
@@ -1888,24 +1917,32 @@ __device__ __forceinline__ void lite_fetch(LiteShared<HLOG, F> &S, const FRec *r
     x.lo = (uint32_t)(o < 0 ? 0 : o);
     x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
     const uint32_t e = min(eb + lane, total - 1);
-    const unsigned long long b0 = SEED ? S.sbase[D][x.lo & 15] : S.e_beg[x.lo];
+    // a seed row's begin is 64-bit (sbase); an interior row's the record's own 32 bits,
+    // shifted by the test knob like sbase (rec is taken back by it)
+    unsigned long long b0;
+    if (SEED) {
+        b0 = S.sbase[D][x.lo & 15];
+    } else {
+        const uint32_t w = S.e_beg[x.lo];
+        b0 = (seeds >> x.lo) & 1ull ? S.sbase[D][w & 15] : (unsigned long long)w + g.seed_shift;
+    }
     x.rc = rec[b0 + (e - x.ls)];
 }
 
 // chunk 0 of an expansion: owner map and record loads only (lite_expand with `pre` pushes it)
-template <int HLOG, int F, int D, bool SEED>
-__device__ __forceinline__ void lite_fetch0(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, uint32_t *own,
+template <class SH, int D, bool SEED>
+__device__ __forceinline__ void lite_fetch0(SH &S, const DevGraph &g, const FRec *rec, uint32_t *own,
                                             uint32_t my_deg, LiteEdge &x) {
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     own[threadIdx.x] = 0xFFFFFFFFu;
-    if (total) lite_fetch<HLOG, F, D, SEED>(S, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, x);
+    if (total) lite_fetch<SH, D, SEED>(S, g, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, 0, x);
 }
 
-template <int HLOG, int F, int D, bool SEED = false>
-__device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+template <class SH, int D, bool SEED = false>
+__device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                             uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc,
-                                            uint32_t *own, const LiteEdge *pre = nullptr) {
+                                            uint32_t *own, const LiteEdge *pre = nullptr, uint64_t seeds = 0) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
@@ -1926,28 +1963,28 @@ __device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGra
                 m = 0;
             }
         }
-        lite_push<HLOG, F, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
+        lite_push<SH, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
     };
     LiteEdge a{}, b{};
     if (pre) {
         a = *pre;
     } else {
         own[lane] = 0xFFFFFFFFu;
-        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, 0, a);
+        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, 0, seeds, a);
     }
     if (total <= 64) {  // one chunk (the common level): no pipelining to pay for
         push(0, a);
         return;
     }
     for (uint32_t eb = 0;;) {
-        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, b);
+        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, eb + 64, seeds, b);
         push(eb, a);
         eb += 64;
         if (eb + 64 >= total) {
             push(eb, b);
             break;
         }
-        lite_fetch<HLOG, F, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, a);
+        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, eb + 64, seeds, a);
         push(eb, b);
         eb += 64;
         if (eb + 64 >= total) {
@@ -1959,8 +1996,8 @@ __device__ __forceinline__ void lite_expand(LiteShared<HLOG, F> &S, const DevGra
 
 // consume direction D's ring (every pending row: one atomic reads and clears its pending
 // bits of D) and expand it
-template <int HLOG, int F, int D>
-__device__ __forceinline__ void lite_level(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
+template <class SH, int D>
+__device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                            uint32_t open, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lane = threadIdx.x;
     const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.head[D]);
@@ -1968,18 +2005,21 @@ __device__ __forceinline__ void lite_level(LiteShared<HLOG, F> &S, const DevGrap
     for (uint32_t c = h0; c < t0; c += 64) {
         const uint32_t i = c + lane;
         uint32_t deg = 0, take = 0;
+        bool seed = false;
         if (i < t0) {
-            const uint32_t w = S.ring_sd[D][i % F], bg = S.ring_bg[D][i % F];
+            const uint32_t w = S.template sd<D>(i), bg = S.template bg<D>(i);
             const uint32_t s = w & 0x3FFFu;
             const unsigned long long old = atomicAnd(&S.st[s], ~(0xFFFFull << (32 * D + 16)));
             take = (uint32_t)(old >> (32 * D + 16)) & open;
             deg = take ? w >> 16 : 0u;
-            S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & 15] : (unsigned long long)bg + g.seed_shift;
+            seed = (w >> 14) & 1u;
+            S.e_beg[lane] = bg;
         }
+        const uint64_t seeds = __ballot(seed);
         S.e_mask[lane] = (uint16_t)take;
         if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
         __syncthreads();
-        lite_expand<HLOG, F, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre);
+        lite_expand<SH, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre, nullptr, seeds);
         __syncthreads();
     }
 }
@@ -1994,12 +2034,11 @@ __device__ __forceinline__ uint32_t wave_sum_all(uint32_t x) {
 }
 
 // one 16-request unit by one wave (seed as bidi_load_rows loads it on lanes < 16)
-template <int HLOG, int F>
-__device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph &g, const FRec *frec, const FRec *brec,
+template <class SH>
+__device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *frec, const FRec *brec,
                                           const BidiSeed &seed, uint64_t *allowed, const uint64_t unit,
                                           uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats,
                                           unsigned long long *stamp = nullptr) {
-    using SH = LiteShared<HLOG, F>;
     const uint32_t lane = threadIdx.x;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t c0 = unit * 16;
@@ -2034,7 +2073,7 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
     for (int side = 0; side < 2; side++) {
         const uint32_t u = side ? t : r, deg = side ? tdeg : rdeg;
         bool inserted = false;
-        const int h = v ? bidi_slot<HLOG>(S.key, u, true, inserted) : -1;
+        const int h = v ? lite_slot<SH::H>(S.key, u, true, inserted) : -1;
         const uint64_t bal = __ballot(inserted);
         if (lane == 0) S.n_used += (uint32_t)__popcll(bal);
         const bool pend = h >= 0 && !eager && deg;
@@ -2047,10 +2086,15 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
         }
         pend_mask[side] = (uint32_t)__ballot(pend);
         const uint32_t idx = lds_append(app, &S.tail[side]);  // idx < 16 <= F
-        if (app) {
+        if (app) {  // idx < 16 <= every ring's size
             if (deg > 0xFFFFu) S.spill = 1;
-            S.ring_sd[side][idx] = (uint32_t)h | (1u << 14) | (deg << 16);
-            S.ring_bg[side][idx] = lane;
+            if (side) {
+                S.template sd<1>(idx) = (uint32_t)h | (1u << 14) | (deg << 16);
+                S.template bg<1>(idx) = lane;
+            } else {
+                S.template sd<0>(idx) = (uint32_t)h | (1u << 14) | (deg << 16);
+                S.template bg<0>(idx) = lane;
+            }
         }
     }
     uint32_t rpend = pend_mask[0], tpend = pend_mask[1];  // seed rows not read yet
@@ -2073,10 +2117,10 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
         // the forward rows' first 64 records are loaded before the backward pushes, so
         // the two dependent expansions of level 0 wait for HBM once
         LiteEdge f0{};
-        lite_fetch0<HLOG, F, 0, true>(S, g, frec, S.c_pre2, df, f0);
-        lite_expand<HLOG, F, 1, true>(S, g, brec, LiteLevel{0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
+        lite_fetch0<SH, 0, true>(S, g, frec, S.c_pre2, df, f0);
+        lite_expand<SH, 1, true>(S, g, brec, LiteLevel{0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
         __syncthreads();
-        lite_expand<HLOG, F, 0, true>(S, g, frec, LiteLevel{0, eager_mask}, df, edges, acc_or[0], acc_deg[0],
+        lite_expand<SH, 0, true>(S, g, frec, LiteLevel{0, eager_mask}, df, edges, acc_or[0], acc_deg[0],
                                       S.c_pre2, &f0);
         __syncthreads();
         pf |= wave_or_all(acc_or[0]);
@@ -2120,12 +2164,12 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
         if (do_f) {
             const LiteLevel L{open & bc, ~tpend};
             acc_or[0] = acc_deg[0] = 0;
-            lite_level<HLOG, F, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
+            lite_level<SH, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
         }
         if (do_b) {
             const LiteLevel L{open & fc, ~rpend};
             acc_or[1] = acc_deg[1] = 0;
-            lite_level<HLOG, F, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
+            lite_level<SH, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
         }
         if (do_f) {
             pf = wave_or_all(acc_or[0]);
@@ -2165,31 +2209,31 @@ __device__ __forceinline__ void lite_unit(LiteShared<HLOG, F> &S, const DevGraph
 }
 
 // plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit)
-template <int HLOG, int F>
+template <class SH>
 __global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, const FRec *brec, const uint32_t *roots,
                                                   const uint32_t *targets, uint64_t n, uint64_t *allowed,
                                                   uint32_t *spill_out, unsigned int *spill_count,
                                                   unsigned long long *stats, uint64_t unit0,
                                                   unsigned long long *stamps) {
-    __shared__ LiteShared<HLOG, F> S;
+    __shared__ SH S;
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
     unsigned long long *stamp =
         (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
-    lite_unit<HLOG, F>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats, stamp);
+    lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats, stamp);
 }
 
 // plan "lite" first stage over pinned host requests read in place (bidi_host_kernel's
 // prologue: K units per workgroup, requests validated and stored in HBM for the spill stages)
-template <int K, int HLOG = 9, int F = kLiteF>
+template <int K, class SH>
 __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
                                                        uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
                                                        unsigned int *spill_count, unsigned long long *stats,
                                                        unsigned long long *first_bad) {
-    __shared__ LiteShared<HLOG, F> S;
+    __shared__ SH S;
     uint32_t r[K], t[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -2221,7 +2265,7 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        lite_unit<HLOG, F>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
+        lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
         __syncthreads();
     }
 }
@@ -2750,12 +2794,12 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
-            if (c.hlog == 8)
-                KLAUNCH((lite_kernel<8, 96>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets,
-                        q.n, q.allowed, out, out_count, stats, unit0, stp);
+            if (c.hlog == 9)
+                KLAUNCH((lite_kernel<LiteShared<512, kLiteF, kLiteF>>), dim3(grid), dim3(64), pad, stream, g, frec,
+                        brec, q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
             else
-                KLAUNCH((lite_kernel<9, kLiteF>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
-                        q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
+                KLAUNCH((lite_kernel<LiteShared<384, 64, 128>>), dim3(grid), dim3(64), pad, stream, g, frec, brec,
+                        q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
             return;
         }
         if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
@@ -3069,11 +3113,10 @@ struct ketogpu_engine {
         if (p == "lite" && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
             bidi_cfg.lite = 1;
-            bidi_cfg.f = kLiteF;
-            if (const char *ls = getenv("KETOGPU_LITE"); ls && atoi(ls) == 8) {  // "8": 256-slot tables, 96-entry rings
-                bidi_cfg.hlog = 8;
-                bidi_cfg.f = 96;
-            }
+            // KETOGPU_LITE=512: the wide shape (512 slots, 128-entry rings); default slim (384 slots)
+            const char *ls = getenv("KETOGPU_LITE");
+            bidi_cfg.hlog = ls && atoi(ls) == 512 ? 9 : 8;
+            bidi_cfg.f = bidi_cfg.hlog == 9 ? kLiteF : 64;
         }
         trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
@@ -3093,7 +3136,10 @@ struct ketogpu_engine {
                 candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0, true, c.u, c.wpe});
                 if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
             }
-            if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
+            if (use_lite) {  // plan "lite": the slim and the wide table shapes
+                candidates.push_back({true, 8, 64, 64, 7, 0, true, 16, 1, 1});
+                candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});
+            }
             if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
             use_bidi = use_bidi || use_lite;
         }
@@ -3473,14 +3519,16 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite && bidi_cfg.hlog == 8)                                                           \
-            KLAUNCH((lite_host_kernel<K, 8, 96>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,   \
-                    list[0], &spill_count[0], st.stats, d_bad);                                            \
+        if (bidi_cfg.lite && bidi_cfg.hlog == 9)                                                           \
+            KLAUNCH((lite_host_kernel<K, LiteShared<512, kLiteF, kLiteF>>),                               \
+                    dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec, src->roots, \
+                    src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],  \
+                    st.stats, d_bad);                                                                      \
         else if (bidi_cfg.lite)                                                                            \
-            KLAUNCH(lite_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
-                    frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
-                    list[0], &spill_count[0], st.stats, d_bad);                                            \
+            KLAUNCH((lite_host_kernel<K, LiteShared<384, 64, 128>>),                                       \
+                    dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec, src->roots, \
+                    src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],  \
+                    st.stats, d_bad);                                                                      \
         else                                                                                               \
             KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
                     frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
