@@ -1817,7 +1817,7 @@ struct LiteShared {
     uint32_t ring_sd[FF + FB];             // slot | seed << 14 | degree << 16 (forward ring, then backward)
     uint32_t ring_bg[FF + FB];             // the row's first record; a seed entry: its request
     unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
-    uint32_t e_beg[64];                    // the chunk's entries' first records (a seed entry: its request)
+    unsigned long long e_beg[64];          // the chunk's entries' first records
     uint32_t c_pre[64];                    // owner map
     uint32_t c_pre2[64];                   // owner map of the prefetched forward seed rows (level 0)
     uint32_t root[16];
@@ -1836,6 +1836,10 @@ struct LiteShared {
 // (or the table is full)
 template <int H>
 __device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
+    if constexpr ((H & (H - 1)) == 0) {  // a power of two: bidi_kernel's probe (masked wrap)
+        constexpr int L = __builtin_ctz(H);
+        return bidi_slot<L>(key, u, insert, inserted);
+    }
     uint32_t hh = (uint32_t)(((uint64_t)(u * 2654435761u) * (uint64_t)H) >> 32);
     for (int p = 0; p < H; p++) {
         const uint32_t kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
@@ -1908,8 +1912,8 @@ struct LiteEdge {
 };
 
 template <class SH, int D, bool SEED>
-__device__ __forceinline__ void lite_fetch(SH &S, const DevGraph &g, const FRec *rec, uint32_t *own, uint32_t my_deg,
-                                           uint32_t start, uint32_t total, uint32_t eb, uint64_t seeds, LiteEdge &x) {
+__device__ __forceinline__ void lite_fetch(SH &S, const FRec *rec, uint32_t *own, uint32_t my_deg, uint32_t start,
+                                           uint32_t total, uint32_t eb, LiteEdge &x) {
     const uint32_t lane = threadIdx.x;
     if (my_deg && start < eb + 64 && start + my_deg > eb) own[(start > eb ? start : eb) - eb] = lane;
     __syncthreads();
@@ -1917,15 +1921,7 @@ __device__ __forceinline__ void lite_fetch(SH &S, const DevGraph &g, const FRec 
     x.lo = (uint32_t)(o < 0 ? 0 : o);
     x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
     const uint32_t e = min(eb + lane, total - 1);
-    // a seed row's begin is 64-bit (sbase); an interior row's the record's own 32 bits,
-    // shifted by the test knob like sbase (rec is taken back by it)
-    unsigned long long b0;
-    if (SEED) {
-        b0 = S.sbase[D][x.lo & 15];
-    } else {
-        const uint32_t w = S.e_beg[x.lo];
-        b0 = (seeds >> x.lo) & 1ull ? S.sbase[D][w & 15] : (unsigned long long)w + g.seed_shift;
-    }
+    const unsigned long long b0 = SEED ? S.sbase[D][x.lo & 15] : S.e_beg[x.lo];
     x.rc = rec[b0 + (e - x.ls)];
 }
 
@@ -1936,13 +1932,13 @@ __device__ __forceinline__ void lite_fetch0(SH &S, const DevGraph &g, const FRec
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     own[threadIdx.x] = 0xFFFFFFFFu;
-    if (total) lite_fetch<SH, D, SEED>(S, g, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, 0, x);
+    if (total) lite_fetch<SH, D, SEED>(S, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, x);
 }
 
 template <class SH, int D, bool SEED = false>
 __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                             uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc,
-                                            uint32_t *own, const LiteEdge *pre = nullptr, uint64_t seeds = 0) {
+                                            uint32_t *own, const LiteEdge *pre = nullptr) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
@@ -1970,21 +1966,21 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
         a = *pre;
     } else {
         own[lane] = 0xFFFFFFFFu;
-        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, 0, seeds, a);
+        lite_fetch<SH, D, SEED>(S, rec, own, my_deg, start, total, 0, a);
     }
     if (total <= 64) {  // one chunk (the common level): no pipelining to pay for
         push(0, a);
         return;
     }
     for (uint32_t eb = 0;;) {
-        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, eb + 64, seeds, b);
+        lite_fetch<SH, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, b);
         push(eb, a);
         eb += 64;
         if (eb + 64 >= total) {
             push(eb, b);
             break;
         }
-        lite_fetch<SH, D, SEED>(S, g, rec, own, my_deg, start, total, eb + 64, seeds, a);
+        lite_fetch<SH, D, SEED>(S, rec, own, my_deg, start, total, eb + 64, a);
         push(eb, b);
         eb += 64;
         if (eb + 64 >= total) {
@@ -2005,21 +2001,20 @@ __device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec 
     for (uint32_t c = h0; c < t0; c += 64) {
         const uint32_t i = c + lane;
         uint32_t deg = 0, take = 0;
-        bool seed = false;
         if (i < t0) {
             const uint32_t w = S.template sd<D>(i), bg = S.template bg<D>(i);
             const uint32_t s = w & 0x3FFFu;
             const unsigned long long old = atomicAnd(&S.st[s], ~(0xFFFFull << (32 * D + 16)));
             take = (uint32_t)(old >> (32 * D + 16)) & open;
             deg = take ? w >> 16 : 0u;
-            seed = (w >> 14) & 1u;
-            S.e_beg[lane] = bg;
+            // a seed row's begin is 64-bit (sbase); an interior row's is the record's 32 bits,
+            // shifted like sbase by the test knob (rec is taken back by it)
+            S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & 15] : (unsigned long long)bg + g.seed_shift;
         }
-        const uint64_t seeds = __ballot(seed);
         S.e_mask[lane] = (uint16_t)take;
         if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
         __syncthreads();
-        lite_expand<SH, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre, nullptr, seeds);
+        lite_expand<SH, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre);
         __syncthreads();
     }
 }
@@ -2797,6 +2792,9 @@ struct ketogpu_engine {
             if (c.hlog == 9)
                 KLAUNCH((lite_kernel<LiteShared<512, kLiteF, kLiteF>>), dim3(grid), dim3(64), pad, stream, g, frec,
                         brec, q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
+            else if (c.hlog == 10)
+                KLAUNCH((lite_kernel<LiteShared<512, 64, 128>>), dim3(grid), dim3(64), pad, stream, g, frec,
+                        brec, q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
             else
                 KLAUNCH((lite_kernel<LiteShared<384, 64, 128>>), dim3(grid), dim3(64), pad, stream, g, frec, brec,
                         q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
@@ -3114,8 +3112,10 @@ struct ketogpu_engine {
             use_bidi = true;
             bidi_cfg.lite = 1;
             // KETOGPU_LITE=512: the wide shape (512 slots, 128-entry rings); default slim (384 slots)
+            // KETOGPU_LITE=512s: 512 slots with the slim rings (an A/B shape, HBM-resident batches)
             const char *ls = getenv("KETOGPU_LITE");
-            bidi_cfg.hlog = ls && atoi(ls) == 512 ? 9 : 8;
+            const std::string lsh = ls ? ls : "";
+            bidi_cfg.hlog = lsh == "512" ? 9 : lsh == "512s" ? 10 : 8;
             bidi_cfg.f = bidi_cfg.hlog == 9 ? kLiteF : 64;
         }
         trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
