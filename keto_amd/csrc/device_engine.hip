@@ -1801,10 +1801,12 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
 //     below Ni come first) fit 32-bit record begins (round-2 verdict item 6).
 // Dead ends are looked up, not stored, as in bidi_kernel.  Same answers, same spill
 // protocol (a spilled unit re-runs on the bidi cascade w, q, s).
-constexpr int kLiteF = 128;  // ring entries per direction (wide shape)
-// the two table shapes: "wide" 512 slots, 128-entry rings; "slim" (default) 384 slots,
-// 64 forward / 128 backward ring entries — 7.4 instead of 9.7 KB of LDS, 21 instead of 16
-// units per CU (config #2: slots p99 230, rings p99 35 / 72 per unit, KETOGPU_STAMPS)
+constexpr int kLiteF = 128;  // ring entries per direction
+// Table shape: 512 slots, 128-entry rings (9.7 KB of LDS, 16 units per CU).  Measured on
+// config #2 (profiles/r03/ab_lite_shapes): a 384-slot table with 64/128-entry rings (7.4 KB,
+// 21 units per CU; slots p99 230 and rings p99 35 / 72 per unit fit it) ran 0.299 vs 0.284
+// ms per 10^6 requests, 512 slots with those rings 0.290: more units in flight do not pay
+// for the non-power-of-two probe, and the first stage is not occupancy-bound here.
 template <int H, int FF, int FB> struct LiteShared;
 
 template <int H_, int FF_, int FB_>
@@ -1831,6 +1833,8 @@ struct LiteShared {
     template <int D>
     __device__ __forceinline__ uint32_t &bg(uint32_t i) { return ring_bg[(D ? FF : 0) + i % (D ? FB : FF)]; }
 };
+
+using LiteShape = LiteShared<512, kLiteF, kLiteF>;
 
 // find (insert == false) or find-or-insert u in a table of H slots (any H); -1 when absent
 // (or the table is full)
@@ -2789,15 +2793,8 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
-            if (c.hlog == 9)
-                KLAUNCH((lite_kernel<LiteShared<512, kLiteF, kLiteF>>), dim3(grid), dim3(64), pad, stream, g, frec,
-                        brec, q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
-            else if (c.hlog == 10)
-                KLAUNCH((lite_kernel<LiteShared<512, 64, 128>>), dim3(grid), dim3(64), pad, stream, g, frec,
-                        brec, q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
-            else
-                KLAUNCH((lite_kernel<LiteShared<384, 64, 128>>), dim3(grid), dim3(64), pad, stream, g, frec, brec,
-                        q.roots, q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
+            KLAUNCH((lite_kernel<LiteShape>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets,
+                    q.n, q.allowed, out, out_count, stats, unit0, stp);
             return;
         }
         if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
@@ -3111,12 +3108,8 @@ struct ketogpu_engine {
         if (p == "lite" && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
             bidi_cfg.lite = 1;
-            // KETOGPU_LITE=512: the wide shape (512 slots, 128-entry rings); default slim (384 slots)
-            // KETOGPU_LITE=512s: 512 slots with the slim rings (an A/B shape, HBM-resident batches)
-            const char *ls = getenv("KETOGPU_LITE");
-            const std::string lsh = ls ? ls : "";
-            bidi_cfg.hlog = lsh == "512" ? 9 : lsh == "512s" ? 10 : 8;
-            bidi_cfg.f = bidi_cfg.hlog == 9 ? kLiteF : 64;
+            bidi_cfg.hlog = 9;
+            bidi_cfg.f = kLiteF;
         }
         trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
@@ -3136,10 +3129,7 @@ struct ketogpu_engine {
                 candidates.push_back({true, c.hlog, c.bt, c.f, c.lf, 0, true, c.u, c.wpe});
                 if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
             }
-            if (use_lite) {  // plan "lite": the slim and the wide table shapes
-                candidates.push_back({true, 8, 64, 64, 7, 0, true, 16, 1, 1});
-                candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});
-            }
+            if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
             if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
             use_bidi = use_bidi || use_lite;
         }
@@ -3519,16 +3509,10 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite && bidi_cfg.hlog == 9)                                                           \
-            KLAUNCH((lite_host_kernel<K, LiteShared<512, kLiteF, kLiteF>>),                               \
-                    dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec, src->roots, \
-                    src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],  \
-                    st.stats, d_bad);                                                                      \
-        else if (bidi_cfg.lite)                                                                            \
-            KLAUNCH((lite_host_kernel<K, LiteShared<384, 64, 128>>),                                       \
-                    dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, frec, brec, src->roots, \
-                    src->targets, io->d_roots, io->d_targets, q.n, q.allowed, list[0], &spill_count[0],  \
-                    st.stats, d_bad);                                                                      \
+        if (bidi_cfg.lite)                                                                                 \
+            KLAUNCH((lite_host_kernel<K, LiteShape>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0,   \
+                    stream, g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n,      \
+                    q.allowed, list[0], &spill_count[0], st.stats, d_bad);                                 \
         else                                                                                               \
             KLAUNCH(bidi_host_kernel<K>, dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g,   \
                     frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \

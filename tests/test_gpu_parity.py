@@ -47,7 +47,7 @@ def test_nil_subject_is_bad_request():
         eng.SubjectIsAllowed(rt.InternalRelationTuple("n", "o", "r", None))
 
 
-@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift", "lite512"])
+@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift"])
 def unit_plan(request, monkeypatch):
     """first LDS pass of engines created while active: the default bidirectional units
     (one-wave, 512-slot tables), bidi with the wide 2048-slot table, forward-only unit2, or
@@ -59,8 +59,6 @@ def unit_plan(request, monkeypatch):
         monkeypatch.setenv("KETOGPU_UNITS", "lite")
         if request.param == "lite-shift":
             monkeypatch.setenv("KETOGPU_TEST_BEGIN_SHIFT", str(3 << 32))
-        if request.param == "lite512":  # the wide shape: 512-slot tables, 128-entry rings
-            monkeypatch.setenv("KETOGPU_LITE", "512")
     else:
         monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     if request.param == "bidi-wide":
