@@ -1840,9 +1840,29 @@ using LiteShape = LiteShared<512, kLiteF, kLiteF>;
 // (or the table is full)
 template <int H>
 __device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
-    if constexpr ((H & (H - 1)) == 0) {  // a power of two: bidi_kernel's probe (masked wrap)
+    if constexpr ((H & (H - 1)) == 0) {
+        // a power of two: the first probe straight-line (most pushes end there: the table
+        // is at most 7/8 full and usually far below), the rare collisions in a rolled loop
+        // (an unrolled probe loop paid ~14 scalar exec-mask instructions on every exit)
         constexpr int L = __builtin_ctz(H);
-        return bidi_slot<L>(key, u, insert, inserted);
+        uint32_t hh = (u * 2654435761u) >> (32 - L);
+        uint32_t kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
+        if (kv == kEmpty) {
+            inserted = insert;
+            return insert ? (int)hh : -1;
+        }
+        if (kv == u) return (int)hh;
+#pragma unroll 1
+        for (int p = 1; p < H; p++) {
+            hh = (hh + 1) & (H - 1);
+            kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
+            if (kv == kEmpty) {
+                inserted = insert;
+                return insert ? (int)hh : -1;
+            }
+            if (kv == u) return (int)hh;
+        }
+        return -1;
     }
     uint32_t hh = (uint32_t)(((uint64_t)(u * 2654435761u) * (uint64_t)H) >> 32);
     for (int p = 0; p < H; p++) {
@@ -1860,6 +1880,7 @@ __device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert,
 
 struct LiteLevel {
     uint32_t lookup, sread;  // for the direction being expanded
+    uint32_t head;           // the direction's ring: entries before it are read (ring_size check)
 };
 
 // one lane's push of node u (record fields deg / begin) in direction D
@@ -1895,7 +1916,7 @@ __device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, 
     }
     const uint32_t idx = lds_append(app, &S.tail[D]);
     if (app) {
-        if (idx - S.head[D] < (uint32_t)SH::template ring_size<D>() && deg <= 0xFFFFu) {
+        if (idx - L.head < (uint32_t)SH::template ring_size<D>() && deg <= 0xFFFFu) {
             S.template sd<D>(idx) = (uint32_t)h | (deg << 16);
             S.template bg<D>(idx) = begin;
         } else {
@@ -1997,8 +2018,8 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
 // consume direction D's ring (every pending row: one atomic reads and clears its pending
 // bits of D) and expand it
 template <class SH, int D>
-__device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
-                                           uint32_t open, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
+__device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec *rec, LiteLevel L, uint32_t open,
+                                           uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
     const uint32_t lane = threadIdx.x;
     const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.head[D]);
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.tail[D]);
@@ -2016,7 +2037,8 @@ __device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec 
             S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & 15] : (unsigned long long)bg + g.seed_shift;
         }
         S.e_mask[lane] = (uint16_t)take;
-        if (lane == 0) S.head[D] = min(c + 64, t0);  // these entries are read: their ring slots are free
+        L.head = min(c + 64, t0);  // these entries are read: their ring slots are free
+        if (lane == 0) S.head[D] = L.head;
         __syncthreads();
         lite_expand<SH, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre);
         __syncthreads();
@@ -2117,9 +2139,9 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         // the two dependent expansions of level 0 wait for HBM once
         LiteEdge f0{};
         lite_fetch0<SH, 0, true>(S, g, frec, S.c_pre2, df, f0);
-        lite_expand<SH, 1, true>(S, g, brec, LiteLevel{0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
+        lite_expand<SH, 1, true>(S, g, brec, LiteLevel{0, 0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
         __syncthreads();
-        lite_expand<SH, 0, true>(S, g, frec, LiteLevel{0, eager_mask}, df, edges, acc_or[0], acc_deg[0],
+        lite_expand<SH, 0, true>(S, g, frec, LiteLevel{0, eager_mask, 0}, df, edges, acc_or[0], acc_deg[0],
                                       S.c_pre2, &f0);
         __syncthreads();
         pf |= wave_or_all(acc_or[0]);
@@ -2161,12 +2183,12 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         // seed row was read in an earlier level (it can meet nothing else)
         n_levels++;
         if (do_f) {
-            const LiteLevel L{open & bc, ~tpend};
+            const LiteLevel L{open & bc, ~tpend, 0};
             acc_or[0] = acc_deg[0] = 0;
             lite_level<SH, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
         }
         if (do_b) {
-            const LiteLevel L{open & fc, ~rpend};
+            const LiteLevel L{open & fc, ~rpend, 0};
             acc_or[1] = acc_deg[1] = 0;
             lite_level<SH, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
         }
