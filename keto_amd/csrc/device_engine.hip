@@ -1840,10 +1840,15 @@ using LiteShape = LiteShared<512, kLiteF, kLiteF>;
 // (or the table is full)
 template <int H>
 __device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert, bool &inserted) {
-    if constexpr ((H & (H - 1)) == 0) {
-        // a power of two: the first probe straight-line (most pushes end there: the table
-        // is at most 7/8 full and usually far below), the rare collisions in a rolled loop
-        // (an unrolled probe loop paid ~14 scalar exec-mask instructions on every exit)
+#ifndef KETO_LITE_PEEL
+#define KETO_LITE_PEEL 0
+#endif
+    if constexpr ((H & (H - 1)) == 0 && !KETO_LITE_PEEL) {  // a power of two: bidi_kernel's probe
+        return bidi_slot<__builtin_ctz(H)>(key, u, insert, inserted);
+    } else if constexpr ((H & (H - 1)) == 0) {
+        // KETO_LITE_PEEL=1: the first probe straight-line, collisions in a rolled loop —
+        // fewer exec-mask instructions per push, measured slower (0.298-0.303 vs 0.284 ms
+        // per 10^6 config #2 requests, profiles/r03/ab_lite_peel)
         constexpr int L = __builtin_ctz(H);
         uint32_t hh = (u * 2654435761u) >> (32 - L);
         uint32_t kv = insert ? atomicCAS(&key[hh], kEmpty, u) : key[hh];
