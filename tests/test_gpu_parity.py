@@ -298,7 +298,7 @@ def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
         w.requests(range(len(roots))), nthreads=8)
     eng = check.Engine(snap)
     np.testing.assert_array_equal(eng.check_ids(roots[:1000], targets[:1000]), want[:1000])
-    assert eng.last_stats()["plan"] == 1  # below the trial size: bidi
+    assert eng.last_stats()["plan"] == 5  # below the trial size: lite
     plans = set()
     for _ in range(4):
         np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
