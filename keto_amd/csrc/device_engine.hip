@@ -2766,6 +2766,7 @@ static std::map<uintptr_t, PinnedRange> g_pinned;
 
 struct ketogpu_engine {
     const Snapshot *snap = nullptr;
+    std::shared_ptr<Snapshot::ReaderLink> snap_link;  // cleared when the snapshot is freed first
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
@@ -3062,7 +3063,10 @@ struct ketogpu_engine {
     }
 
     ~ketogpu_engine() {
-        if (snap) snap->reader_gone(this);
+        if (snap_link) {
+            std::lock_guard<std::mutex> lk(snap_link->mu);
+            if (snap_link->snap) snap_link->snap->reader_gone(this);
+        }
         // every stream of the engine drains before anything it may read or write is freed
         // (the chunk pipeline's copies run on copy_stream and its launches on stream2)
         (void)hipSetDevice(device);
@@ -4142,6 +4146,11 @@ int ketogpu_engine_new(const ketogpu_snapshot *s, const ketogpu_engine_opts *opt
     e->synced_version = snap.version;  // built from the current rows
     e->patch_pos = snap.patch_end();
     snap.reader_at(e.get(), e->patch_pos);
+    e->snap_link = snap.link;
+    {
+        std::lock_guard<std::mutex> lk(snap.link->mu);
+        snap.link->snap = &snap;
+    }
     *out = e.release();
     API_END
 }

@@ -194,7 +194,7 @@ struct Snapshot {
     std::vector<Patch> patches;         // device rows changed, in write order (engines replay)
     uint64_t patch_base = 0;            // patches trimmed off the front (absolute index of patches[0])
     // engines over this snapshot -> the absolute patch position each has replayed up to;
-    // a write trims the log below the smallest (an engine must be freed before its snapshot)
+    // a write trims the log below the smallest
     mutable std::mutex readers_mu;
     mutable std::map<const void *, uint64_t> readers;
     void reader_at(const void *who, uint64_t pos) const {
@@ -219,6 +219,21 @@ struct Snapshot {
         }
     }
     mutable std::shared_mutex mu;       // writes exclusive; engine, resolve and expand calls shared
+    // An engine's way back to its snapshot at teardown: the snapshot's destructor clears it,
+    // so an engine freed after its snapshot (a garbage collector's order) skips the
+    // deregistration instead of touching freed memory.
+    struct ReaderLink {
+        std::mutex mu;
+        const Snapshot *snap = nullptr;
+    };
+    std::shared_ptr<ReaderLink> link = std::make_shared<ReaderLink>();
+    Snapshot() = default;
+    Snapshot(const Snapshot &) = delete;
+    Snapshot &operator=(const Snapshot &) = delete;
+    ~Snapshot() {
+        std::lock_guard<std::mutex> lk(link->mu);
+        link->snap = nullptr;
+    }
 
     // ---- helpers
     const Namespace *ns_by_name(std::string_view name) const {

@@ -217,3 +217,21 @@ def test_pinned_subrange_pointers_every_engine(rbac):
             eng.check_ids_raw(pr.p.value + 4 * off, pt.p.value + 4 * off, n, out.p.value + 8 * 3)
             np.testing.assert_array_equal(check.unpack_bits(out.array[3:3 + words].copy(), n), want)
             assert not out.array[:3].any()
+
+
+@pytest.mark.gpu
+def test_engines_freed_after_their_snapshot():
+    """a garbage collector may finalise a snapshot before the engines over it (a reference
+    cycle): engine teardown then skips the snapshot's reader registry instead of touching
+    freed memory (Snapshot::ReaderLink)"""
+    _gpu()
+    w = synth.rbac(users=500, groups=50, docs=100, tuples=3000, checks=200, seed=5)
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    eng = check.Engine(snap)
+    multi = check.MultiEngine(snap, [0])
+    roots, targets = w.resolve(snap)
+    eng.check_ids(roots, targets)
+    multi.check_ids(roots, targets)
+    snap.__del__()  # the snapshot goes first
+    multi.close()
+    eng.close()
