@@ -659,6 +659,94 @@ typedef struct {
 int ketogpu_part_engine_new_steps(const ketogpu_part_steps *steps, ketogpu_comm *c,
                                   const ketogpu_part_engine_opts *opts, ketogpu_part_engine **out);
 
+/* ------------------------------------------- partitioned mode: two-tier */
+/* The same hash-partitioned network (ketogpu_shard_*) checked with TWO exchanges per batch
+ * instead of two per BFS level, when its CORE fits every GPU.  The core is the rows among
+ * interior nodes: fint(v) and the interior predecessors of every interior node v (group
+ * nesting: ~0.3% of config #5's tuples).  Every path r -> v1 -> ... -> t of the reference's
+ * recursion (internal/check/engine.go:33-91) has v1 in fint(r), its last interior node in
+ * rev(t) and everything between inside the core, so each rank keeps a copy of the core and
+ * only the two seed rows of a request live elsewhere:
+ *   queries  request i asks owner(r) for fint(r) and owner(t) for rev(t)  [all-to-all]
+ *   replies  the owners send those rows                                     [all-to-all]
+ *   evaluate the bidirectional LDS unit of the single-GPU engine over the local core
+ * A world of one rank reads its own rows in place (no exchange at all).  Unlike
+ * ketogpu_part_check_ids, every rank passes ITS OWN requests (any number, 0 included)
+ * and gets the answers to them; the call is collective (every rank calls it for each of
+ * its batches, as with the per-level engine).  Requests whose search outgrows the LDS
+ * tables (none on the benchmark graphs) are answered by the per-level engine, built on
+ * first need from the same shard and communicator.  Same answers as ketogpu_check_ids on
+ * the whole graph (the R2 formula, no depth cutoff).
+ *
+ *   ketogpu_core_gather (collective, once per load) -> ketogpu_tier_new -> check_ids ...
+ *
+ * ketogpu_core_gather fails with KETOGPU_ENOMEM on every rank alike when the core passes
+ * core_budget_bytes (the per-level engine is then the partitioned mode to use). */
+typedef struct ketogpu_core ketogpu_core;
+typedef struct {
+    uint32_t num_interior;     /* Ni: core rows                                          */
+    const uint64_t *f_off;     /* Ni + 1: interior successors of each interior node      */
+    const uint32_t *f_col;
+    const uint64_t *b_off;     /* Ni + 1: interior predecessors of each interior node    */
+    const uint32_t *b_col;
+    uint64_t bytes;            /* device bytes of the core's records                     */
+} ketogpu_core_view;
+/* opts: the shard's; comm NULL for a single rank.  core_budget_bytes 0: no limit here */
+int ketogpu_core_gather(const ketogpu_shard *s, ketogpu_comm *comm, uint64_t core_budget_bytes, ketogpu_core **out);
+int ketogpu_core_get_view(const ketogpu_core *c, ketogpu_core_view *out);
+void ketogpu_core_free(ketogpu_core *c);
+
+typedef struct ketogpu_tier ketogpu_tier;
+typedef struct {
+    int32_t device;
+    uint64_t max_batch;            /* requests evaluated per step; 0 = 4M                */
+    uint64_t fallback_state_bytes; /* the per-level engine's state budget; 0 = 2 GB      */
+} ketogpu_tier_opts;
+/* a request's query in transit: tag = request index << 1 | 0 (fint(r)) / 1 (rev(t)) */
+typedef struct {
+    uint32_t tag, node;
+} ketogpu_tier_query;
+/* a row entry in transit: the entry's node, its core row (count, first record), tag */
+typedef struct {
+    uint32_t node, deg, begin, tag;
+} ketogpu_tier_rec;
+typedef struct {
+    uint64_t calls, batches, requests, overflow_requests, fallback_calls;
+    uint64_t queries_sent, records_sent, records_received, collectives;
+    uint64_t rows_opened, records_read; /* device statistics of the evaluation      */
+    double exchange_ms, evaluate_ms;    /* host wall time inside collectives / evaluation */
+    uint64_t core_records, seed_records; /* device records: core (both directions), own rows */
+} ketogpu_tier_stats;
+/* the shard and core stay owned by the caller; the tier borrows s, core and comm */
+int ketogpu_tier_new(const ketogpu_shard *s, const ketogpu_core *core, ketogpu_comm *comm,
+                     const ketogpu_tier_opts *opts, ketogpu_tier **out);
+/* this rank's n requests (host memory; pinned buffers are read in place at world 1) ->
+ * ceil(n/64) words of answer bits.  An id outside the layout fails the call with
+ * KETOGPU_EINVAL on that rank (its peers fail with the same code). */
+int ketogpu_tier_check_ids(ketogpu_tier *t, const uint32_t *roots, const uint32_t *targets, size_t n,
+                           uint64_t *allowed_bits);
+int ketogpu_tier_stats_get(ketogpu_tier *t, ketogpu_tier_stats *out);
+void ketogpu_tier_free(ketogpu_tier *t);
+/* Test hook: the same protocol over caller steps in host memory (tests/tier_cpu.py).
+ * queries: this rank's requests -> queries grouped by owner (counts[world]);
+ * reply_sizes: received queries (grouped by source, from[world] each) -> records per
+ * destination (counts[world]); reply_emit: those records, in query order;
+ * evaluate: the answers (recv NULL: the rank owns every row, world 1) and the indices of
+ * requests it could not finish (overflow; none for host steps). */
+typedef struct {
+    void *ctx;
+    int (*queries)(void *ctx, const uint32_t *roots, const uint32_t *targets, uint64_t n, ketogpu_tier_query *send,
+                   uint64_t *counts);
+    int (*reply_sizes)(void *ctx, const ketogpu_tier_query *recv, uint64_t n, const uint64_t *from,
+                       uint64_t *counts);
+    int (*reply_emit)(void *ctx, ketogpu_tier_rec *send);
+    int (*evaluate)(void *ctx, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                    const ketogpu_tier_rec *recv, uint64_t nrecv, uint64_t *allowed_bits, uint32_t *overflow,
+                    uint64_t *n_overflow);
+} ketogpu_tier_steps;
+int ketogpu_tier_new_steps(const ketogpu_tier_steps *steps, ketogpu_comm *comm, const ketogpu_tier_opts *opts,
+                           ketogpu_tier **out);
+
 /* ------------------------------------------------------------------ expand */
 /* BuildTree(subject, rest_depth).  *out = NULL is the nil tree (JSON null).
  * KETOGPU_ENOTFOUND when a fetched page references an unknown namespace. */

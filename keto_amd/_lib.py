@@ -234,6 +234,42 @@ class PartSteps(C.Structure):
                 ("abort", STEP_FN)]
 
 
+# include/ketogpu.h two-tier partitioned mode
+class CoreView(C.Structure):
+    _fields_ = [("num_interior", C.c_uint32), ("f_off", C.POINTER(C.c_uint64)), ("f_col", C.POINTER(C.c_uint32)),
+                ("b_off", C.POINTER(C.c_uint64)), ("b_col", C.POINTER(C.c_uint32)), ("bytes", C.c_uint64)]
+
+
+class TierOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_batch", C.c_uint64), ("fallback_state_bytes", C.c_uint64)]
+
+
+class TierStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "calls", "batches", "requests", "overflow_requests", "fallback_calls", "queries_sent", "records_sent",
+        "records_received", "collectives", "rows_opened", "records_read")] + [
+        ("exchange_ms", C.c_double), ("evaluate_ms", C.c_double), ("core_records", C.c_uint64),
+        ("seed_records", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+TIER_QUERIES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint64,
+                              C.c_void_p, C.POINTER(C.c_uint64))
+TIER_REPLY_SIZES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint64))
+TIER_REPLY_EMIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
+TIER_EVALUATE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint64,
+                               C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                               C.POINTER(C.c_uint64))
+
+
+class TierSteps(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("queries", TIER_QUERIES_FN), ("reply_sizes", TIER_REPLY_SIZES_FN),
+                ("reply_emit", TIER_REPLY_EMIT_FN), ("evaluate", TIER_EVALUATE_FN)]
+
+
 # every symbol declared in include/ketogpu.h, with its ctypes signature
 vp, i32, u32, sz = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
 SIGNATURES = {
@@ -325,6 +361,14 @@ SIGNATURES = {
     "ketogpu_part_check_ids": (C.c_int, [vp, vp, vp, sz, vp]),
     "ketogpu_part_engine_stats_get": (C.c_int, [vp, C.POINTER(PartEngineStats)]),
     "ketogpu_part_engine_free": (None, [vp]),
+    "ketogpu_core_gather": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
+    "ketogpu_core_get_view": (C.c_int, [vp, C.POINTER(CoreView)]),
+    "ketogpu_core_free": (None, [vp]),
+    "ketogpu_tier_new": (C.c_int, [vp, vp, vp, C.POINTER(TierOpts), C.POINTER(vp)]),
+    "ketogpu_tier_new_steps": (C.c_int, [C.POINTER(TierSteps), vp, C.POINTER(TierOpts), C.POINTER(vp)]),
+    "ketogpu_tier_check_ids": (C.c_int, [vp, vp, vp, sz, vp]),
+    "ketogpu_tier_stats_get": (C.c_int, [vp, C.POINTER(TierStats)]),
+    "ketogpu_tier_free": (None, [vp]),
 }
 
 _lib = None

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "device_util.hpp"
+#include "tier.hpp"
 #include "ketogpu_internal.hpp"
 
 using namespace ketogpu;
@@ -2076,7 +2077,9 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     if (lane < 16) {
         if (r != KETOGPU_NODE_NONE && r < kDynBase) {
             rows += 2;
-            if (seed.re > seed.rb) atomicOr(&S.active, 1u << lane);  // nothing reaches a t without predecessors
+            // nothing reaches a t without predecessors (!=: the two-tier mode's begins are
+            // offsets from another array and may wrap, tier.hpp)
+            if (seed.re != seed.rb) atomicOr(&S.active, 1u << lane);
         }
         if (r != KETOGPU_NODE_NONE && r >= kDynBase) S.spill = 1;
         S.root[lane] = r;
@@ -2293,6 +2296,319 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
             if (j == k) rk = r[j], tk = t[j];
         lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
         __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------- two-tier mode
+// Kernels of the two-tier partitioned mode (tier.hpp, tier.cpp).  The evaluation is
+// lite_unit over the rank's copy of the CORE (core_f / core_b: the rows among interior
+// nodes, replicated) with seed rows that are either the rank's own rows read in place
+// (world 1) or the rows the owners sent (recv, bounds per request): a seed's begins are
+// offsets from core_f / core_b to the seed array (they may be "negative", i.e. wrap),
+// which is all lite_unit needs to read them.
+using TierStage1 = LiteShared<2048, 512, 512>;
+using TierStage2 = LiteShared<8192, 1024, 1024>;
+
+// owner and local index of global id v (shard.cpp layout: ids interleave the ranks inside
+// each class range); NONE when another rank owns v or the slot is unused
+__device__ __forceinline__ uint32_t tier_local(const tier::Graph &G, uint32_t v) {
+    uint32_t base, l0, lim;
+    if (v < G.Ni) {
+        base = 0, l0 = 0, lim = G.Nil;
+    } else if (v < G.Nx) {
+        base = G.Ni, l0 = G.Nil, lim = G.Nxl;
+    } else {
+        base = G.Nx, l0 = G.Nxl, lim = G.Nl;
+    }
+    if (v >= G.N || (v - base) % G.world != G.rank) return KETOGPU_NODE_NONE;
+    const uint32_t l = l0 + (v - base) / G.world;
+    return l < lim ? l : KETOGPU_NODE_NONE;
+}
+__device__ __forceinline__ uint32_t tier_owner(const tier::Graph &G, uint32_t v) {
+    const uint32_t base = v < G.Ni ? 0u : v < G.Nx ? G.Ni : G.Nx;
+    return (v - base) % G.world;
+}
+
+// request c's ids, validated like validate_kernel (an id outside the layout: first_bad,
+// and the request is answered false)
+__device__ __forceinline__ void tier_request(const tier::Graph &G, const tier::Eval &E, uint64_t c, uint32_t &r,
+                                             uint32_t &t) {
+    r = t = KETOGPU_NODE_NONE;
+    if (c >= E.n) return;
+    r = E.roots[c];
+    t = E.targets[c];
+    if ((r != KETOGPU_NODE_NONE && r >= G.Nx) || (t != KETOGPU_NODE_NONE && t >= G.N)) {
+        atomicMin(E.first_bad, (unsigned long long)c);
+        r = t = KETOGPU_NODE_NONE;
+    }
+    if (t == KETOGPU_NODE_NONE) r = KETOGPU_NODE_NONE;
+}
+
+template <bool DIRECT>
+__device__ __forceinline__ BidiSeed tier_seed(const tier::Graph &G, const tier::Eval &E, uint64_t unit) {
+    BidiSeed s{KETOGPU_NODE_NONE, KETOGPU_NODE_NONE, 0, 0, 0, 0};
+    if (threadIdx.x >= 16) return s;
+    const uint64_t c = unit * 16 + threadIdx.x;
+    tier_request(G, E, c, s.r, s.t);
+    if (s.r == KETOGPU_NODE_NONE) return s;
+    if constexpr (DIRECT) {
+        const uint32_t lr = tier_local(G, s.r), lt = tier_local(G, s.t);
+        uint64_t fb = 0, fe = 0, rb = 0, re = 0;
+        if (lr != KETOGPU_NODE_NONE && lr < G.Nxl) fb = G.lf_off[lr], fe = G.lf_off[lr + 1];
+        if (lt != KETOGPU_NODE_NONE) rb = G.lr_off[lt], re = G.lr_off[lt + 1];
+        s.fb = (uint64_t)G.lf_base + fb;
+        s.fe = (uint64_t)G.lf_base + fe;
+        s.rb = (uint64_t)G.lr_base + rb;
+        s.re = (uint64_t)G.lr_base + re;
+    } else {
+        const uint4 b = E.bnd[c];
+        s.fb = (uint64_t)E.recv_base_f + b.x;
+        s.fe = (uint64_t)E.recv_base_f + b.y;
+        s.rb = (uint64_t)E.recv_base_b + b.z;
+        s.re = (uint64_t)E.recv_base_b + b.w;
+    }
+    return s;
+}
+
+__device__ __forceinline__ DevGraph tier_devgraph(const tier::Graph &G) {
+    DevGraph g{};
+    g.Ni = G.Ni;
+    g.Nx = G.Nx;
+    g.N = G.N;
+    g.both_max = G.both_max;
+    g.seed_max = G.seed_max;
+    g.seed_shift = 0;
+    return g;
+}
+
+// stage 0: one unit per workgroup
+template <class SH, bool DIRECT>
+__global__ __launch_bounds__(64) void tier_eval_kernel(tier::Graph G, tier::Eval E, uint32_t *spill_out,
+                                                       unsigned int *spill_count) {
+    __shared__ SH S;
+    const uint64_t unit = blockIdx.x;
+    const DevGraph g = tier_devgraph(G);
+    lite_unit<SH>(S, g, reinterpret_cast<const FRec *>(G.core_f), reinterpret_cast<const FRec *>(G.core_b),
+                  tier_seed<DIRECT>(G, E, unit), E.allowed, unit, spill_out, spill_count, E.stats);
+}
+
+// stages 1 and 2: persistent over the previous stage's spilled units
+template <class SH, bool DIRECT>
+__global__ __launch_bounds__(64) void tier_cascade_kernel(tier::Graph G, tier::Eval E, const uint32_t *in_list,
+                                                          const unsigned int *in_count, uint32_t *spill_out,
+                                                          unsigned int *spill_count) {
+    __shared__ SH S;
+    const DevGraph g = tier_devgraph(G);
+    const uint32_t cnt = *in_count;
+    for (uint32_t b = blockIdx.x; b < cnt; b += gridDim.x) {
+        const uint64_t unit = in_list[b];
+        lite_unit<SH>(S, g, reinterpret_cast<const FRec *>(G.core_f), reinterpret_cast<const FRec *>(G.core_b),
+                      tier_seed<DIRECT>(G, E, unit), E.allowed, unit, spill_out, spill_count, E.stats);
+        __syncthreads();
+    }
+}
+
+// queries of the batch: request i asks owner(r) for fint(r) (tag 2i) and owner(t) for
+// rev(t) (tag 2i + 1).  Counting pass: per-destination totals (LDS histogram per block).
+constexpr int kTB = 256;
+__global__ __launch_bounds__(kTB) void tier_query_count_kernel(tier::Graph G, const uint32_t *roots,
+                                                               const uint32_t *targets, uint64_t n,
+                                                               unsigned long long *counts,
+                                                               unsigned long long *first_bad) {
+    __shared__ unsigned int hist[64];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kTB) {
+        const uint32_t r = roots[i], t = targets[i];
+        if ((r != KETOGPU_NODE_NONE && r >= G.Nx) || (t != KETOGPU_NODE_NONE && t >= G.N)) {
+            atomicMin(first_bad, (unsigned long long)i);
+            continue;
+        }
+        if (r == KETOGPU_NODE_NONE || t == KETOGPU_NODE_NONE) continue;
+        atomicAdd(&hist[tier_owner(G, r)], 1u);
+        atomicAdd(&hist[tier_owner(G, t)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < G.world && hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
+}
+
+// scatter pass: per block, an LDS count per destination reserves one range per
+// (block, destination) at the global cursor; lanes place their queries inside it
+__global__ __launch_bounds__(kTB) void tier_query_scatter_kernel(tier::Graph G, const uint32_t *roots,
+                                                                 const uint32_t *targets, uint64_t n,
+                                                                 unsigned long long *cursor, tier::Query *out) {
+    __shared__ unsigned int hist[64];
+    __shared__ unsigned long long at[64];
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kTB; i0 < n; i0 += (uint64_t)gridDim.x * kTB) {
+        if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t i = i0 + threadIdx.x;
+        uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE, dr = 0, dt = 0, pr = 0, pt = 0;
+        bool ok = false;
+        if (i < n) {
+            r = roots[i];
+            t = targets[i];
+            ok = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE && r < G.Nx && t < G.N;
+        }
+        if (ok) {
+            dr = tier_owner(G, r);
+            dt = tier_owner(G, t);
+            pr = atomicAdd(&hist[dr], 1u);
+            pt = atomicAdd(&hist[dt], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < G.world)
+            at[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
+        __syncthreads();
+        if (ok) {
+            out[at[dr] + pr] = tier::Query{(uint32_t)(i << 1), r};
+            out[at[dt] + pt] = tier::Query{(uint32_t)(i << 1 | 1), t};
+        }
+        __syncthreads();
+    }
+}
+
+// the owner's side: the length of the row each received query asks for (lens[j]); a
+// query for a node this rank does not own (a misrouted record) raises *bad
+__device__ __forceinline__ void tier_row(const tier::Graph &G, const tier::Query &q, uint64_t &b, uint64_t &e,
+                                         bool &bad) {
+    b = e = 0;
+    bad = false;
+    const uint32_t l = tier_local(G, q.node);
+    if (l == KETOGPU_NODE_NONE) {
+        bad = true;
+        return;
+    }
+    if (q.tag & 1u) {
+        b = G.lr_off[l];
+        e = G.lr_off[l + 1];
+    } else if (l < G.Nxl) {
+        b = G.lf_off[l];
+        e = G.lf_off[l + 1];
+    }
+}
+
+__global__ __launch_bounds__(kTB) void tier_reply_len_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
+                                                             uint64_t *lens, unsigned long long *bad) {
+    for (uint64_t j = (uint64_t)blockIdx.x * kTB + threadIdx.x; j < n; j += (uint64_t)gridDim.x * kTB) {
+        uint64_t b, e;
+        bool miss;
+        tier_row(G, q[j], b, e, miss);
+        if (miss) atomicMin(bad, (unsigned long long)j);
+        lens[j] = e - b;
+    }
+}
+
+// exclusive scan of u64 in place over tiles of kTB * 4: tile sums, the sums' scan (one
+// block), then each tile scanned with its offset; v[n] = the total
+constexpr int kScanTile = kTB * 4;
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t *tmp, uint64_t &total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t incl = wave_incl_scan(x, lane);
+    if (lane == 63) tmp[wv] = incl;
+    __syncthreads();
+    uint64_t before = 0;
+    total = 0;
+    for (int w = 0; w < kTB / 64; w++) {
+        if (w < wv) before += tmp[w];
+        total += tmp[w];
+    }
+    __syncthreads();
+    return before + incl - x;
+}
+__global__ __launch_bounds__(kTB) void tier_scan_sums_kernel(const uint64_t *v, uint64_t n, uint64_t *sums) {
+    __shared__ uint64_t tmp[kTB / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * 4;
+    uint64_t x = 0;
+    for (int k = 0; k < 4; k++)
+        if (base + k < n) x += v[base + k];
+    uint64_t total;
+    block_excl_scan(x, tmp, total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(kTB) void tier_scan_top_kernel(uint64_t *sums, uint64_t nb) {
+    __shared__ uint64_t tmp[kTB / 64];
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += kTB) {
+        const uint64_t i = b0 + threadIdx.x;
+        const uint64_t x = i < nb ? sums[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_excl_scan(x, tmp, total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) sums[nb] = carry;
+}
+__global__ __launch_bounds__(kTB) void tier_scan_tiles_kernel(uint64_t *v, uint64_t n, const uint64_t *sums, uint64_t nb) {
+    __shared__ uint64_t tmp[kTB / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * 4;
+    uint64_t x[4], s = 0;
+    for (int k = 0; k < 4; k++) {
+        x[k] = base + k < n ? v[base + k] : 0;
+        s += x[k];
+    }
+    uint64_t total;
+    uint64_t run = sums[blockIdx.x] + block_excl_scan(s, tmp, total);
+    for (int k = 0; k < 4; k++) {
+        if (base + k < n) v[base + k] = run;
+        run += x[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) v[n] = sums[nb];
+}
+
+// the replies: one wave per 64 queries writes their rows as consecutive records (each
+// output index finds its query by a binary search over the wave's offsets in LDS, so
+// consecutive lanes write consecutive records), pad = the query's tag
+__global__ __launch_bounds__(kTB) void tier_reply_copy_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
+                                                              const uint64_t *off, tier::Rec *out, uint64_t cap) {
+    __shared__ uint64_t s_pre[kTB / 64][65];
+    __shared__ uint64_t s_src[kTB / 64][64];
+    __shared__ uint32_t s_tag[kTB / 64][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t j0 = ((uint64_t)blockIdx.x * (kTB / 64) + wv) * 64; j0 < n; j0 += (uint64_t)gridDim.x * kTB) {
+        const uint64_t j = j0 + lane;
+        uint64_t b = 0, e = 0;
+        uint32_t tag = 0;
+        if (j < n) {
+            bool miss;
+            tier_row(G, q[j], b, e, miss);
+            tag = q[j].tag;
+        }
+        const uint64_t o0 = off[j0];
+        s_pre[wv][lane] = (j < n ? off[j] : off[n]) - o0;
+        s_src[wv][lane] = b;
+        s_tag[wv][lane] = tag;
+        const uint64_t total = (j0 + 64 < n ? off[j0 + 64] : off[n]) - o0;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (uint64_t o = lane; o < total; o += 64) {
+            int lo = 0, hi = 64;  // the last query whose offset is <= o owns it (empty rows never win)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_pre[wv][mid] <= o)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const uint32_t tg = s_tag[wv][lo];
+            const tier::Rec *src = (tg & 1u) ? G.lr_rec : G.lf_rec;
+            tier::Rec rec = src[s_src[wv][lo] + (o - s_pre[wv][lo])];
+            rec.pad = tg;
+            if (o0 + o < cap) out[o0 + o] = rec;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// received replies -> per request seed bounds (each query's row is contiguous)
+__global__ __launch_bounds__(kTB) void tier_bounds_kernel(const tier::Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kTB + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kTB) {
+        const uint32_t tag = recv[k].pad;
+        const uint64_t i = tag >> 1;
+        if (i >= nreq) continue;
+        uint32_t *b = reinterpret_cast<uint32_t *>(&bnd[i]) + 2 * (tag & 1u);
+        if (k == 0 || recv[k - 1].pad != tag) b[0] = (uint32_t)k;
+        if (k + 1 == n || recv[k + 1].pad != tag) b[1] = (uint32_t)(k + 1);
     }
 }
 
@@ -2707,6 +3023,79 @@ T *dupload(const std::vector<T> &v) {
 
 }  // namespace
 
+// ------------------------------------------------ two-tier mode: launches (tier.hpp)
+namespace ketogpu {
+namespace tier {
+
+static_assert(sizeof(Rec) == sizeof(FRec), "tier::Rec is the 16-byte edge record");
+
+int stage_units_per_cu(int stage) { return stage == 1 ? 4 : 1; }
+
+void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_list, const unsigned *in_count,
+                 uint32_t *out_list, unsigned *out_count, unsigned grid, hipStream_t s) {
+    const bool direct = e.bnd == nullptr;
+    if (stage == 0) {
+        if (!e.n) return;
+        const unsigned units = (unsigned)((e.n + 15) / 16);
+        if (direct)
+            KLAUNCH((tier_eval_kernel<LiteShape, true>), dim3(units), dim3(64), 0, s, g, e, out_list, out_count);
+        else
+            KLAUNCH((tier_eval_kernel<LiteShape, false>), dim3(units), dim3(64), 0, s, g, e, out_list, out_count);
+    } else if (stage == 1) {
+        if (direct)
+            KLAUNCH((tier_cascade_kernel<TierStage1, true>), dim3(grid), dim3(64), 0, s, g, e, in_list, in_count, out_list,
+                    out_count);
+        else
+            KLAUNCH((tier_cascade_kernel<TierStage1, false>), dim3(grid), dim3(64), 0, s, g, e, in_list, in_count, out_list,
+                    out_count);
+    } else {
+        if (direct)
+            KLAUNCH((tier_cascade_kernel<TierStage2, true>), dim3(grid), dim3(64), 0, s, g, e, in_list, in_count, out_list,
+                    out_count);
+        else
+            KLAUNCH((tier_cascade_kernel<TierStage2, false>), dim3(grid), dim3(64), 0, s, g, e, in_list, in_count, out_list,
+                    out_count);
+    }
+}
+
+static unsigned tier_grid(uint64_t n, uint64_t per, unsigned cap = 8192) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, cap));
+}
+
+void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                        unsigned long long *counts, unsigned long long *first_bad, hipStream_t s) {
+    if (n) KLAUNCH(tier_query_count_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, roots, targets, n, counts, first_bad);
+}
+
+void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                          unsigned long long *cursor, Query *out, hipStream_t s) {
+    if (n) KLAUNCH(tier_query_scatter_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, roots, targets, n, cursor, out);
+}
+
+void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *lens, unsigned long long *bad,
+                          hipStream_t s) {
+    if (n) KLAUNCH(tier_reply_len_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, q, n, lens, bad);
+}
+
+void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s) {
+    const uint64_t nb = std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile);
+    KLAUNCH(tier_scan_sums_kernel, dim3((unsigned)nb), dim3(kTB), 0, s, v, n, scratch);
+    KLAUNCH(tier_scan_top_kernel, dim3(1), dim3(kTB), 0, s, scratch, nb);
+    KLAUNCH(tier_scan_tiles_kernel, dim3((unsigned)nb), dim3(kTB), 0, s, v, n, scratch, nb);
+}
+
+void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Rec *out, uint64_t cap,
+                       hipStream_t s) {
+    if (n) KLAUNCH(tier_reply_copy_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, out, cap);
+}
+
+void launch_bounds(const Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq, hipStream_t s) {
+    if (n) KLAUNCH(tier_bounds_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, recv, n, bnd, nreq);
+}
+
+}  // namespace tier
+}  // namespace ketogpu
+
 // --------------------------------------------------------------------- engine
 // A batch as the traversal kernels see it (device pointers)
 struct Batch {
@@ -2763,6 +3152,58 @@ struct PinnedRange {
 };
 static std::mutex g_pinned_mu;
 static std::map<uintptr_t, PinnedRange> g_pinned;
+
+namespace ketogpu {
+// `device`'s view of host memory it can read in place (pinned: ketogpu_host_alloc /
+// hipHostMalloc / hipHostRegister; or device memory of `device`), else nullptr (the
+// caller has made `device` current)
+// (pageable memory goes through DMA copies).
+const void *host_view(const void *p, int device, bool query) {
+    if (!p) return nullptr;
+    {  // buffers of ketogpu_host_alloc (portable + mapped): the view of THIS device,
+       // known without a runtime query (~10 us per call) after its first use here
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        auto it = g_pinned.upper_bound((uintptr_t)p);
+        if (it != g_pinned.begin()) {
+            --it;
+            const uintptr_t off = (uintptr_t)p - it->first;
+            if (off < it->second.bytes) {
+                auto d = it->second.dev.find(device);
+                if (d == it->second.dev.end()) {
+                    void *v = nullptr;  // the caller has made `device` current
+                    if (hipHostGetDevicePointer(&v, (void *)it->first, 0) != hipSuccess) {
+                        (void)hipGetLastError();
+                        v = nullptr;
+                    }
+                    d = it->second.dev.emplace(device, (uintptr_t)v).first;
+                }
+                if (d->second) return (const void *)(d->second + off);
+                return nullptr;  // not mappable here: DMA path
+            }
+        }
+    }
+    if (!query) return nullptr;
+    hipPointerAttribute_t at{};
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    static const bool dbg = getenv("KETOGPU_DEBUG_PTR") != nullptr;
+    if (dbg)
+        fprintf(stderr, "[ptr] %p: err %d type %d device %d devptr %p hostptr %p managed %d flags %u\n", p, (int)e,
+                (int)at.type, at.device, at.devicePointer, at.hostPointer, (int)at.isManaged, at.allocationFlags);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the query's error
+        return nullptr;
+    }
+    if (!at.devicePointer) return nullptr;
+    if (at.type == hipMemoryTypeDevice && at.device != device) return nullptr;
+    if (at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeUnified &&
+        at.type != hipMemoryTypeManaged)
+        return nullptr;
+    // the attributes describe the allocation: offset the device view like p
+    const char *host = at.hostPointer ? (const char *)at.hostPointer : (const char *)at.devicePointer;
+    const char *dev = (const char *)at.devicePointer + ((const char *)p - host);
+    return (const void *)dev;
+}
+}  // namespace ketogpu
 
 struct ketogpu_engine {
     const Snapshot *snap = nullptr;
@@ -3948,53 +4389,9 @@ struct ketogpu_engine {
         io = q.release();
     }
 
-    // The device's view of host memory it can read in place (pinned: ketogpu_host_alloc /
-    // hipHostMalloc / hipHostRegister; or device memory of this engine's GPU), else nullptr
-    // (pageable memory goes through DMA copies).
+    // the device's view of host memory it can read in place (host_view), else nullptr
     const uint32_t *device_view(const uint32_t *p, bool query = true) {
-        if (!p) return nullptr;
-        {  // buffers of ketogpu_host_alloc (portable + mapped): the view of THIS device,
-           // known without a runtime query (~10 us per call) after its first use here
-            std::lock_guard<std::mutex> lk(g_pinned_mu);
-            auto it = g_pinned.upper_bound((uintptr_t)p);
-            if (it != g_pinned.begin()) {
-                --it;
-                const uintptr_t off = (uintptr_t)p - it->first;
-                if (off < it->second.bytes) {
-                    auto d = it->second.dev.find(device);
-                    if (d == it->second.dev.end()) {
-                        void *v = nullptr;  // the caller has made `device` current
-                        if (hipHostGetDevicePointer(&v, (void *)it->first, 0) != hipSuccess) {
-                            (void)hipGetLastError();
-                            v = nullptr;
-                        }
-                        d = it->second.dev.emplace(device, (uintptr_t)v).first;
-                    }
-                    if (d->second) return (const uint32_t *)(d->second + off);
-                    return nullptr;  // not mappable here: DMA path
-                }
-            }
-        }
-        if (!query) return nullptr;
-        hipPointerAttribute_t at{};
-        const hipError_t e = hipPointerGetAttributes(&at, p);
-        static const bool dbg = getenv("KETOGPU_DEBUG_PTR") != nullptr;
-        if (dbg)
-            fprintf(stderr, "[ptr] %p: err %d type %d device %d devptr %p hostptr %p managed %d flags %u\n", p, (int)e,
-                    (int)at.type, at.device, at.devicePointer, at.hostPointer, (int)at.isManaged, at.allocationFlags);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();  // pageable memory: clear the query's error
-            return nullptr;
-        }
-        if (!at.devicePointer) return nullptr;
-        if (at.type == hipMemoryTypeDevice && at.device != device) return nullptr;
-        if (at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeUnified &&
-            at.type != hipMemoryTypeManaged)
-            return nullptr;
-        // the attributes describe the allocation: offset the device view like p
-        const char *host = at.hostPointer ? (const char *)at.hostPointer : (const char *)at.devicePointer;
-        const char *dev = (const char *)at.devicePointer + ((const char *)p - host);
-        return (const uint32_t *)dev;
+        return (const uint32_t *)host_view(p, device, query);
     }
 
     void ensure_res(uint64_t n) {

@@ -477,79 +477,89 @@ struct SelfComm : Comm {
 }  // namespace
 
 // ------------------------------------------------ the loader's id exchange
-// Collectives on host arrays over any communicator (RCCL: staged through device memory).
-namespace {
-struct HostColl {
-    Comm *c;
-    std::vector<uint64_t> mat;
-    void *dbuf = nullptr;
-    uint64_t dcap = 0;
-    ~HostColl() {
+// Collectives on host arrays over any communicator (part_round.hpp HostColl; RCCL:
+// staged through device memory).
+namespace ketogpu {
+HostColl::~HostColl() {
+    if (dbuf) (void)hipFree(dbuf);
+}
+
+char *HostColl::dev(uint64_t bytes) {
+    if (bytes > dcap) {
         if (dbuf) (void)hipFree(dbuf);
+        dbuf = nullptr;
+        dcap = std::max<uint64_t>(bytes, 4096);
+        RHIP(hipMalloc(&dbuf, dcap));
     }
-    char *dev(uint64_t bytes) {
-        if (bytes > dcap) {
-            if (dbuf) (void)hipFree(dbuf);
-            dbuf = nullptr;
-            dcap = std::max<uint64_t>(bytes, 4096);
-            RHIP(hipMalloc(&dbuf, dcap));
-        }
-        return (char *)dbuf;
+    return (char *)dbuf;
+}
+
+void HostColl::allgather(const void *send, void *recv, uint64_t bytes) {
+    if (!c->device) return c->allgather(send, recv, bytes, nullptr);
+    RHIP(hipSetDevice(c->dev));
+    char *d = dev(bytes * (c->world + 1));
+    RHIP(hipMemcpy(d, send, bytes, hipMemcpyHostToDevice));
+    c->allgather(d, d + bytes, bytes, nullptr);
+    c->wait(nullptr);
+    RHIP(hipMemcpy(recv, d + bytes, bytes * c->world, hipMemcpyDeviceToHost));
+}
+
+const std::vector<uint64_t> &HostColl::gather(const std::vector<uint64_t> &v) {
+    mat.assign(v.size() * c->world, 0);
+    allgather(v.data(), mat.data(), v.size() * 8);
+    return mat;
+}
+
+int HostColl::agree(int rc) {
+    gather({(uint64_t)rc});
+    int m = 0;
+    for (uint64_t x : mat) m = std::max(m, (int)x);
+    return m;
+}
+
+std::vector<char> HostColl::alltoallv(const void *send, const std::vector<uint64_t> &counts, uint64_t unit,
+                                      std::vector<uint64_t> *rcounts) {
+    const int W = c->world, me = c->rank;
+    gather(counts);
+    std::vector<uint64_t> sb(W), rb(W);
+    uint64_t ns = 0, nr = 0;
+    for (int p = 0; p < W; p++) {
+        sb[p] = counts[p] * unit;
+        rb[p] = mat[(size_t)p * W + me] * unit;
+        ns += sb[p];
+        nr += rb[p];
     }
-    void allgather(const void *send, void *recv, uint64_t bytes) {
-        if (!c->device) return c->allgather(send, recv, bytes, nullptr);
-        RHIP(hipSetDevice(c->dev));
-        char *d = dev(bytes * (c->world + 1));
-        RHIP(hipMemcpy(d, send, bytes, hipMemcpyHostToDevice));
-        c->allgather(d, d + bytes, bytes, nullptr);
-        c->wait(nullptr);
-        RHIP(hipMemcpy(recv, d + bytes, bytes * c->world, hipMemcpyDeviceToHost));
+    if (rcounts) {
+        rcounts->resize(W);
+        for (int p = 0; p < W; p++) (*rcounts)[p] = rb[p] / unit;
     }
-    // every rank's u64 list of `k` values -> mat[world][k]
-    const std::vector<uint64_t> &gather(const std::vector<uint64_t> &v) {
-        mat.assign(v.size() * c->world, 0);
-        allgather(v.data(), mat.data(), v.size() * 8);
-        return mat;
-    }
-    // status agreement: the largest code of any rank (0 when every rank succeeded)
-    int agree(int rc) {
-        gather({(uint64_t)rc});
-        int m = 0;
-        for (uint64_t x : mat) m = std::max(m, (int)x);
-        return m;
-    }
-    // variable all-to-all of `unit`-byte items: counts[world] items per destination
-    std::vector<char> alltoallv(const void *send, const std::vector<uint64_t> &counts, uint64_t unit,
-                                std::vector<uint64_t> *rcounts) {
-        const int W = c->world, me = c->rank;
-        gather(counts);
-        std::vector<uint64_t> sb(W), rb(W);
-        uint64_t ns = 0, nr = 0;
-        for (int p = 0; p < W; p++) {
-            sb[p] = counts[p] * unit;
-            rb[p] = mat[(size_t)p * W + me] * unit;
-            ns += sb[p];
-            nr += rb[p];
-        }
-        if (rcounts) {
-            rcounts->resize(W);
-            for (int p = 0; p < W; p++) (*rcounts)[p] = rb[p] / unit;
-        }
-        std::vector<char> out(nr);
-        if (!c->device) {
-            c->alltoallv(send, sb.data(), out.data(), rb.data(), nullptr);
-            return out;
-        }
-        RHIP(hipSetDevice(c->dev));
-        char *d = dev(ns + nr);
-        if (ns) RHIP(hipMemcpy(d, send, ns, hipMemcpyHostToDevice));
-        c->alltoallv(d, sb.data(), d + ns, rb.data(), nullptr);
-        c->wait(nullptr);
-        if (nr) RHIP(hipMemcpy(out.data(), d + ns, nr, hipMemcpyDeviceToHost));
+    std::vector<char> out(nr);
+    if (!c->device) {
+        c->alltoallv(send, sb.data(), out.data(), rb.data(), nullptr);
         return out;
     }
-};
-}  // namespace
+    RHIP(hipSetDevice(c->dev));
+    char *d = dev(ns + nr);
+    if (ns) RHIP(hipMemcpy(d, send, ns, hipMemcpyHostToDevice));
+    c->alltoallv(d, sb.data(), d + ns, rb.data(), nullptr);
+    c->wait(nullptr);
+    if (nr) RHIP(hipMemcpy(out.data(), d + ns, nr, hipMemcpyDeviceToHost));
+    return out;
+}
+
+std::vector<char> HostColl::allgatherv(const void *send, uint64_t bytes, std::vector<uint64_t> *sizes) {
+    const int W = c->world;
+    std::vector<uint64_t> counts(W, bytes);
+    std::vector<uint64_t> rc;
+    // the same bytes to every rank: an all-to-all whose every send part is the whole buffer
+    std::vector<char> rep((size_t)bytes * W);
+    for (int p = 0; p < W; p++)
+        if (bytes) memcpy(rep.data() + (size_t)p * bytes, send, bytes);
+    std::vector<char> out = alltoallv(rep.data(), counts, 1, &rc);
+    if (sizes) *sizes = rc;
+    return out;
+}
+}  // namespace ketogpu
 
 extern "C" {
 

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "ketogpu_internal.hpp"
 
@@ -63,6 +64,29 @@ struct Steps {
     // records must really be written into `send` even at world 1 (an exchange reads them)
     virtual void set_exchange(bool) {}
     virtual std::string error() = 0;
+};
+
+// Collectives on host arrays over any communicator (RCCL: staged through device memory
+// of the communicator's GPU); load-time exchanges, not the per-batch path.
+struct HostColl {
+    Comm *c;
+    std::vector<uint64_t> mat;
+    void *dbuf = nullptr;
+    uint64_t dcap = 0;
+    explicit HostColl(Comm *cc) : c(cc) {}
+    HostColl(const HostColl &) = delete;
+    ~HostColl();
+    char *dev(uint64_t bytes);
+    void allgather(const void *send, void *recv, uint64_t bytes);
+    // every rank's u64 list of the same length -> mat[world][k]
+    const std::vector<uint64_t> &gather(const std::vector<uint64_t> &v);
+    // status agreement: the largest code of any rank (0 when every rank succeeded)
+    int agree(int rc);
+    // variable all-to-all of `unit`-byte items: counts[world] items per destination
+    std::vector<char> alltoallv(const void *send, const std::vector<uint64_t> &counts, uint64_t unit,
+                                std::vector<uint64_t> *rcounts);
+    // every rank's `bytes` bytes (any length per rank) -> their concatenation in rank order
+    std::vector<char> allgatherv(const void *send, uint64_t bytes, std::vector<uint64_t> *sizes);
 };
 
 // partition.hip: the HIP steps of a ketogpu_part

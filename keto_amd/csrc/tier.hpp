@@ -1,0 +1,89 @@
+// tier.hpp — the two-tier partitioned mode (internal; include/ketogpu.h "two-tier").
+//
+// A hash-partitioned network (shard.cpp) whose CORE — the rows among interior nodes:
+// fint(v) and the interior predecessors of every interior node v — is small enough to be
+// copied to every rank, while the bulk of the rows (a document's grants, a user's
+// memberships: every row that starts or ends outside the interior) stays with its owner.
+// Every path r -> v1 -> ... -> v(k-1) -> t has v1 in fint(r), v(k-1) in rev(t) and
+// everything between in the core, so a check needs exactly two rows from the owners —
+// fint(r) from owner(r), rev(t) from owner(t) — and then runs the bidirectional LDS unit
+// (device_engine.hip lite_unit) on the local copy of the core, with no exchange per level.
+// The kernels live in device_engine.hip (they share lite_unit); the host state and the
+// exchange protocol in tier.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "ketogpu_internal.hpp"
+
+namespace ketogpu {
+
+// device_engine.hip: `device`'s view of host memory it can read in place (pinned), else
+// nullptr
+const void *host_view(const void *p, int device, bool query);
+
+namespace tier {
+
+// a 16-byte edge record (device_engine.hip FRec): the entry's node, the entry's own core
+// row (forward: |fint(node)| and its first record; backward: |interior predecessors of
+// node| and its first record; 0/0 for a backward entry outside the interior), pad (in
+// transit: the request tag)
+struct Rec {
+    uint32_t node, deg, begin, pad;
+};
+// a query in transit: tag = request index << 1 | direction (0: fint(r), 1: rev(t))
+struct Query {
+    uint32_t tag, node;
+};
+
+// device view of one rank's graph
+struct Graph {
+    uint32_t world, rank, Ni, Nx, N;  // global layout (shard.cpp)
+    uint32_t Nil, Nxl, Nl;            // owned class bounds
+    const Rec *core_f, *core_b;       // core rows of every interior node (replicated)
+    const uint64_t *lf_off, *lr_off;  // owned seed rows: fint of owned expandable, rev of owned nodes
+    const Rec *lf_rec, *lr_rec;
+    int64_t lf_base, lr_base;         // lf_rec - core_f and lr_rec - core_b in records
+    uint32_t both_max, seed_max;
+};
+
+// evaluation stages: 0 = one 16-request unit per workgroup over every unit of the batch,
+// 1 / 2 = persistent cascades over the previous stage's spilled units (larger tables)
+constexpr int kStages = 3;
+// bnd: per request {fb, fe, rb, re} into recv (exchange mode), or nullptr: the rank owns
+// every root and target and reads the seed rows in place (world 1)
+struct Eval {
+    const uint32_t *roots, *targets;  // device-readable (HBM or a pinned host view)
+    uint64_t n;
+    const uint4 *bnd;
+    const Rec *recv;
+    int64_t recv_base_f, recv_base_b;  // recv - core_f, recv - core_b in records
+    uint64_t *allowed;                 // ceil(n/64) words, cleared by the caller
+    unsigned long long *stats;         // [0] rows opened, [1] records read
+    unsigned long long *first_bad;     // lowest invalid request index (~0: none)
+};
+void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_list, const unsigned *in_count,
+                 uint32_t *out_list, unsigned *out_count, unsigned grid, hipStream_t s);
+int stage_units_per_cu(int stage);
+
+// queries of the batch grouped by owner: count (per destination) then scatter at cursors
+void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                        unsigned long long *counts, unsigned long long *first_bad, hipStream_t s);
+void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                          unsigned long long *cursor, Query *out, hipStream_t s);
+// replies: the rows the received queries ask for, in query order (so grouped like the
+// queries' sources); `lens` scratch of n + 1 entries, *total the number of records
+// (device word), written with pad = the query's tag
+void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *lens, unsigned long long *bad,
+                          hipStream_t s);
+void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s);  // exclusive, in place, v[n] = total
+void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Rec *out, uint64_t cap,
+                       hipStream_t s);
+// received replies -> per request seed bounds (bnd cleared by the caller)
+void launch_bounds(const Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq, hipStream_t s);
+
+}  // namespace tier
+}  // namespace ketogpu

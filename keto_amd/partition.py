@@ -433,3 +433,95 @@ class PartitionedEngine:
 
     def __del__(self):
         self.close()
+
+
+class Core:
+    """The core of a partitioned network on every rank (ketogpu_core_gather, collective):
+    the rows among interior nodes — interior successors and interior predecessors of every
+    interior node — gathered from their owners.  Raises KETOGPU_ENOMEM on every rank alike
+    when it passes `budget` bytes of device records (then use PartitionedEngine)."""
+
+    def __init__(self, shard, comm=None, budget=0):
+        self.L = L.lib()
+        self.shard = shard
+        comm = comm if comm is not None else shard.native_comm()
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_core_gather(shard.h, comm.handle, int(budget), C.byref(h)))
+        self.h = h
+
+    def view(self):
+        v = L.CoreView()
+        L.check(self.L.ketogpu_core_get_view(self.h, C.byref(v)))
+        n = v.num_interior
+
+        def arr(p, k, dt):
+            return np.ctypeslib.as_array(p, (k,)).copy() if k else np.zeros(0, dtype=dt)
+        f_off = arr(v.f_off, n + 1, np.uint64)
+        b_off = arr(v.b_off, n + 1, np.uint64)
+        return {"num_interior": n, "bytes": v.bytes, "f_off": f_off, "f_col": arr(v.f_col, int(f_off[-1]), np.uint32),
+                "b_off": b_off, "b_col": arr(v.b_col, int(b_off[-1]), np.uint32)}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ketogpu_core_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class TieredEngine:
+    """check_ids over the partitioned graph in TWO exchanges per batch (ketogpu_tier_*,
+    include/ketogpu.h "two-tier"): every rank holds the core (Core) and its own rows; a
+    request's two seed rows travel from their owners, then the single-GPU engine's
+    bidirectional LDS unit runs over the local core.  Unlike PartitionedEngine, each rank
+    passes ITS OWN requests and gets their answers (the call is still collective: every
+    rank calls check_ids once per batch, with 0 requests if it has none).  `local` (tests
+    only): an object whose vtable() gives host steps (tests/tier_cpu.py)."""
+
+    def __init__(self, shard, device=0, local=None, core=None, comm=None, max_batch=0, core_budget=0,
+                 fallback_state_bytes=0):
+        self.L = L.lib()
+        self.shard = shard
+        if comm is None:
+            comm = shard.native_comm(device, host_steps=local is not None)
+        self.ncomm = comm
+        opts = L.TierOpts(device, int(max_batch), int(fallback_state_bytes))
+        h = C.c_void_p()
+        if local is None:
+            self.core = core if core is not None else Core(shard, comm, core_budget)
+            L.check(self.L.ketogpu_tier_new(shard.h, self.core.h, comm.handle, C.byref(opts), C.byref(h)))
+            self.local = None
+        else:
+            self.core = core
+            self.local = local
+            self._vt = local.vtable()
+            L.check(self.L.ketogpu_tier_new_steps(C.byref(self._vt), comm.handle, C.byref(opts), C.byref(h)))
+        self.h = h
+
+    def stats(self):
+        st = L.TierStats()
+        L.check(self.L.ketogpu_tier_stats_get(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def check_ids(self, roots, targets):
+        """this rank's (roots, targets) -> bool answers"""
+        roots = np.ascontiguousarray(roots, dtype=np.uint32)
+        targets = np.ascontiguousarray(targets, dtype=np.uint32)
+        n = len(roots)
+        bits = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        L.check(self.L.ketogpu_tier_check_ids(self.h, roots.ctypes.data, targets.ctypes.data, n, bits.ctypes.data))
+        return np.unpackbits(bits.view(np.uint8), bitorder="little")[:n].astype(bool)
+
+    def check_ids_raw(self, roots, targets, bits):
+        """the batch call on caller arrays (pinned buffers are read in place at world 1)"""
+        L.check(self.L.ketogpu_tier_check_ids(self.h, roots.ctypes.data, targets.ctypes.data, len(roots),
+                                              bits.ctypes.data))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ketogpu_tier_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
