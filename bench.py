@@ -50,6 +50,9 @@ def parse():
                         "partitioned: hash-partitioned graph, per-level all-to-all (config #5 path)")
     p.add_argument("--scale", type=float, default=0.02,
                    help="partitioned: config #5 size as a fraction of its 5B tuples (1.0 = full)")
+    p.add_argument("--part-engine", choices=["tier", "level"], default="tier",
+                   help="partitioned: tier = two exchanges per batch over the replicated core (ketogpu_tier_*); "
+                        "level = the per-level frontier exchange (ketogpu_part_*)")
     return p.parse_args()
 
 
@@ -304,11 +307,14 @@ def max_rss_gb():
 def main_partitioned(a, rank, world, local):
     """Config #5's path (BASELINE.json configs[4]): the RBAC shape at `--scale` x 5B tuples,
     generated as a stream (synth.config5) that every rank reads in ORDER BY order while
-    the partition-aware loader keeps only what the rank owns (keto_amd/partition.py Shard);
-    then per-level all_to_all over RCCL.  Every rank holds the same global batch of
-    1M x world requests (weak scaling); value = that batch / the slowest rank's time."""
+    the partition-aware loader keeps only what the rank owns (keto_amd/partition.py Shard).
+    --part-engine tier (default): the core (rows among interior nodes) gathered on every
+    rank, then each rank checks ITS OWN 1M requests per step with two exchanges (seed-row
+    queries and replies); level: the per-level frontier exchange over the whole batch of
+    1M x world requests on every rank.  Weak scaling either way; value = the requests of
+    all ranks / the slowest rank's time."""
     from keto_amd import synth
-    from keto_amd.partition import PartitionedEngine, Shard
+    from keto_amd.partition import Core, PartitionedEngine, Shard, TieredEngine
     f = a.scale
     sizes = dict(users=max(1000, int(500_000_000 * f)), groups=max(100, int(10_000_000 * f)),
                  docs=max(100, int(200_000_000 * f)), tuples=max(10_000, int(5_000_000_000 * f)))
@@ -324,30 +330,65 @@ def main_partitioned(a, rank, world, local):
     log(f"shard loaded in {t_load:.1f}s: {sst['rows']} rows streamed, {sst['owned_nodes']} nodes owned, "
         f"host arrays {sst['host_bytes'] / 1e9:.2f} GB, peak RSS {rss_load:.2f} GB")
     roots, targets, status = sh.resolve_batch(w.request_batch())
-    # requests in pinned host memory, as for the replicated line (ketogpu_part_begin copies
-    # them to HBM by DMA)
     from keto_amd import check
-    pinned = (check.pinned(roots), check.pinned(targets))
-    roots, targets = pinned[0].array, pinned[1].array
-    eng = PartitionedEngine(sh, device=local, record_capacity=1 << 26)
-    for _ in range(max(a.warmup, 1)):  # the first call also picks the direction (auto)
-        got = eng.check_ids(roots, targets)
+    tier = a.part_engine == "tier"
+    core_info = None
+    if tier:
+        t0 = time.time()
+        core = Core(sh)
+        cv = core.view()
+        core_info = {"seconds": round(time.time() - t0, 2), "interior_nodes": int(cv["num_interior"]),
+                     "forward_entries": int(len(cv["f_col"])), "backward_entries": int(len(cv["b_col"])),
+                     "device_bytes": int(cv["bytes"]), "share_of_rows": round((len(cv["f_col"]) + len(cv["b_col"])) /
+                                                                              max(sst["rows"], 1), 5)}
+        del cv
+        log(f"core gathered: {core_info}")
+        eng = TieredEngine(sh, device=local, core=core)
+        mine = slice(rank * per_gpu, (rank + 1) * per_gpu)  # this rank's own requests
+        pinned = (check.pinned(roots[mine]), check.pinned(targets[mine]))
+        bits = np.zeros((per_gpu + 63) // 64, dtype=np.uint64)
+
+        def step():
+            eng.check_ids_raw(pinned[0].array, pinned[1].array, bits)
+    else:
+        # requests in pinned host memory, as for the replicated line (ketogpu_part_begin
+        # copies them to HBM by DMA); every rank passes the whole batch
+        pinned = (check.pinned(roots), check.pinned(targets))
+        eng = PartitionedEngine(sh, device=local, record_capacity=1 << 26)
+
+        def step():
+            return eng.check_ids(pinned[0].array, pinned[1].array)
+    for _ in range(max(a.warmup, 1)):  # the level engine's first call also picks the direction
+        step()
+    st0 = eng.stats() if tier else None
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        got = eng.check_ids(roots, targets)
+        step()
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    # measurement pass: the same step with every kernel launch bracketed by hipEvents
-    before = eng.local.stats()["kernels"]
-    eng.local.set_timing(True)
-    t0 = time.perf_counter()
-    eng.check_ids(roots, targets)
-    t_timed = time.perf_counter() - t0
-    eng.local.set_timing(False)
-    after = eng.local.stats()
-    fam = {k: {kk: after["kernels"][k][kk] - before[k][kk] for kk in ("bytes", "ms", "launches")}
-           for k in after["kernels"]}
+    if tier:
+        got = np.unpackbits(bits.view(np.uint8), bitorder="little")[:per_gpu].astype(bool)
+        st1 = eng.stats()
+        d = {k: st1[k] - st0[k] for k in ("rows_opened", "records_read", "eval_kernel_ms", "eval_kernel_launches")}
+        launches = max(d["eval_kernel_launches"], 1)
+        bytes_launch = (16 * d["rows_opened"] + 16 * d["records_read"]) / launches + 8 * per_gpu + per_gpu / 8
+        ms_launch = d["eval_kernel_ms"] / launches
+        achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
+        fam = None
+        t_timed = None
+    else:
+        got = step()
+        # measurement pass: the same step with every kernel launch bracketed by hipEvents
+        before = eng.local.stats()["kernels"]
+        eng.local.set_timing(True)
+        t1 = time.perf_counter()
+        step()
+        t_timed = time.perf_counter() - t1
+        eng.local.set_timing(False)
+        after = eng.local.stats()
+        fam = {k: {kk: after["kernels"][k][kk] - before[k][kk] for kk in ("bytes", "ms", "launches")}
+               for k in after["kernels"]}
     rss = [max_rss_gb()]
     if world > 1:
         import torch.distributed as dist
@@ -360,32 +401,42 @@ def main_partitioned(a, rank, world, local):
         per_rank = [[rss[0], rss_load, float(sst["host_bytes"])]]
     out = None
     if rank == 0:
-        dominant = max(fam, key=lambda k: fam[k]["ms"])
-        d = fam[dominant]
-        achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                "traffic_source": "no PMC summary for this workload", "kernel": dominant,
-                "bytes_per_launch": int(d["bytes"] / max(d["launches"], 1)),
-                "ms_per_launch": round(d["ms"] / max(d["launches"], 1), 4),
-                "measured": "one extra step with hipEvents around every launch (ketogpu_part_set_timing)",
-                "kernels": {k: {"GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
-                                "ms": round(v["ms"], 4), "bytes": v["bytes"], "launches": v["launches"]}
-                            for k, v in fam.items() if v["launches"]}}
+        if tier:
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "traffic_source": "no PMC summary for this workload", "kernel": "tier_eval_kernel",
+                    "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
+                    "measured": "hipEvents around the first evaluation stage on the engine's stream, every timed step",
+                    "bytes_formula": "16*rows_opened + 16*records_read + 8*requests + requests/8 (as the replicated "
+                                     "line's lite kernel)"}
+        else:
+            dominant = max(fam, key=lambda k: fam[k]["ms"])
+            d = fam[dominant]
+            achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "traffic_source": "no PMC summary for this workload", "kernel": dominant,
+                    "bytes_per_launch": int(d["bytes"] / max(d["launches"], 1)),
+                    "ms_per_launch": round(d["ms"] / max(d["launches"], 1), 4),
+                    "measured": "one extra step with hipEvents around every launch (ketogpu_part_set_timing)",
+                    "kernels": {k: {"GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
+                                    "ms": round(v["ms"], 4), "bytes": v["bytes"], "launches": v["launches"]}
+                                for k, v in fam.items() if v["launches"]}}
         cpu, parity = None, None
         if not a.no_cpu_baseline:
             cpu, parity = cpu_baseline_stream(w, got, a.cpu_seconds, world)
-        pos = np.asarray(w.chk_pos, dtype=bool)
+        pos = np.asarray(w.chk_pos, dtype=bool)[:len(got)]
         parity = dict(parity or {}, constructed_positives=int(pos.sum()),
                       constructed_positives_denied=int((pos & ~got.astype(bool)).sum()))
-        st = eng.local.stats()
         out = {"metric": METRIC, "value": round(n_req * a.steps / dt, 1), "unit": "checks/s", "n_gpus": world,
                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "u32 ids / u64 bitmasks (integer)",
                "data": "synthetic: config #5 RBAC-shape stream generator (keto_amd/csrc/synth.cpp ks_c5), seed 0x4B45544F",
                "config": {"workload": f"config5_partitioned_x{f:g}", **sizes, "checks": n_req,
-                          "mode": "hash-partitioned graph (partition-aware loader), native per-level exchange",
+                          "mode": ("hash-partitioned graph (partition-aware loader), two-tier: core on every rank, "
+                                   "seed rows exchanged, each rank its own requests") if tier else
+                                  "hash-partitioned graph (partition-aware loader), native per-level exchange",
                           "parallelism": f"partition x{world}"},
                "roofline": roof, "cpu_baseline": cpu, "parity": parity,
                "load": {"seconds": round(t_load, 1), "rows": sst["rows"], "rows_per_s": round(sst["rows"] / t_load, 1),
@@ -393,14 +444,22 @@ def main_partitioned(a, rank, world, local):
                         "per_rank_peak_rss_gb": [round(r[0], 2) for r in per_rank],
                         "per_rank_rss_after_load_gb": [round(r[1], 2) for r in per_rank],
                         "per_rank_loader_array_gb": [round(r[2] / 1e9, 3) for r in per_rank],
-                        "shard": sst},
-               "partition": {k: v for k, v in st.items() if k != "kernels"},
-               "direction": {0: "forward", 1: "backward"}.get(eng.direction, "undecided"),
-               "direction_trials_ns_per_check": {{0: "forward", 1: "backward"}[k]: v for k, v in eng._trial.items()},
-               "exchange": dict(eng.stats(), driver="native: ketogpu_part_check_ids (part_round.cpp), "
-                                "RCCL grouped send/recv + all-gather" if world > 1 else
-                                "native: ketogpu_part_check_ids (part_round.cpp), world 1: no exchange"),
-               "timed_pass_s": round(t_timed, 4)}
+                        "shard": sst}}
+        if tier:
+            out.update({"engine": "two-tier (ketogpu_tier_check_ids, keto_amd/csrc/tier.cpp)", "core": core_info,
+                        "tier": dict(eng.stats(), exchange="RCCL grouped send/recv + all-gather" if world > 1 else
+                                     "world 1: rows read in place, no exchange")})
+        else:
+            st = eng.local.stats()
+            out.update({"engine": "per-level (ketogpu_part_check_ids, keto_amd/csrc/part_round.cpp)",
+                        "partition": {k: v for k, v in st.items() if k != "kernels"},
+                        "direction": {0: "forward", 1: "backward"}.get(eng.direction, "undecided"),
+                        "direction_trials_ns_per_check": {{0: "forward", 1: "backward"}[k]: v
+                                                          for k, v in eng._trial.items()},
+                        "exchange": dict(eng.stats(), driver="native: ketogpu_part_check_ids (part_round.cpp), "
+                                         "RCCL grouped send/recv + all-gather" if world > 1 else
+                                         "native: ketogpu_part_check_ids (part_round.cpp), world 1: no exchange"),
+                        "timed_pass_s": round(t_timed, 4)})
         print(json.dumps(out), flush=True)
     barrier(world)
     if world > 1:

@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 6 /* 6: partitioned rounds behind the C ABI (comm, part_engine);
+#define KETOGPU_ABI_VERSION 7 /* 7: two-tier partitioned mode (ketogpu_core_*, ketogpu_tier_*);
+                                 6: partitioned rounds behind the C ABI (comm, part_engine);
                                  5: writable snapshots (in-place writes, engine sync);
                                  4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
 
@@ -716,6 +717,8 @@ typedef struct {
     uint64_t rows_opened, records_read; /* device statistics of the evaluation      */
     double exchange_ms, evaluate_ms;    /* host wall time inside collectives / evaluation */
     uint64_t core_records, seed_records; /* device records: core (both directions), own rows */
+    double eval_kernel_ms;               /* hipEvent time of the first evaluation stage      */
+    uint64_t eval_kernel_launches;
 } ketogpu_tier_stats;
 /* the shard and core stay owned by the caller; the tier borrows s, core and comm */
 int ketogpu_tier_new(const ketogpu_shard *s, const ketogpu_core *core, ketogpu_comm *comm,

@@ -254,6 +254,10 @@ struct TierDevice : TierSteps {
     uint64_t cur_n = 0;
     const tier::Query *rq = nullptr;
     uint64_t rq_n = 0;
+    // the first evaluation stage bracketed by events (the roofline's kernel time)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double eval_ms = 0;
+    uint64_t eval_launches = 0;
 
     static constexpr size_t kCounts = 0, kCursor = 64, kFirstBad = 128, kBadQuery = 129, kLists = 130, kStats = 136;
     static constexpr size_t kSmall = kStats + kEvalStatsLen;
@@ -265,6 +269,8 @@ struct TierDevice : TierSteps {
         }
         for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) b->release();
         for (void *p : owned) (void)hipFree(p);
+        for (hipEvent_t e : {ev0, ev1})
+            if (e) (void)hipEventDestroy(e);
         if (d_small) (void)hipFree(d_small);
         if (h_small) (void)hipHostFree(h_small);
         if (stream) (void)hipStreamDestroy(stream);
@@ -322,6 +328,8 @@ struct TierDevice : TierSteps {
         dev = device;
         THIP(hipSetDevice(dev));
         THIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        THIP(hipEventCreate(&ev0));
+        THIP(hipEventCreate(&ev1));
         THIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
         for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) {
             b->device = true;
@@ -468,13 +476,21 @@ struct TierDevice : TierSteps {
                 E.recv_base_b = (int64_t)((intptr_t)recv - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
             }
             unsigned *lc = (unsigned *)(d_small + kLists);  // three u32 list counts (+ padding)
+            THIP(hipEventRecord(ev0, stream));
             tier::launch_eval(0, G, E, nullptr, nullptr, lists[0], lc + 0, 0, stream);
+            THIP(hipEventRecord(ev1, stream));
             for (int s = 1; s < tier::kStages; s++)
                 tier::launch_eval(s, G, E, lists[s - 1], lc + (s - 1), lists[s], lc + s,
                                   (unsigned)(n_cu * tier::stage_units_per_cu(s)), stream);
             if (words) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
             THIP(hipMemcpyAsync(h_small + kFirstBad, d_small + kFirstBad, 8 * 4, hipMemcpyDeviceToHost, stream));
             THIP(hipStreamSynchronize(stream));
+            if (n) {
+                float ms = 0;
+                THIP(hipEventElapsedTime(&ms, ev0, ev1));
+                eval_ms += ms;
+                eval_launches++;
+            }
             if (h_small[kFirstBad] != ~0ull)
                 throw Error(KETOGPU_EINVAL, "request " + std::to_string(h_small[kFirstBad]) +
                                                 " has an id outside the partitioned layout");
@@ -503,6 +519,8 @@ struct TierDevice : TierSteps {
         st.records_read = edges;
         st.core_records = core_records;
         st.seed_records = seed_records;
+        st.eval_kernel_ms = eval_ms;
+        st.eval_kernel_launches = eval_launches;
     }
 
     std::string error() override { return err; }
