@@ -713,12 +713,51 @@ constexpr int kFront = KETO_U2_FRONT;
 constexpr int kRevCache = 16;
 constexpr int kHubList = 128;  // hubs a unit may reach (spill beyond)
 
+// Table shape per unit size: 16- and 4-request units keep 2^kHashLog slots and kFront
+// frontier entries; the single-request stage (the last before the multi-word global path)
+// takes most of a CU's LDS — 2^14 slots, 512 entries per level, ~142 KB, one workgroup per
+// CU — so a closure of up to 12k non-hub nodes stays in LDS (round 3: with 2048 slots, 304
+// of 10^6 config #4-shape requests at 200M tuples went on to the host-driven global path,
+// ~0.8 ms of a 1.6 ms step).
+#ifndef KETO_U2_HLOG1
+#define KETO_U2_HLOG1 14
+#endif
+#ifndef KETO_U2_FRONT1
+#define KETO_U2_FRONT1 512
+#endif
+template <int U>
+struct Unit2Shape {
+    static constexpr int HLOG = U == 1 ? KETO_U2_HLOG1 : kHashLog;
+    static constexpr int H = 1 << HLOG;
+    static constexpr int HMAX = H * 3 / 4;
+    static constexpr int FRONT = U == 1 ? KETO_U2_FRONT1 : kFront;
+    static_assert(H <= 65535, "slots are kept in 16 bits (0xFFFF marks a hub root)");
+};
+
+template <int HLOG>
+__device__ __forceinline__ uint32_t hslot_l(uint32_t u) {
+    return (u * 2654435761u) >> (32 - HLOG);
+}
+
+template <int HLOG>
+__device__ __forceinline__ int key_lookup_l(const uint32_t *key, uint32_t v) {
+    constexpr int H = 1 << HLOG;
+    uint32_t h = hslot_l<HLOG>(v);
+    for (int p = 0; p < H; p++, h = (h + 1) & (H - 1)) {
+        uint32_t kv = key[h];
+        if (kv == v) return (int)h;
+        if (kv == kEmpty) return -1;
+    }
+    return -1;
+}
+
 template <int U>
 struct Unit2Shared {
-    uint32_t key[kHash];
-    uint32_t st[kHash];  // visited bits (low 16) | pending bits (high 16)
-    uint16_t cur_slot[kFront], cur_mask[kFront], nxt_slot[kFront];
-    uint32_t cur_begin[kFront], cur_deg[kFront], nxt_begin[kFront], nxt_deg[kFront];
+    using Shape = Unit2Shape<U>;
+    uint32_t key[Shape::H];
+    uint32_t st[Shape::H];  // visited bits (low 16) | pending bits (high 16)
+    uint16_t cur_slot[Shape::FRONT], cur_mask[Shape::FRONT], nxt_slot[Shape::FRONT];
+    uint32_t cur_begin[Shape::FRONT], cur_deg[Shape::FRONT], nxt_begin[Shape::FRONT], nxt_deg[Shape::FRONT];
     uint32_t c_pre[kChunk + 1];
     uint32_t wave_sum[kBlock / 64];
     uint32_t root[U], target[U], rev_n[U];
@@ -763,8 +802,9 @@ __device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S,
     int h = -1;
     bool inserted = false;
     if (want) {
-        uint32_t hh = hslot(u);
-        for (int p = 0; p < kHash; p++, hh = (hh + 1) & (kHash - 1)) {
+        using Shape = Unit2Shape<U>;
+        uint32_t hh = hslot_l<Shape::HLOG>(u);
+        for (int p = 0; p < Shape::H; p++, hh = (hh + 1) & (Shape::H - 1)) {
             uint32_t kv = S.key[hh];
             if (kv == kEmpty) {
                 uint32_t prev = atomicCAS(&S.key[hh], kEmpty, u);
@@ -786,7 +826,7 @@ __device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S,
     uint64_t bal = __ballot(inserted);
     if (bal && lane == __ffsll((unsigned long long)bal) - 1) {
         uint32_t c = (uint32_t)__popcll(bal);
-        if (atomicAdd(&S.n_used, c) + c > (uint32_t)kHashMax) S.spill = 1;
+        if (atomicAdd(&S.n_used, c) + c > (uint32_t)Unit2Shape<U>::HMAX) S.spill = 1;
     }
     bool app = false;
     // a hub is visited but not expanded: the pull reads its closure from hub_mask
@@ -820,7 +860,7 @@ __device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S,
         base = __shfl(base, leader, 64);
         if (app) {
             uint32_t idx = base + lanes_below(ab);
-            if (idx < (uint32_t)kFront) {
+            if (idx < (uint32_t)Unit2Shape<U>::FRONT) {
                 S.nxt_slot[idx] = (uint16_t)h;
                 S.nxt_begin[idx] = rc.begin;
                 S.nxt_deg[idx] = rc.deg;
@@ -880,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
     uint64_t *flag_word = &flags[c0 >> 6];
     const int shift = (int)(c0 & 63);
     const unsigned long long unit_bits = ((1ull << U) - 1) << shift;
-    for (int i = tid; i < kHash; i += kBlock) {
+    for (int i = tid; i < Unit2Shape<U>::H; i += kBlock) {
         S.key[i] = kEmpty;
         S.st[i] = 0;
     }
@@ -985,7 +1025,7 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
                 if (v == r) {
                     ok = true;
                 } else if (v < g.Ni) {
-                    int s = key_lookup(S.key, v);
+                    int s = key_lookup_l<Unit2Shape<U>::HLOG>(S.key, v);
                     ok = s >= 0 && ((S.st[s] >> rj) & 1u);
                     // v in the closure of a hub this request reached
                     for (uint32_t j = 0, nh = S.n_hub; j < nh && !ok; j++) {
@@ -3514,6 +3554,7 @@ struct ketogpu_engine {
         for (hipStream_t x : {stream, stream2, copy_stream})
             if (x) (void)hipStreamSynchronize(x);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
+        if (wait_ev) (void)hipEventDestroy(wait_ev);
         for (void *p : owned) (void)hipFree(p);
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags})
@@ -3881,7 +3922,7 @@ struct ketogpu_engine {
                 12, E);
         if (before_sync) before_sync();
         if (!b) HIP_CHECK(hipEventRecord(d, stream));
-        HIP_CHECK(hipStreamSynchronize(stream));
+        wait_stream();
         unit_end = d;
         if (b) {
             unit_ev.push_back({a, b});
@@ -3911,6 +3952,28 @@ struct ketogpu_engine {
     // The LDS cascade: 16-request units, then 4-request and 1-request units for what
     // spilled.  Returns the number of single requests left in spill_units[0..) for the
     // global path.
+    // The end of a run.  KETOGPU_WAIT=spin: poll an event recorded after the last launch
+    // (the host thread busy-waits, no wake-up latency); default: hipStreamSynchronize.
+    hipEvent_t wait_ev = nullptr;
+    void wait_stream() {
+        static const bool spin = [] {
+            const char *w = getenv("KETOGPU_WAIT");
+            return w && !strcmp(w, "spin");
+        }();
+        if (!spin) {
+            HIP_CHECK(hipStreamSynchronize(stream));
+            return;
+        }
+        if (!wait_ev) HIP_CHECK(hipEventCreateWithFlags(&wait_ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(wait_ev, stream));
+        for (;;) {
+            const hipError_t e = hipEventQuery(wait_ev);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) HIP_CHECK(e);
+            __builtin_ia32_pause();
+        }
+    }
+
     uint64_t run_units(const Batch &q, ketogpu_run_stats &rs, std::vector<std::pair<hipEvent_t, hipEvent_t>> &unit_ev,
                        const HostSrc *src = nullptr, const std::function<void()> &before_sync = {}) {
         ensure_spill(q.n);

@@ -197,14 +197,15 @@ def test_unit_spill_to_global_path():
 
 
 def test_large_forward_closure_small_backward_side():
-    # a 6000-group forward closure with a 1-entry backward side: bidi expands the backward
-    # side and looks the root's row up, so nothing spills; the forward-only plan spills
-    rows = [(1, "top", "m", None, 1, f"g{i:05d}", "m") for i in range(6000)]
-    rows += [(1, f"g{i:05d}", "m", f"u{i}", None, None, None) for i in range(6000)]
+    # a 14000-group forward closure with a 1-entry backward side: bidi expands the backward
+    # side and looks the root's row up, so nothing spills; the forward-only plan spills past
+    # even the single-request stage's 12288-node table to the global path
+    rows = [(1, "top", "m", None, 1, f"g{i:05d}", "m") for i in range(14000)]
+    rows += [(1, f"g{i:05d}", "m", f"u{i}", None, None, None) for i in range(14000)]
     rows += [(1, "small", "m", None, 1, "g00007", "m")]
     snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
     reqs, want = [], []
-    for i in range(0, 6000, 97):
+    for i in range(0, 14000, 233):
         reqs.append(rt.InternalRelationTuple("n", "top", "m", rt.SubjectID(f"u{i}")))
         reqs.append(rt.InternalRelationTuple("n", "small", "m", rt.SubjectID(f"u{i}")))
         want += [True, i == 7]
