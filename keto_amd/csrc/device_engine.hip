@@ -456,16 +456,6 @@ __device__ __forceinline__ void unit_push(const DevGraph &g, UnitShared &S, bool
     }
 }
 
-__device__ __forceinline__ int key_lookup(const uint32_t *key, uint32_t v) {
-    uint32_t h = hslot(v);
-    for (int p = 0; p < kHash; p++, h = (h + 1) & (kHash - 1)) {
-        uint32_t kv = key[h];
-        if (kv == v) return (int)h;
-        if (kv == kEmpty) return -1;
-    }
-    return -1;
-}
-
 __device__ __forceinline__ int unit_lookup(const UnitShared &S, uint32_t v) {
     uint32_t h = hslot(v);
     for (int p = 0; p < kHash; p++, h = (h + 1) & (kHash - 1)) {
@@ -725,12 +715,19 @@ constexpr int kHubList = 128;  // hubs a unit may reach (spill beyond)
 #ifndef KETO_U2_FRONT1
 #define KETO_U2_FRONT1 512
 #endif
+#ifndef KETO_U2_HUBS1
+#define KETO_U2_HUBS1 1024
+#endif
+#ifndef KETO_U2_HUBS
+#define KETO_U2_HUBS kHubList
+#endif
 template <int U>
 struct Unit2Shape {
     static constexpr int HLOG = U == 1 ? KETO_U2_HLOG1 : kHashLog;
     static constexpr int H = 1 << HLOG;
     static constexpr int HMAX = H * 3 / 4;
     static constexpr int FRONT = U == 1 ? KETO_U2_FRONT1 : kFront;
+    static constexpr int HUBS = U == 1 ? KETO_U2_HUBS1 : KETO_U2_HUBS;  // hubs a unit may reach (spill beyond)
     static_assert(H <= 65535, "slots are kept in 16 bits (0xFFFF marks a hub root)");
 };
 
@@ -765,8 +762,8 @@ struct Unit2Shared {
     uint32_t rev_c[U][kRevCache];
     // hubs reached (hub index on): hub number, table slot (its visited bits are the
     // requests that reached it) or 0xFFFF for a hub ROOT, whose requests are hub_bits
-    uint32_t hub_id[kHubList];
-    uint16_t hub_slot[kHubList], hub_bits[kHubList];
+    uint32_t hub_id[Shape::HUBS];
+    uint16_t hub_slot[Shape::HUBS], hub_bits[Shape::HUBS];
     uint32_t n_used, n_nxt, spill, res, n_hub;
     unsigned long long cnt_rows, cnt_edges, cnt_rev;
 };
@@ -833,7 +830,7 @@ __device__ __forceinline__ void unit2_push(const DevGraph &g, Unit2Shared<U> &S,
     const bool hub = g.hub_mask && rc.pad;
     if (inserted && hub) {
         uint32_t j = atomicAdd(&S.n_hub, 1u);
-        if (j < (uint32_t)kHubList) {
+        if (j < (uint32_t)Unit2Shape<U>::HUBS) {
             S.hub_id[j] = rc.pad - 1;
             S.hub_slot[j] = (uint16_t)h;
         } else {
@@ -902,20 +899,16 @@ __device__ __forceinline__ void unit2_expand(const DevGraph &g, const FRec *frec
     }
 }
 
-// Pass 1 (parents == nullptr): unit b = requests [U*b, U*b+U).  Later passes split the
-// spilled units of the previous pass (size U*fan) into `fan` units each.
+// One unit (requests [U*unit, U*unit+U)) by the whole workgroup.
 template <int U>
-__global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *frec, const uint32_t *roots,
-                                                       const uint32_t *targets, uint64_t n, uint64_t *allowed,
-                                                       uint64_t *flags, const uint32_t *parents, uint32_t fan,
-                                                       uint32_t *spill_out, unsigned int *spill_count,
-                                                       unsigned long long *stats, unsigned long long *stamps) {
-    __shared__ Unit2Shared<U> S;
+__device__ __forceinline__ void unit2_unit(Unit2Shared<U> &S, const DevGraph &g, const FRec *frec,
+                                           const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                                           uint64_t *allowed, uint64_t *flags, const uint64_t unit,
+                                           uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats,
+                                           unsigned long long *stamp) {
     const int tid = threadIdx.x;
-    unsigned long long *stamp = (stamps && blockIdx.x < 65536 && tid == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
     uint32_t n_levels = 0;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
-    const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
     const uint64_t c0 = unit * U;
     uint64_t *flag_word = &flags[c0 >> 6];
     const int shift = (int)(c0 & 63);
@@ -951,7 +944,7 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
             if (hid != KETOGPU_NODE_NONE) {  // X(r) of a hub root is its closure: nothing to expand
                 fe = fb;
                 uint32_t j = atomicAdd(&S.n_hub, 1u);
-                if (j < (uint32_t)kHubList) {
+                if (j < (uint32_t)Unit2Shape<U>::HUBS) {
                     S.hub_id[j] = hid;
                     S.hub_slot[j] = 0xFFFF;
                     S.hub_bits[j] = (uint16_t)(1u << tid);
@@ -1054,6 +1047,39 @@ __global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *f
         atomicAdd(&stat_slot(stats)[0], S.cnt_rows);
         atomicAdd(&stat_slot(stats)[1], S.cnt_edges);
         atomicAdd(&stat_slot(stats)[2], S.cnt_rev);
+    }
+}
+
+// Pass 1 (parents == nullptr): unit b = requests [U*b, U*b+U).  Later passes split the
+// spilled units of the previous pass (size U*fan) into `fan` units each.
+template <int U>
+__global__ __launch_bounds__(kBlock) void unit2_kernel(DevGraph g, const FRec *frec, const uint32_t *roots,
+                                                       const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                       uint64_t *flags, const uint32_t *parents, uint32_t fan,
+                                                       uint32_t *spill_out, unsigned int *spill_count,
+                                                       unsigned long long *stats, unsigned long long *stamps) {
+    __shared__ Unit2Shared<U> S;
+    unsigned long long *stamp =
+        (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
+    const uint64_t unit = parents ? (uint64_t)parents[blockIdx.x / fan] * fan + blockIdx.x % fan : blockIdx.x;
+    unit2_unit<U>(S, g, frec, roots, targets, n, allowed, flags, unit, spill_out, spill_count, stats, stamp);
+}
+
+// The cascade's later stages, persistent: every unit the previous stage spilled (its count
+// read on the device, so no host synchronization between stages) splits into `fan` units.
+template <int U>
+__global__ __launch_bounds__(kBlock) void unit2_cascade_kernel(DevGraph g, const FRec *frec, const uint32_t *roots,
+                                                               const uint32_t *targets, uint64_t n, uint64_t *allowed,
+                                                               uint64_t *flags, const uint32_t *parents,
+                                                               const unsigned int *in_count, uint32_t fan,
+                                                               uint32_t *spill_out, unsigned int *spill_count,
+                                                               unsigned long long *stats) {
+    __shared__ Unit2Shared<U> S;
+    const uint64_t cnt = (uint64_t)*in_count * fan;
+    for (uint64_t b = blockIdx.x; b < cnt; b += gridDim.x) {
+        const uint64_t unit = (uint64_t)parents[b / fan] * fan + b % fan;
+        unit2_unit<U>(S, g, frec, roots, targets, n, allowed, flags, unit, spill_out, spill_count, stats, nullptr);
+        __syncthreads();
     }
 }
 
@@ -3357,6 +3383,7 @@ struct ketogpu_engine {
     // grid): an empty stage of 1024 workgroups still cost ~18 us per call on config #2,
     // where one unit in 60k spills; a grid that is too small for one run only slows it.
     uint64_t stage_prev[8] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+    uint64_t u2_prev[2] = {~0ull, ~0ull};  // the unit2 cascade's last units per stage
     static unsigned stage_grid(uint64_t prev, unsigned full) {
         if (prev >= full) return full;
         unsigned g = 32;
@@ -4106,58 +4133,61 @@ struct ketogpu_engine {
                 if (b) HIP_CHECK(hipEventRecord(b, stream));
                 return bidi_tail(q, rs, unit_ev, a, b, bunits, before_sync);
             }
-            uint32_t *from = nullptr;  // spilled 16-request units entering the unit2 cascade
-            struct Stage {
-                int u;
-                uint32_t fan;
-            };
-            const Stage stages[3] = {{16, 1}, {4, 4}, {1, 4}};
-            uint32_t *in = from;
-            uint32_t *bufs[2] = {from == list[0] ? list[1] : list[0], from == list[0] ? list[0] : list[1]};
-            if (!from) bufs[0] = list[0], bufs[1] = list[1];
-            for (int si = 0; si < 3; si++) {
-                const Stage &sg = stages[si];
-                const bool first = !from && si == 0;  // unit2<16> over every unit (plan "v2")
-                uint64_t grid = first ? units : left * sg.fan;
-                if (!grid) return 0;
-                uint32_t *out = bufs[si & 1];
-                unsigned long long *stp = first ? stamps : nullptr;
-                unsigned pad = first ? lds_pad : 0;
-                HIP_CHECK(hipMemsetAsync(spill_count + 2, 0, sizeof(unsigned int), stream));
-                hipEvent_t a = ev(), b = ev();
-                HIP_CHECK(hipEventRecord(a, stream));
-                const uint32_t *par = first ? nullptr : in;
-                if (sg.u == 16)
-                    KLAUNCH(unit2_kernel<16>, dim3((unsigned)grid), dim3(kBlock), pad, stream, g, frec,
-                                       q.roots, q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
-                                       st.stats, stp);
-                else if (sg.u == 4)
-                    KLAUNCH(unit2_kernel<4>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
-                                       st.stats, nullptr);
-                else
-                    KLAUNCH(unit2_kernel<1>, dim3((unsigned)grid), dim3(kBlock), 0, stream, g, frec, q.roots,
-                                       q.targets, q.n, q.allowed, q.flags, par, sg.fan, out, spill_count + 2,
-                                       st.stats, nullptr);
-                HIP_CHECK(hipEventRecord(b, stream));
-                unit_ev.push_back({a, b});
-                HIP_CHECK(hipMemcpyAsync(h_ctr + 12, spill_count + 2, sizeof(unsigned int), hipMemcpyDeviceToHost,
-                                         stream));
-                HIP_CHECK(hipStreamSynchronize(stream));
-                left = (uint32_t)h_ctr[12];
-                rs.spilled_units += left;
-                rs.push_launches++;
-                rs.unit_launches++;
-                if (first) {  // the dominant launch: keep its own byte count
-                    uint64_t t3[3];
-                    read_unit_stats(t3);
-                    rs.main_bytes = 16 * t3[0] + 16 * t3[1] + 4 * t3[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
-                }
-                in = out;
+            // Forward-only plan "v2": unit2<16> over every unit, then the persistent
+            // unit2<4> and unit2<1> stages over the spilled units (counts read on the
+            // device: no host synchronization between the stages; grids sized by the
+            // previous call's counts, as the bidi cascade), one synchronization for the count
+            // the global path needs.  list[0] <- 16 -> list[1] <- 4 -> list[0] <- 1.
+            if (!units) return 0;
+            unsigned int *c16 = spill_count + 2, *c4 = spill_count + 3, *c1 = spill_count + 4;
+            HIP_CHECK(hipMemsetAsync(c16, 0, 3 * sizeof(unsigned int), stream));
+            hipEvent_t a = ev(), b = ev();
+            HIP_CHECK(hipEventRecord(a, stream));
+            KLAUNCH(unit2_kernel<16>, dim3((unsigned)units), dim3(kBlock), lds_pad, stream, g, frec, q.roots, q.targets,
+                    q.n, q.allowed, q.flags, nullptr, 1u, list[0], c16, st.stats, stamps);
+            HIP_CHECK(hipEventRecord(b, stream));
+            unit_ev.push_back({a, b});
+            hipEvent_t c = ev();
+            // KETOGPU_U2_SYNC=1 (A/B knob): the stages as one-unit-per-workgroup launches sized
+            // by a host read of the previous stage's count (round 2's cascade)
+            static const bool sync_stages = getenv("KETOGPU_U2_SYNC") != nullptr;
+            if (sync_stages) {
+                auto count = [&](unsigned int *cp) {
+                    HIP_CHECK(hipMemcpyAsync(h_ctr + 12, cp, sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+                    HIP_CHECK(hipStreamSynchronize(stream));
+                    return (uint64_t)*(const unsigned int *)(h_ctr + 12);
+                };
+                if (const uint64_t k = count(c16))
+                    KLAUNCH(unit2_kernel<4>, dim3((unsigned)(k * 4)), dim3(kBlock), 0, stream, g, frec, q.roots,
+                            q.targets, q.n, q.allowed, q.flags, list[0], 4u, list[1], c4, st.stats, nullptr);
+                if (const uint64_t k = count(c4))
+                    KLAUNCH(unit2_kernel<1>, dim3((unsigned)(k * 4)), dim3(kBlock), 0, stream, g, frec, q.roots,
+                            q.targets, q.n, q.allowed, q.flags, list[1], 4u, list[0], c1, st.stats, nullptr);
+            } else {
+                KLAUNCH(unit2_cascade_kernel<4>, dim3(stage_grid(u2_prev[0], 1536)), dim3(kBlock), 0, stream, g,
+                        frec, q.roots, q.targets, q.n, q.allowed, q.flags, list[0], c16, 4u, list[1], c4, st.stats);
+                KLAUNCH(unit2_cascade_kernel<1>, dim3(stage_grid(u2_prev[1], 256)), dim3(kBlock), 0, stream, g,
+                        frec, q.roots, q.targets, q.n, q.allowed, q.flags, list[1], c4, 4u, list[0], c1, st.stats);
             }
-            // the global path reads the last stage's single requests from list[0]
-            if (left && in != list[0])
-                HIP_CHECK(hipMemcpyAsync(list[0], in, left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+            HIP_CHECK(hipEventRecord(c, stream));
+            unit_ev.push_back({b, c});
+            // the counts and the cascade's statistics (rows, edges, reverse entries: the first
+            // stage dominates them) in one synchronization
+            HIP_CHECK(hipMemcpyAsync(h_ctr + 12, c16, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+            KLAUNCH(stats_reduce_kernel, dim3(1), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), nullptr, 0,
+                    EmitReq{});
+            HIP_CHECK(hipMemcpyAsync(h_ctr + 32, stat_out(), 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+            HIP_CHECK(hipStreamSynchronize(stream));
+            const unsigned int *hc = (const unsigned int *)(h_ctr + 12);
+            u2_prev[0] = (uint64_t)hc[0] * 4;
+            u2_prev[1] = (uint64_t)hc[1] * 4;
+            left = hc[2];
+            rs.spilled_units += hc[0] + hc[1] + hc[2];
+            rs.push_launches += 3;
+            rs.unit_launches += 3;
+            uint64_t t3[3];
+            for (int k = 0; k < 3; k++) t3[k] = h_ctr[32 + k] + h_ctr[35 + k];
+            rs.main_bytes = 16 * t3[0] + 16 * t3[1] + 4 * t3[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
             return left;
         }
         for (int pass = 0; pass < 3; pass++) {
