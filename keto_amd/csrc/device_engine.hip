@@ -2728,11 +2728,17 @@ __global__ __launch_bounds__(kBlock) void load_kernel(const uint32_t *hr, const 
 
 // The run's results in one launch into pinned host memory: result words, flag words (when
 // wanted) and the first invalid request index — instead of one DMA copy each.
+// out_bits (may be null): the result words go to the caller's own pinned buffer instead
 __global__ __launch_bounds__(kBlock) void emit_kernel(const uint64_t *allowed, const uint64_t *flags, uint64_t words,
-                                                      const unsigned long long *first_bad, uint64_t *out) {
+                                                      const unsigned long long *first_bad, uint64_t *out,
+                                                      uint64_t *out_bits) {
     const uint64_t nf = flags ? words : 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words + nf + 1; i += (uint64_t)gridDim.x * kBlock)
-        out[i] = i < words ? allowed[i] : i < words + nf ? flags[i - words] : (uint64_t)*first_bad;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words + nf + 1; i += (uint64_t)gridDim.x * kBlock) {
+        if (i < words && out_bits)
+            out_bits[i] = allowed[i];
+        else
+            out[i] = i < words ? allowed[i] : i < words + nf ? flags[i - words] : (uint64_t)*first_bad;
+    }
 }
 
 // sum the spread statistics slots of `regions` regions into out[3 * region + k]
@@ -2746,6 +2752,7 @@ struct EmitReq {
     uint64_t words = 0;
     const unsigned long long *first_bad = nullptr;
     uint64_t *out = nullptr;
+    uint64_t *out_bits = nullptr;  // the caller's own pinned result words (else out[0, words))
 };
 __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned long long *slots, int regions,
                                                               unsigned long long *out, unsigned long long *mirror,
@@ -2753,7 +2760,10 @@ __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned lon
     if (blockIdx.x) {
         const uint64_t nf = E.flags ? E.words : 0, m = E.words + nf + 1;
         for (uint64_t i = (uint64_t)(blockIdx.x - 1) * kBlock + threadIdx.x; i < m; i += (uint64_t)(gridDim.x - 1) * kBlock)
-            E.out[i] = i < E.words ? E.allowed[i] : i < E.words + nf ? E.flags[i - E.words] : (uint64_t)*E.first_bad;
+            if (i < E.words && E.out_bits)
+                E.out_bits[i] = E.allowed[i];
+            else
+                E.out[i] = i < E.words ? E.allowed[i] : i < E.words + nf ? E.flags[i - E.words] : (uint64_t)*E.first_bad;
         return;
     }
     __shared__ unsigned long long part[kBlock / 64][3];
@@ -4544,18 +4554,22 @@ struct ketogpu_engine {
             ensure_res(2 * words + 1);
             clear_bad = d_bad;  // reset by the run's clear launch
             // results, flags and the validation verdict in one launch with the statistics
-            emit_req = EmitReq{q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res};
+            // result words straight into the caller's buffer when it is a ketogpu_host_alloc
+            // buffer (no host copy after the call)
+            uint64_t *direct_bits = allowed ? (uint64_t *)host_view(allowed, device, false) : nullptr;
+            emit_req = EmitReq{q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res, direct_bits};
             run_once(q, &src, [&] {
                 if (emit_req.out) {  // not taken by the bidi cascade's tail
                     KLAUNCH(emit_kernel, dim3((unsigned)std::min<uint64_t>(blocks_for(2 * words + 1), 256)),
-                            dim3(kBlock), 0, stream, q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res);
+                            dim3(kBlock), 0, stream, q.d_allowed, flagged ? q.d_flags : nullptr, words, d_bad, h_res,
+                            direct_bits);
                     emit_req = EmitReq{};
                 }
             });
             // the staged words were final unless requests went on to the global path
             if (!last.spilled_requests) {
                 const uint64_t nf = flagged ? words : 0;
-                if (allowed) memcpy(allowed, h_res, words * 8);
+                if (allowed && !direct_bits) memcpy(allowed, h_res, words * 8);
                 if (flagged) memcpy(flagged, h_res + words, words * 8);
                 check_bad(h_res[words + nf]);
                 return;
