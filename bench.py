@@ -50,6 +50,9 @@ def parse():
                         "partitioned: hash-partitioned graph, per-level all-to-all (config #5 path)")
     p.add_argument("--scale", type=float, default=0.02,
                    help="partitioned: config #5 size as a fraction of its 5B tuples (1.0 = full)")
+    p.add_argument("--tier-exchange", action="store_true",
+                   help="partitioned tier at world 1: run the exchange path over an RCCL communicator of one rank "
+                        "(queries and replies through ncclSend/ncclRecv to itself) instead of reading rows in place")
     p.add_argument("--part-engine", choices=["tier", "level"], default="tier",
                    help="partitioned: tier = two exchanges per batch over the replicated core (ketogpu_tier_*); "
                         "level = the per-level frontier exchange (ketogpu_part_*)")
@@ -323,7 +326,11 @@ def main_partitioned(a, rank, world, local):
     w = synth.config5(**sizes, checks=n_req, check_seed=synth.SEED + 1)
     rss0 = max_rss_gb()
     t0 = time.time()
-    sh = Shard.load(w.namespaces, lambda: w.batches(1 << 20))
+    ncomm = None
+    if a.tier_exchange and world == 1:
+        from keto_amd.partition import NativeComm
+        ncomm = NativeComm(device=local, kind="rccl")
+    sh = Shard.load(w.namespaces, lambda: w.batches(1 << 20), native_comm=ncomm)
     t_load = time.time() - t0
     rss_load = max_rss_gb()
     sst = sh.stats()
@@ -335,7 +342,7 @@ def main_partitioned(a, rank, world, local):
     core_info = None
     if tier:
         t0 = time.time()
-        core = Core(sh)
+        core = Core(sh, ncomm)
         cv = core.view()
         core_info = {"seconds": round(time.time() - t0, 2), "interior_nodes": int(cv["num_interior"]),
                      "forward_entries": int(len(cv["f_col"])), "backward_entries": int(len(cv["b_col"])),
@@ -343,7 +350,7 @@ def main_partitioned(a, rank, world, local):
                                                                               max(sst["rows"], 1), 5)}
         del cv
         log(f"core gathered: {core_info}")
-        eng = TieredEngine(sh, device=local, core=core)
+        eng = TieredEngine(sh, device=local, core=core, comm=ncomm)
         mine = slice(rank * per_gpu, (rank + 1) * per_gpu)  # this rank's own requests
         pinned = (check.pinned(roots[mine]), check.pinned(targets[mine]))
         bits = np.zeros((per_gpu + 63) // 64, dtype=np.uint64)
@@ -447,8 +454,8 @@ def main_partitioned(a, rank, world, local):
                         "shard": sst}}
         if tier:
             out.update({"engine": "two-tier (ketogpu_tier_check_ids, keto_amd/csrc/tier.cpp)", "core": core_info,
-                        "tier": dict(eng.stats(), exchange="RCCL grouped send/recv + all-gather" if world > 1 else
-                                     "world 1: rows read in place, no exchange")})
+                        "tier": dict(eng.stats(), exchange="RCCL grouped send/recv + all-gather"
+                                     if world > 1 or ncomm is not None else "world 1: rows read in place, no exchange")})
         else:
             st = eng.local.stats()
             out.update({"engine": "per-level (ketogpu_part_check_ids, keto_amd/csrc/part_round.cpp)",

@@ -408,8 +408,8 @@ struct TierDevice : TierSteps {
                 at += counts[p];
             }
             THIP(hipMemcpyAsync(d_small + kCursor, h_small + kCursor, 64 * 8, hipMemcpyHostToDevice, stream));
+            // no wait: the exchange reads `send` on this stream (or copies it to the host here first)
             tier::launch_query_scatter(G, cur_r, cur_t, n, d_small + kCursor, send, stream);
-            THIP(hipStreamSynchronize(stream));
         });
     }
 
@@ -441,8 +441,7 @@ struct TierDevice : TierSteps {
     int reply_emit(tier::Rec *send, uint64_t cap) override {
         return guarded("two-tier replies", [&] {
             THIP(hipSetDevice(dev));
-            tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);
-            THIP(hipStreamSynchronize(stream));
+            tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
         });
     }
 
@@ -494,6 +493,14 @@ struct TierDevice : TierSteps {
             if (h_small[kFirstBad] != ~0ull)
                 throw Error(KETOGPU_EINVAL, "request " + std::to_string(h_small[kFirstBad]) +
                                                 " has an id outside the partitioned layout");
+            // KETOGPU_TEST_TIER_OVERFLOW=1 (tests): every request is reported unfinished, its
+            // bit cleared, so the per-level engine answers the whole batch
+            static const bool force_overflow = getenv("KETOGPU_TEST_TIER_OVERFLOW") != nullptr;
+            if (force_overflow) {
+                std::fill(bits, bits + words, 0);
+                for (uint64_t c = 0; c < n; c++) overflow.push_back((uint32_t)c);
+                return;
+            }
             const uint32_t *hc = (const uint32_t *)(h_small + kLists);
             const uint32_t last = hc[tier::kStages - 1];
             if (last) {  // units no table held: their requests go to the per-level engine
@@ -613,8 +620,8 @@ struct ketogpu_tier {
             if (nr) THIP(hipMemcpyAsync(recv.p, h_recv.p, nr, hipMemcpyHostToDevice, stream()));
             THIP(hipStreamSynchronize(stream()));
         } else {
+            // RCCL: on the steps' stream, ordered before the next step's kernels (no wait)
             comm->alltoallv(send.p, sb.data(), recv.p, rb.data(), stream());
-            if (comm->device) comm->wait(stream());
         }
         st.collectives++;
         st.exchange_ms += ms_since(t0);

@@ -25,8 +25,10 @@ def _slices(n, world):
     return [np.arange(k, n, world) for k in range(world)]
 
 
-def _tier_worker(rank, world, port, seed, out_dir, device_steps, max_batch):
+def _tier_worker(rank, world, port, seed, out_dir, device_steps, max_batch, force_overflow=False):
     import torch.distributed as dist
+    if force_overflow:
+        os.environ["KETOGPU_TEST_TIER_OVERFLOW"] = "1"
     from keto_amd.partition import Core, TieredEngine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -52,16 +54,17 @@ def _tier_worker(rank, world, port, seed, out_dir, device_steps, max_batch):
         st = eng.stats()
         np.save(os.path.join(out_dir, f"rank{rank}.npy"), np.stack([idx, got.astype(np.int64)]))
         np.save(os.path.join(out_dir, f"stats{rank}.npy"),
-                np.array([st["queries_sent"], st["records_sent"], st["records_received"], st["batches"]]))
+                np.array([st["queries_sent"], st["records_sent"], st["records_received"], st["batches"],
+                          st["overflow_requests"], st["fallback_calls"]]))
         eng.close()
     finally:
         dist.destroy_process_group()
 
 
-def _run_tier(world, seed, port, device_steps=False, max_batch=0):
+def _run_tier(world, seed, port, device_steps=False, max_batch=0, force_overflow=False):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_tier_worker, args=(world, port, seed, d, device_steps, max_batch), nprocs=world,
-                           join=True, start_method="spawn")
+        mp.start_processes(_tier_worker, args=(world, port, seed, d, device_steps, max_batch, force_overflow),
+                           nprocs=world, join=True, start_method="spawn")
         got = [np.load(os.path.join(d, f"rank{r}.npy")) for r in range(world)]
         stats = [np.load(os.path.join(d, f"stats{r}.npy")) for r in range(world)]
         cores = [np.load(os.path.join(d, f"core{r}.npy")) for r in range(world)] if not device_steps else []
@@ -319,3 +322,32 @@ def test_tier_device_two_ranks_share_gpu():
     for idx, ans in got:
         np.testing.assert_array_equal(ans.astype(bool), want[idx])
     assert all(s[0] > 0 for s in stats)
+
+
+@pytest.mark.gpu
+def test_tier_device_fallback_to_per_level_engine(monkeypatch):
+    """KETOGPU_TEST_TIER_OVERFLOW=1: every request reported unfinished by the LDS stages, so
+    the per-level engine (built on first need from the same shard) answers all of them —
+    one rank, then two ranks sharing the GPU over gloo (the overflow lists gathered from
+    both ranks, each rank keeping its own answers)"""
+    from keto_amd.partition import TieredEngine
+    _need_gpu()
+    namespaces, rows, reqs = _case(86, n_rows=1200, n_req=1500)
+    want = _want(namespaces, rows, reqs)
+    sh = _load(namespaces, rows)
+    roots, targets, _ = sh.resolve_batch(persistence.request_columns(reqs))
+    monkeypatch.setenv("KETOGPU_TEST_TIER_OVERFLOW", "1")
+    eng = TieredEngine(sh, device=0)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    st = eng.stats()
+    assert st["fallback_calls"] == 1 and st["overflow_requests"] == len(reqs)
+    monkeypatch.delenv("KETOGPU_TEST_TIER_OVERFLOW")
+    got, stats, _ = _run_tier(2, 86, 29795, device_steps=True, force_overflow=True)
+    for idx, ans in got:
+        np.testing.assert_array_equal(ans.astype(bool), _case_want(86, idx))  # the workers' _case(86)
+    assert all(s[5] >= 1 and s[4] > 0 for s in stats)
+
+
+def _case_want(seed, idx):
+    namespaces, rows, reqs = _case(seed)
+    return _want(namespaces, rows, reqs)[idx]
