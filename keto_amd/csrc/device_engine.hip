@@ -40,6 +40,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "device_util.hpp"
@@ -1874,23 +1875,38 @@ constexpr int kLiteF = 128;  // ring entries per direction
 // 21 units per CU; slots p99 230 and rings p99 35 / 72 per unit fit it) ran 0.299 vs 0.284
 // ms per 10^6 requests, 512 slots with those rings 0.290: more units in flight do not pay
 // for the non-power-of-two probe, and the first stage is not occupancy-bound here.
-template <int H, int FF, int FB> struct LiteShared;
+template <int H, int FF, int FB, int U = 16> struct LiteShared;
 
-template <int H_, int FF_, int FB_>
+// U = 16 requests per unit: one 64-bit state word per slot, direction d's visited bits at
+// 32d and pending bits at 32d + 16.  U = 32 (plan "lite32"): visited words in st (32 bits
+// per direction: the meet is still one atomic) and pending words in pd.
+template <int H_, int FF_, int FB_, int U_>
 struct LiteShared {
     static constexpr int H = H_;             // table slots (not necessarily a power of two)
     static constexpr int HMAX = H * 7 / 8;   // load limit: a unit spills beyond it
     static constexpr int FF = FF_, FB = FB_; // ring entries, forward / backward
+    static constexpr int U = U_;             // requests per unit
+    static_assert(U == 16 || U == 32, "16 or 32 request bits per direction");
+    using Mask = std::conditional_t<U == 16, uint16_t, uint32_t>;
+    static constexpr uint32_t MASK = U == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    static constexpr int psh(int d) { return U == 16 ? 32 * d + 16 : 32 * d; }  // pending bits of direction d
     alignas(16) uint32_t key[H];
-    alignas(16) unsigned long long st[H];  // fwd visited | fwd pending | bwd visited | bwd pending
+    alignas(16) unsigned long long st[H];  // visited (and for U = 16 pending) bits, as above
+    alignas(16) unsigned long long pd[U == 32 ? H : 2];  // U = 32: pending bits
     uint32_t ring_sd[FF + FB];             // slot | seed << 14 | degree << 16 (forward ring, then backward)
     uint32_t ring_bg[FF + FB];             // the row's first record; a seed entry: its request
-    unsigned long long sbase[2][16];       // seed rows' first records (64-bit)
+    unsigned long long sbase[2][U];        // seed rows' first records (64-bit)
     unsigned long long e_beg[64];          // the chunk's entries' first records
     uint32_t c_pre[64];                    // owner map
     uint32_t c_pre2[64];                   // owner map of the prefetched forward seed rows (level 0)
-    uint32_t root[16];
-    uint16_t e_mask[64];
+    uint32_t root[U];
+    Mask e_mask[64];
+    __device__ __forceinline__ unsigned long long &pend(int h) {
+        if constexpr (U == 32)
+            return pd[h];
+        else
+            return st[h];
+    }
     uint32_t n_used, spill, found, active;
     uint32_t head[2], tail[2];
     template <int D>
@@ -1902,6 +1918,8 @@ struct LiteShared {
 };
 
 using LiteShape = LiteShared<512, kLiteF, kLiteF>;
+// plan "lite32": 32 requests per unit, 1024 slots, 256-entry rings (26 KB: 6 units per CU)
+using LiteShape32 = LiteShared<1024, 2 * kLiteF, 2 * kLiteF, 32>;
 
 // find (insert == false) or find-or-insert u in a table of H slots (any H); -1 when absent
 // (or the table is full)
@@ -1975,13 +1993,13 @@ __device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, 
         // one 64-bit atomic: the old word carries the other direction's visited bits, so of
         // two pushes that complete a meet the later one sees it
         const unsigned long long old = atomicOr(&S.st[h], (unsigned long long)m << (32 * D));
-        uint32_t newly = m & ~(uint32_t)(old >> (32 * D)) & 0xFFFFu;
-        const uint32_t meet = newly & (uint32_t)(old >> (32 - 32 * D)) & 0xFFFFu;
+        uint32_t newly = m & ~(uint32_t)(old >> (32 * D)) & SH::MASK;
+        const uint32_t meet = newly & (uint32_t)(old >> (32 - 32 * D)) & SH::MASK;
         if (meet) atomicOr(&S.found, meet);
         newly &= ~(meet | lk);
         if (newly && deg) {
-            const unsigned long long o2 = atomicOr(&S.st[h], (unsigned long long)newly << (32 * D + 16));
-            app = !((uint32_t)(o2 >> (32 * D + 16)) & 0xFFFFu);
+            const unsigned long long o2 = atomicOr(&S.pend(h), (unsigned long long)newly << SH::psh(D));
+            app = !((uint32_t)(o2 >> SH::psh(D)) & SH::MASK);
             or_acc |= newly;
             deg_acc += app ? deg : 0u;
         }
@@ -2018,7 +2036,7 @@ __device__ __forceinline__ void lite_fetch(SH &S, const FRec *rec, uint32_t *own
     x.lo = (uint32_t)(o < 0 ? 0 : o);
     x.ls = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x.lo << 2), (int)start);
     const uint32_t e = min(eb + lane, total - 1);
-    const unsigned long long b0 = SEED ? S.sbase[D][x.lo & 15] : S.e_beg[x.lo];
+    const unsigned long long b0 = SEED ? S.sbase[D][x.lo & (SH::U - 1)] : S.e_beg[x.lo];
     x.rc = rec[b0 + (e - x.ls)];
 }
 
@@ -2046,7 +2064,7 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
         const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
         uint32_t m = 0;
         if (eb + lane < total) {
-            m = (SEED ? (1u << (x.lo & 15)) : (uint32_t)S.e_mask[x.lo]) & ~found;
+            m = (SEED ? (1u << (x.lo & (SH::U - 1))) : (uint32_t)S.e_mask[x.lo]) & ~found;
             edges++;
             if (D == 1 && x.rc.node >= g.Ni) {  // a source entry of rev(t): it can only meet r itself
                 uint32_t hit = 0;
@@ -2101,14 +2119,14 @@ __device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec 
         if (i < t0) {
             const uint32_t w = S.template sd<D>(i), bg = S.template bg<D>(i);
             const uint32_t s = w & 0x3FFFu;
-            const unsigned long long old = atomicAnd(&S.st[s], ~(0xFFFFull << (32 * D + 16)));
-            take = (uint32_t)(old >> (32 * D + 16)) & open;
+            const unsigned long long old = atomicAnd(&S.pend(s), ~((unsigned long long)SH::MASK << SH::psh(D)));
+            take = (uint32_t)(old >> SH::psh(D)) & open;
             deg = take ? w >> 16 : 0u;
             // a seed row's begin is 64-bit (sbase); an interior row's is the record's 32 bits,
             // shifted like sbase by the test knob (rec is taken back by it)
-            S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & 15] : (unsigned long long)bg + g.seed_shift;
+            S.e_beg[lane] = (w >> 14) & 1u ? S.sbase[D][bg & (SH::U - 1)] : (unsigned long long)bg + g.seed_shift;
         }
-        S.e_mask[lane] = (uint16_t)take;
+        S.e_mask[lane] = (typename SH::Mask)take;
         L.head = min(c + 64, t0);  // these entries are read: their ring slots are free
         if (lane == 0) S.head[D] = L.head;
         __syncthreads();
@@ -2134,13 +2152,15 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
                                           unsigned long long *stamp = nullptr) {
     const uint32_t lane = threadIdx.x;
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
-    const uint64_t c0 = unit * 16;
+    const uint64_t c0 = unit * SH::U;
     for (int i = lane; i < SH::H / 4; i += 64) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
     for (int i = lane; i < SH::H / 2; i += 64) reinterpret_cast<uint4 *>(S.st)[i] = make_uint4(0, 0, 0, 0);
+    if constexpr (SH::U == 32)
+        for (int i = lane; i < SH::H / 2; i += 64) reinterpret_cast<uint4 *>(S.pd)[i] = make_uint4(0, 0, 0, 0);
     if (lane == 0) S.n_used = S.spill = S.found = S.active = S.head[0] = S.head[1] = S.tail[0] = S.tail[1] = 0;
     const uint32_t r = seed.r, t = seed.t;
     uint64_t rows = 0, edges = 0;
-    if (lane < 16) {
+    if (lane < SH::U) {
         if (r != KETOGPU_NODE_NONE && r < kDynBase) {
             rows += 2;
             // nothing reaches a t without predecessors (!=: the two-tier mode's begins are
@@ -2160,8 +2180,8 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     uint32_t active = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.active);
     // seeds: r forward-visited and t backward-visited at distance 0 (t = r excluded: a meet
     // needs >= 1 edge); both rows short: both read at level 0, else both become pending
-    const bool v = lane < 16 && ((active >> lane) & 1u);
-    const uint32_t bit = 1u << (lane & 15);
+    const bool v = lane < SH::U && ((active >> lane) & 1u);
+    const uint32_t bit = 1u << (lane & (SH::U - 1));
     const uint32_t rdeg = (uint32_t)(seed.fe - seed.fb), tdeg = (uint32_t)(seed.re - seed.rb);
     const bool eager = rdeg <= g.seed_max && tdeg <= g.seed_max;
     uint32_t pend_mask[2];
@@ -2174,10 +2194,16 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         const bool pend = h >= 0 && !eager && deg;
         bool app = false;
         if (h >= 0) {
-            unsigned long long bits = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
-            if (pend) bits |= (unsigned long long)bit << (32 * side + 16);
-            const unsigned long long old = atomicOr(&S.st[h], bits);
-            app = pend && !((uint32_t)(old >> (32 * side + 16)) & 0xFFFFu);
+            const unsigned long long vb = (side == 0 || t != r) ? (unsigned long long)bit << (32 * side) : 0ull;
+            const unsigned long long pb = pend ? (unsigned long long)bit << SH::psh(side) : 0ull;
+            unsigned long long oldp;
+            if constexpr (SH::U == 16) {
+                oldp = atomicOr(&S.st[h], vb | pb);
+            } else {
+                if (vb) atomicOr(&S.st[h], vb);
+                oldp = pb ? atomicOr(&S.pd[h], pb) : 0ull;
+            }
+            app = pend && !((uint32_t)(oldp >> SH::psh(side)) & SH::MASK);
         }
         pend_mask[side] = (uint32_t)__ballot(pend);
         const uint32_t idx = lds_append(app, &S.tail[side]);  // idx < 16 <= F
@@ -2197,7 +2223,7 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     uint32_t pf = rpend, pb = tpend, sf = 0, sb = 0;
     uint32_t acc_or[2] = {0, 0}, acc_deg[2] = {0, 0};
     for (int side = 0; side < 2; side++) {  // the pending seed rows' degrees
-        const uint32_t d = (lane < 16 && ((pend_mask[side] >> lane) & 1u)) ? (side ? tdeg : rdeg) : 0u;
+        const uint32_t d = (lane < SH::U && ((pend_mask[side] >> lane) & 1u)) ? (side ? tdeg : rdeg) : 0u;
         (side ? sb : sf) = wave_sum_all(d);
     }
     if (stamp) stamp[1] = __builtin_amdgcn_s_memtime();
@@ -2207,8 +2233,8 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     // not stored
     {
         const bool e = v && eager;
-        const uint32_t eager_mask = (uint32_t)__ballot(e) & 0xFFFFu;
-        const uint32_t df = (lane < 16 && e) ? rdeg : 0u, db = (lane < 16 && e) ? tdeg : 0u;
+        const uint32_t eager_mask = (uint32_t)__ballot(e) & SH::MASK;
+        const uint32_t df = (lane < SH::U && e) ? rdeg : 0u, db = (lane < SH::U && e) ? tdeg : 0u;
         // the forward rows' first 64 records are loaded before the backward pushes, so
         // the two dependent expansions of level 0 wait for HBM once
         LiteEdge f0{};
@@ -2296,7 +2322,7 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         edges += __shfl_down(edges, s, 64);
     }
     if (lane == 0) {
-        const uint32_t res = S.found & 0xFFFFu;
+        const uint32_t res = S.found & SH::MASK;
         if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
         atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
         atomicAdd(&stat_slot(stats)[1], (unsigned long long)edges);
@@ -2311,10 +2337,10 @@ __global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, 
                                                   unsigned long long *stats, uint64_t unit0,
                                                   unsigned long long *stamps) {
     __shared__ SH S;
-    const uint64_t units = (n + 15) / 16;
+    const uint64_t units = (n + SH::U - 1) / SH::U;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
-    bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
+    bidi_load_rt<SH::U>(unit, units, roots, targets, n, r, t);
     unsigned long long *stamp =
         (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
     lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats, stamp);
@@ -2332,17 +2358,17 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
     uint32_t r[K], t[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * SH::U + threadIdx.x;
         r[k] = t[k] = KETOGPU_NODE_NONE;
-        if (threadIdx.x < 16 && c < n) {
+        if (threadIdx.x < SH::U && c < n) {
             r[k] = hr[c];
             t[k] = ht[c];
         }
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
-        if (threadIdx.x < 16 && c < n) {
+        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * SH::U + threadIdx.x;
+        if (threadIdx.x < SH::U && c < n) {
             if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
                 atomicMin(first_bad, (unsigned long long)c);
                 r[k] = t[k] = KETOGPU_NODE_NONE;
@@ -2351,7 +2377,7 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
             dt[c] = t[k];
         }
     }
-    const uint64_t units = (n + 15) / 16;
+    const uint64_t units = (n + SH::U - 1) / SH::U;
 #pragma unroll 1
     for (int k = 0; k < K; k++) {
         const uint64_t unit = (uint64_t)blockIdx.x * K + k;
@@ -3338,8 +3364,12 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
-            KLAUNCH((lite_kernel<LiteShape>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets,
-                    q.n, q.allowed, out, out_count, stats, unit0, stp);
+            if (c.u == 32)
+                KLAUNCH((lite_kernel<LiteShape32>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
+                        q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp);
+            else
+                KLAUNCH((lite_kernel<LiteShape>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots, q.targets,
+                        q.n, q.allowed, out, out_count, stats, unit0, stp);
             return;
         }
         if (chunked && c == BidiCfg{9, 64, KETO_F1, 7, 16, 1}) {  // the default shape's chunk instantiation
@@ -3630,7 +3660,7 @@ struct ketogpu_engine {
         const char *plan = getenv("KETOGPU_UNITS");
         std::string p = plan ? plan : "auto";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        const bool lite_req = p == "lite" || p == "auto";
+        const bool lite_req = p == "lite" || p == "lite32" || p == "auto";
         use_v2 = p == "v2" || p == "bidi" || lite_req;
         // Edge records carry 32-bit row begins.  Plan lite reads only INTERIOR rows through
         // records (ids below Ni come first, so their begins are the smallest) and carries
@@ -3655,11 +3685,12 @@ struct ketogpu_engine {
             disabled("bidi", "rows pass 2^32 entries (32-bit seed begins)");
         if (lite_req && !s.has_ambiguous && !lite_ok) disabled("lite", "interior rows pass 2^32 entries");
         frec_needed = recs && (use_v2 || use_bidi || use_lite);
-        if (p == "lite" && use_lite) {  // forced: the lite first stage, no trials
+        if ((p == "lite" || p == "lite32") && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
             bidi_cfg.lite = 1;
-            bidi_cfg.hlog = 9;
-            bidi_cfg.f = kLiteF;
+            bidi_cfg.hlog = p == "lite32" ? 10 : 9;
+            bidi_cfg.f = p == "lite32" ? 2 * kLiteF : kLiteF;
+            bidi_cfg.u = p == "lite32" ? 32 : 16;
         }
         trials_left = p == "auto" && (use_bidi || use_lite) && use_units ? kTrialRuns : 0;
         if (const char *pad = getenv("KETOGPU_LDS_PAD")) lds_pad = (unsigned)atoi(pad);
@@ -4084,7 +4115,11 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite)                                                                                 \
+        if (bidi_cfg.lite && bidi_cfg.u == 32)                                                             \
+            KLAUNCH((lite_host_kernel<K, LiteShape32>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, \
+                    stream, g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n,      \
+                    q.allowed, list[0], &spill_count[0], st.stats, d_bad);                                 \
+        else if (bidi_cfg.lite)                                                                            \
             KLAUNCH((lite_host_kernel<K, LiteShape>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0,   \
                     stream, g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n,      \
                     q.allowed, list[0], &spill_count[0], st.stats, d_bad);                                 \

@@ -47,14 +47,16 @@ def test_nil_subject_is_bad_request():
         eng.SubjectIsAllowed(rt.InternalRelationTuple("n", "o", "r", None))
 
 
-@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift"])
+@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift", "lite32"])
 def unit_plan(request, monkeypatch):
     """first LDS pass of engines created while active: the default bidirectional units
     (one-wave, 512-slot tables), bidi with the wide 2048-slot table, forward-only unit2, or
     plan lite (per-unit direction) — also with every row begin carried past 2^32 through
-    its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT)"""
+    its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT) — and lite with 32-request units"""
     if request.param == "v2":
         monkeypatch.setenv("KETOGPU_UNITS", "v2")
+    elif request.param == "lite32":
+        monkeypatch.setenv("KETOGPU_UNITS", "lite32")
     elif request.param.startswith("lite"):
         monkeypatch.setenv("KETOGPU_UNITS", "lite")
         if request.param == "lite-shift":
