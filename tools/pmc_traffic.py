@@ -68,16 +68,32 @@ def summarise(src, workload):
     # the kernel sources this profile was taken at: bench.py reports the traffic only
     # while they are unchanged
     out = {"workload": workload, "source": src, "source_hash": kernel_source_hash(), "kernels": {}}
-    dur = defaultdict(list)
-    res = {}
+    # Per family, only the dispatches of its most frequent grid size are averaged: a run
+    # also launches the same kernel over smaller batches (trials, chunks, tails), whose
+    # per-launch bytes and durations would otherwise be mixed into the bench's launch.
+    def grid(r):  # total work-items (kernel trace: Grid_Size_X/Y/Z; counter collection: Grid_Size)
+        if "Grid_Size_X" in r:
+            return str(int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y") or 1) * int(r.get("Grid_Size_Z") or 1))
+        return r.get("Grid_Size", "")
+
+    grids = defaultdict(lambda: defaultdict(int))
+    rows = []
     for tr in glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True):
         for r in read_csv(tr):
             fam = family(r.get("Kernel_Name", ""))
-            if not fam:
-                continue
-            dur[fam].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-            res[fam] = {k: r[k] for k in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size",
-                                          "Workgroup_Size", "Grid_Size") if k in r}
+            if fam:
+                rows.append((fam, r))
+                grids[fam][grid(r)] += 1
+    modal = {fam: max(g, key=g.get) for fam, g in grids.items()}
+    dur = defaultdict(list)
+    res = {}
+    for fam, r in rows:
+        if grid(r) != modal[fam]:
+            continue
+        dur[fam].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        res[fam] = {k: r[k] for k in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size",
+                                      "Workgroup_Size") if k in r}
+        res[fam]["grid_size"] = modal[fam]
     per = defaultdict(lambda: defaultdict(list))
     for cc in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
         by_dispatch = defaultdict(lambda: defaultdict(float))
@@ -85,6 +101,8 @@ def summarise(src, workload):
         for r in read_csv(cc):
             fam = family(r.get("Kernel_Name", ""))
             if not fam:
+                continue
+            if fam in modal and grid(r) != modal[fam]:
                 continue
             d = (cc, r.get("Dispatch_Id"), r.get("Agent_Id"))
             by_dispatch[d][r["Counter_Name"]] += float(r["Counter_Value"])
