@@ -4209,9 +4209,13 @@ struct ketogpu_engine {
                     KLAUNCH(unit2_kernel<1>, dim3((unsigned)(k * 4)), dim3(kBlock), 0, stream, g, frec, q.roots,
                             q.targets, q.n, q.allowed, q.flags, list[1], 4u, list[0], c1, st.stats, nullptr);
             } else {
-                KLAUNCH(unit2_cascade_kernel<4>, dim3(stage_grid(u2_prev[0], 1536)), dim3(kBlock), 0, stream, g,
+                // persistent grids: as many workgroups as fit the CUs at once (LDS-bound)
+                constexpr unsigned per4 = (unsigned)(160 * 1024 / sizeof(Unit2Shared<4>));
+                constexpr unsigned per1 = (unsigned)(160 * 1024 / sizeof(Unit2Shared<1>));
+                static_assert(per4 >= 1 && per1 >= 1, "a unit2 stage's LDS exceeds a CU");
+                KLAUNCH(unit2_cascade_kernel<4>, dim3(stage_grid(u2_prev[0], 256 * per4)), dim3(kBlock), 0, stream, g,
                         frec, q.roots, q.targets, q.n, q.allowed, q.flags, list[0], c16, 4u, list[1], c4, st.stats);
-                KLAUNCH(unit2_cascade_kernel<1>, dim3(stage_grid(u2_prev[1], 256)), dim3(kBlock), 0, stream, g,
+                KLAUNCH(unit2_cascade_kernel<1>, dim3(stage_grid(u2_prev[1], 256 * per1)), dim3(kBlock), 0, stream, g,
                         frec, q.roots, q.targets, q.n, q.allowed, q.flags, list[1], c4, 4u, list[0], c1, st.stats);
             }
             HIP_CHECK(hipEventRecord(c, stream));
