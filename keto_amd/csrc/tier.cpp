@@ -243,6 +243,9 @@ struct TierDevice : TierSteps {
     std::vector<void *> owned;
     int n_cu = 256;
     uint64_t core_records = 0, seed_records = 0;
+    // KETOGPU_TEST_TIER_OVERFLOW=1 when the engine is made (tests): every request is reported
+    // unfinished, its bit cleared, so the per-level engine answers the whole batch
+    bool force_overflow = false;
     std::string err;
     // per-step scratch (grown on demand)
     Buf d_req, d_lens, d_scan, d_bnd, d_bits, d_list[3];
@@ -326,6 +329,7 @@ struct TierDevice : TierSteps {
         if (device < 0 || device >= ndev) throw Error(KETOGPU_EDEVICE, "no such HIP device");
         this->device = true;
         dev = device;
+        force_overflow = getenv("KETOGPU_TEST_TIER_OVERFLOW") != nullptr;
         THIP(hipSetDevice(dev));
         THIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         THIP(hipEventCreate(&ev0));
@@ -493,9 +497,6 @@ struct TierDevice : TierSteps {
             if (h_small[kFirstBad] != ~0ull)
                 throw Error(KETOGPU_EINVAL, "request " + std::to_string(h_small[kFirstBad]) +
                                                 " has an id outside the partitioned layout");
-            // KETOGPU_TEST_TIER_OVERFLOW=1 (tests): every request is reported unfinished, its
-            // bit cleared, so the per-level engine answers the whole batch
-            static const bool force_overflow = getenv("KETOGPU_TEST_TIER_OVERFLOW") != nullptr;
             if (force_overflow) {
                 std::fill(bits, bits + words, 0);
                 for (uint64_t c = 0; c < n; c++) overflow.push_back((uint32_t)c);

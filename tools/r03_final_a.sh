@@ -2,7 +2,7 @@
 # round 3 close-out, part A: the whole GPU suite, smoke, and the undelivered-copy probes
 export TMPDIR=/tmp
 mkdir -p gpurun_out/final
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
   > gpurun_out/final/gpu_tests.log 2>&1 || { echo "GPU tests failed"; tail -30 gpurun_out/final/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/final/gpu_tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1 \
