@@ -707,9 +707,10 @@ typedef struct {
 typedef struct {
     uint32_t tag, node;
 } ketogpu_tier_query;
-/* a row entry in transit: the entry's node, its core row (count, first record), tag */
+/* a row entry in transit: the entry's node and its request's tag (the receiver looks the
+ * entry's core row up in its own copy of the core) */
 typedef struct {
-    uint32_t node, deg, begin, tag;
+    uint32_t node, tag;
 } ketogpu_tier_rec;
 typedef struct {
     uint64_t calls, batches, requests, overflow_requests, fallback_calls;

@@ -101,13 +101,21 @@ struct RcclComm : Comm {
     void alltoallv(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb, hipStream_t s) override {
         CHIP(hipSetDevice(dev));
         const RcclApi &a = rccl();
-        nccl_check(a.GroupStart(), "ncclGroupStart");
         uint64_t so = 0, ro = 0;
+        for (int p = 0; p < rank; p++) so += sb[p], ro += rb[p];
+        // the rank's own segment: a copy engine's DMA on the same stream (RCCL's self
+        // send/receive runs as a kernel at ~1 TB/s)
+        if (sb[rank] != rb[rank]) throw Error(KETOGPU_EINVAL, "alltoallv: own segment sizes differ");
+        if (sb[rank])
+            CHIP(hipMemcpyAsync((char *)recv + ro, (const char *)send + so, sb[rank], hipMemcpyDeviceToDevice, s));
+        if (world == 1) return;
+        nccl_check(a.GroupStart(), "ncclGroupStart");
+        so = ro = 0;
         for (int p = 0; p < world; p++) {
             // one send and one receive per peer in one group: RCCL runs them concurrently,
             // one xGMI link per peer pair
-            if (sb[p]) nccl_check(a.Send((const char *)send + so, sb[p], ncclUint8, p, comm, s), "ncclSend");
-            if (rb[p]) nccl_check(a.Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, s), "ncclRecv");
+            if (p != rank && sb[p]) nccl_check(a.Send((const char *)send + so, sb[p], ncclUint8, p, comm, s), "ncclSend");
+            if (p != rank && rb[p]) nccl_check(a.Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, s), "ncclRecv");
             so += sb[p];
             ro += rb[p];
         }

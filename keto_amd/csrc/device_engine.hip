@@ -2062,10 +2062,10 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
     rec -= g.seed_shift;  // begins carry the shift (0 outside the test knob)
     auto push = [&](uint32_t eb, const LiteEdge &x) {
         const uint32_t found = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.found);
+        edges += min(64u, total - eb);  // the wave's count (uniform: scalar), not one per lane
         uint32_t m = 0;
         if (eb + lane < total) {
             m = (SEED ? (1u << (x.lo & (SH::U - 1))) : (uint32_t)S.e_mask[x.lo]) & ~found;
-            edges++;
             if (D == 1 && x.rc.node >= g.Ni) {  // a source entry of rev(t): it can only meet r itself
                 uint32_t hit = 0;
                 for (uint32_t b = m; b; b &= b - 1)
@@ -2317,10 +2317,7 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         stamp[13] = ring_max[1];
     }
 #pragma unroll
-    for (int s = 32; s; s >>= 1) {
-        rows += __shfl_down(rows, s, 64);
-        edges += __shfl_down(edges, s, 64);
-    }
+    for (int s = 32; s; s >>= 1) rows += __shfl_down(rows, s, 64);  // edges: already the wave's
     if (lane == 0) {
         const uint32_t res = S.found & SH::MASK;
         if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
@@ -2506,12 +2503,16 @@ constexpr int kTB = 256;
 __global__ __launch_bounds__(kTB) void tier_query_count_kernel(tier::Graph G, const uint32_t *roots,
                                                                const uint32_t *targets, uint64_t n,
                                                                unsigned long long *counts,
-                                                               unsigned long long *first_bad) {
+                                                               unsigned long long *first_bad, uint32_t *stage) {
     __shared__ unsigned int hist[64];
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kTB) {
         const uint32_t r = roots[i], t = targets[i];
+        if (stage) {  // one read of pinned host memory over PCIe; the later passes read HBM
+            stage[i] = r;
+            stage[n + i] = t;
+        }
         if ((r != KETOGPU_NODE_NONE && r >= G.Nx) || (t != KETOGPU_NODE_NONE && t >= G.N)) {
             atomicMin(first_bad, (unsigned long long)i);
             continue;
@@ -2652,7 +2653,7 @@ __global__ __launch_bounds__(kTB) void tier_scan_tiles_kernel(uint64_t *v, uint6
 // output index finds its query by a binary search over the wave's offsets in LDS, so
 // consecutive lanes write consecutive records), pad = the query's tag
 __global__ __launch_bounds__(kTB) void tier_reply_copy_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
-                                                              const uint64_t *off, tier::Rec *out, uint64_t cap) {
+                                                              const uint64_t *off, tier::Reply *out, uint64_t cap) {
     __shared__ uint64_t s_pre[kTB / 64][65];
     __shared__ uint64_t s_src[kTB / 64][64];
     __shared__ uint32_t s_tag[kTB / 64][64];
@@ -2683,24 +2684,57 @@ __global__ __launch_bounds__(kTB) void tier_reply_copy_kernel(tier::Graph G, con
                     hi = mid;
             }
             const uint32_t tg = s_tag[wv][lo];
-            const tier::Rec *src = (tg & 1u) ? G.lr_rec : G.lf_rec;
-            tier::Rec rec = src[s_src[wv][lo] + (o - s_pre[wv][lo])];
-            rec.pad = tg;
-            if (o0 + o < cap) out[o0 + o] = rec;
+            const uint32_t *src = (tg & 1u) ? G.lr_node : G.lf_node;  // 4 bytes per entry, not the 16-byte record
+            const uint32_t node = src[s_src[wv][lo] + (o - s_pre[wv][lo])];
+            if (o0 + o < cap) out[o0 + o] = tier::Reply{node, tg};
         }
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-// received replies -> per request seed bounds (each query's row is contiguous)
-__global__ __launch_bounds__(kTB) void tier_bounds_kernel(const tier::Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq) {
-    for (uint64_t k = (uint64_t)blockIdx.x * kTB + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kTB) {
-        const uint32_t tag = recv[k].pad;
-        const uint64_t i = tag >> 1;
-        if (i >= nreq) continue;
-        uint32_t *b = reinterpret_cast<uint32_t *>(&bnd[i]) + 2 * (tag & 1u);
-        if (k == 0 || recv[k - 1].pad != tag) b[0] = (uint32_t)k;
-        if (k + 1 == n || recv[k + 1].pad != tag) b[1] = (uint32_t)(k + 1);
+// received replies -> seed records (entry x: its core row in this rank's copy of the core —
+// forward entries are interior; a backward entry outside the interior is (x, 0, 0): only
+// compared with the root) and per request seed bounds (each query's row is contiguous)
+// Four consecutive entries per thread, one 8-byte {begin, count} read per entry: the
+// random reads into the core's row table are L2 requests, one per lane, and set the time.
+constexpr int kSeedPer = 4;
+__global__ __launch_bounds__(kTB) void tier_seed_kernel(tier::Graph G, const tier::Reply *recv, uint64_t n,
+                                                        tier::Rec *seed, uint4 *bnd, uint64_t nreq) {
+    for (uint64_t k0 = ((uint64_t)blockIdx.x * kTB + threadIdx.x) * kSeedPer; k0 < n;
+         k0 += (uint64_t)gridDim.x * kTB * kSeedPer) {
+        tier::Reply e[kSeedPer];
+        if (k0 + kSeedPer <= n) {  // 32-byte aligned: two 16-byte loads
+            const uint4 *v = reinterpret_cast<const uint4 *>(recv + k0);
+            const uint4 a = v[0], b = v[1];
+            e[0] = {a.x, a.y};
+            e[1] = {a.z, a.w};
+            e[2] = {b.x, b.y};
+            e[3] = {b.z, b.w};
+        } else {
+#pragma unroll
+            for (int j = 0; j < kSeedPer; j++) e[j] = k0 + j < n ? recv[k0 + j] : tier::Reply{~0u, ~0u};
+        }
+        const uint32_t prev = k0 ? recv[k0 - 1].tag : ~0u;
+        const uint32_t next = k0 + kSeedPer < n ? recv[k0 + kSeedPer].tag : ~0u;
+        uint2 row[kSeedPer];
+#pragma unroll
+        for (int j = 0; j < kSeedPer; j++) {
+            const uint2 *rows = (e[j].tag & 1u) ? G.core_b_row : G.core_f_row;
+            const bool in = e[j].node < G.Ni && k0 + j < n;
+            row[j] = in ? rows[e[j].node] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kSeedPer; j++) {
+            const uint64_t k = k0 + j;
+            if (k >= n) break;
+            const uint32_t tag = e[j].tag;
+            seed[k] = tier::Rec{e[j].node, row[j].y, row[j].x, tag};
+            const uint64_t i = tag >> 1;
+            if (i >= nreq) continue;
+            uint32_t *b = reinterpret_cast<uint32_t *>(&bnd[i]) + 2 * (tag & 1u);
+            if ((j ? e[j - 1].tag : prev) != tag) b[0] = (uint32_t)k;
+            if ((j + 1 < kSeedPer ? (k + 1 < n ? e[j + 1].tag : ~0u) : next) != tag) b[1] = (uint32_t)(k + 1);
+        }
     }
 }
 
@@ -3165,8 +3199,10 @@ static unsigned tier_grid(uint64_t n, uint64_t per, unsigned cap = 8192) {
 }
 
 void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
-                        unsigned long long *counts, unsigned long long *first_bad, hipStream_t s) {
-    if (n) KLAUNCH(tier_query_count_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, roots, targets, n, counts, first_bad);
+                        unsigned long long *counts, unsigned long long *first_bad, uint32_t *stage, hipStream_t s) {
+    if (n)
+        KLAUNCH(tier_query_count_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, roots, targets, n, counts,
+                first_bad, stage);
 }
 
 void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
@@ -3186,13 +3222,14 @@ void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s) {
     KLAUNCH(tier_scan_tiles_kernel, dim3((unsigned)nb), dim3(kTB), 0, s, v, n, scratch, nb);
 }
 
-void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Rec *out, uint64_t cap,
+void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Reply *out, uint64_t cap,
                        hipStream_t s) {
     if (n) KLAUNCH(tier_reply_copy_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, out, cap);
 }
 
-void launch_bounds(const Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq, hipStream_t s) {
-    if (n) KLAUNCH(tier_bounds_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, recv, n, bnd, nreq);
+void launch_seed_records(const Graph &g, const Reply *recv, uint64_t n, Rec *seed, uint4 *bnd, uint64_t nreq,
+                         hipStream_t s) {
+    if (n) KLAUNCH(tier_seed_kernel, dim3(tier_grid(n, kTB * kSeedPer)), dim3(kTB), 0, s, g, recv, n, seed, bnd, nreq);
 }
 
 }  // namespace tier

@@ -203,9 +203,9 @@ struct TierSteps {
     virtual int queries(const uint32_t *roots, const uint32_t *targets, uint64_t n, tier::Query *send,
                         uint64_t *counts) = 0;
     virtual int reply_sizes(const tier::Query *recv, uint64_t n, const uint64_t *from, uint64_t *counts) = 0;
-    virtual int reply_emit(tier::Rec *send, uint64_t cap) = 0;
+    virtual int reply_emit(tier::Reply *send, uint64_t cap) = 0;
     // recv null: the rank owns every root and target (world 1)
-    virtual int evaluate(const uint32_t *roots, const uint32_t *targets, uint64_t n, const tier::Rec *recv,
+    virtual int evaluate(const uint32_t *roots, const uint32_t *targets, uint64_t n, const tier::Reply *recv,
                          uint64_t nrecv, uint64_t *bits, std::vector<uint32_t> &overflow) = 0;
     virtual void stats(ketogpu_tier_stats &) {}
     virtual std::string error() = 0;
@@ -224,8 +224,10 @@ struct VtableTier : TierSteps {
     int reply_sizes(const tier::Query *recv, uint64_t n, const uint64_t *from, uint64_t *counts) override {
         return rc(v.reply_sizes(v.ctx, (const ketogpu_tier_query *)recv, n, from, counts), "reply_sizes");
     }
-    int reply_emit(tier::Rec *send, uint64_t) override { return rc(v.reply_emit(v.ctx, (ketogpu_tier_rec *)send), "reply_emit"); }
-    int evaluate(const uint32_t *r, const uint32_t *t, uint64_t n, const tier::Rec *recv, uint64_t nrecv, uint64_t *bits,
+    int reply_emit(tier::Reply *send, uint64_t) override {
+        return rc(v.reply_emit(v.ctx, (ketogpu_tier_rec *)send), "reply_emit");
+    }
+    int evaluate(const uint32_t *r, const uint32_t *t, uint64_t n, const tier::Reply *recv, uint64_t nrecv, uint64_t *bits,
                  std::vector<uint32_t> &overflow) override {
         overflow.assign(std::max<uint64_t>(n, 1), 0);
         uint64_t no = 0;
@@ -248,13 +250,14 @@ struct TierDevice : TierSteps {
     bool force_overflow = false;
     std::string err;
     // per-step scratch (grown on demand)
-    Buf d_req, d_lens, d_scan, d_bnd, d_bits, d_list[3];
+    Buf d_req, d_lens, d_scan, d_bnd, d_seed, d_bits, d_list[3];
     unsigned long long *d_small = nullptr;  // [0..63] counts, [64..127] cursors, [128] first_bad, [129] bad query,
                                             // [130..132] list counts, [136..] stats
     uint64_t *h_small = nullptr;            // pinned mirror
     // the current step's requests (device-readable) and replies in flight
     const uint32_t *cur_r = nullptr, *cur_t = nullptr, *src_r = nullptr, *src_t = nullptr;
     uint64_t cur_n = 0;
+    bool in_place = false;  // cur_r / cur_t are the caller's buffers (a pinned view)
     const tier::Query *rq = nullptr;
     uint64_t rq_n = 0;
     // the first evaluation stage bracketed by events (the roofline's kernel time)
@@ -270,7 +273,7 @@ struct TierDevice : TierSteps {
             (void)hipSetDevice(dev);
             (void)hipStreamSynchronize(stream);
         }
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) b->release();
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) b->release();
         for (void *p : owned) (void)hipFree(p);
         for (hipEvent_t e : {ev0, ev1})
             if (e) (void)hipEventDestroy(e);
@@ -335,7 +338,7 @@ struct TierDevice : TierSteps {
         THIP(hipEventCreate(&ev0));
         THIP(hipEventCreate(&ev1));
         THIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) {
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) {
             b->device = true;
             b->dev = dev;
         }
@@ -355,10 +358,22 @@ struct TierDevice : TierSteps {
         const uint64_t Ni = core->Ni;
         G.core_f = records(core->f_off.data(), Ni, core->f_col.data(), core->f_off, Ni);
         G.core_b = records(core->b_off.data(), Ni, core->b_col.data(), core->b_off, Ni);
+        {  // {begin, count} per interior node, one 8-byte read per received entry (u32 like the
+           // records' begin fields)
+            std::vector<uint2> o(Ni);
+            for (uint64_t x = 0; x < Ni; x++)
+                o[x] = make_uint2((uint32_t)core->f_off[x], (uint32_t)(core->f_off[x + 1] - core->f_off[x]));
+            G.core_f_row = upload(o.data(), o.size());
+            for (uint64_t x = 0; x < Ni; x++)
+                o[x] = make_uint2((uint32_t)core->b_off[x], (uint32_t)(core->b_off[x + 1] - core->b_off[x]));
+            G.core_b_row = upload(o.data(), o.size());
+        }
         G.lf_off = upload(v.lf_off, (size_t)v.owned_expandable + 1);
         G.lr_off = upload(v.lr_off, (size_t)v.owned_nodes + 1);
         G.lf_rec = records(v.lf_off, v.owned_expandable, v.lf_col, core->f_off, Ni);
         G.lr_rec = records(v.lr_off, v.owned_nodes, v.lr_col, core->b_off, Ni);
+        G.lf_node = upload(v.lf_col, (size_t)v.lf_off[v.owned_expandable]);
+        G.lr_node = upload(v.lr_col, (size_t)v.lr_off[v.owned_nodes]);
         G.lf_base = (int64_t)((intptr_t)G.lf_rec - (intptr_t)G.core_f) / (int64_t)sizeof(tier::Rec);
         G.lr_base = (int64_t)((intptr_t)G.lr_rec - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
         core_records = core->f_col.size() + core->b_col.size();
@@ -375,7 +390,8 @@ struct TierDevice : TierSteps {
         cur_n = n;
         cur_r = (const uint32_t *)host_view(r, dev, true);
         cur_t = cur_r ? (const uint32_t *)host_view(t, dev, true) : nullptr;
-        if (!cur_r || !cur_t) {
+        in_place = cur_r && cur_t;
+        if (!in_place) {
             uint32_t *d = (uint32_t *)d_req.ensure(8 * std::max<uint64_t>(n, 1));
             if (n) {
                 THIP(hipMemcpyAsync(d, r, 4 * n, hipMemcpyHostToDevice, stream));
@@ -402,7 +418,13 @@ struct TierDevice : TierSteps {
             set_requests(r, t, n, true);
             THIP(hipMemsetAsync(d_small, 0, 128 * 8, stream));
             THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 8, stream));
-            tier::launch_query_count(G, cur_r, cur_t, n, d_small + kCounts, d_small + kFirstBad, stream);
+            // requests read in place from pinned memory are staged into HBM by the count pass
+            uint32_t *stage = n && in_place ? (uint32_t *)d_req.ensure(8 * n) : nullptr;
+            tier::launch_query_count(G, cur_r, cur_t, n, d_small + kCounts, d_small + kFirstBad, stage, stream);
+            if (stage) {
+                cur_r = stage;
+                cur_t = stage + n;
+            }
             THIP(hipMemcpyAsync(h_small, d_small, 129 * 8, hipMemcpyDeviceToHost, stream));
             THIP(hipStreamSynchronize(stream));
             uint64_t at = 0;
@@ -442,14 +464,14 @@ struct TierDevice : TierSteps {
         });
     }
 
-    int reply_emit(tier::Rec *send, uint64_t cap) override {
+    int reply_emit(tier::Reply *send, uint64_t cap) override {
         return guarded("two-tier replies", [&] {
             THIP(hipSetDevice(dev));
             tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
         });
     }
 
-    int evaluate(const uint32_t *r, const uint32_t *t, uint64_t n, const tier::Rec *recv, uint64_t nrecv, uint64_t *bits,
+    int evaluate(const uint32_t *r, const uint32_t *t, uint64_t n, const tier::Reply *recv, uint64_t nrecv, uint64_t *bits,
                  std::vector<uint32_t> &overflow) override {
         overflow.clear();
         return guarded("two-tier evaluation", [&] {
@@ -472,11 +494,12 @@ struct TierDevice : TierSteps {
             if (recv) {
                 uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
                 THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
-                tier::launch_bounds(recv, nrecv, bnd, n, stream);
+                tier::Rec *seed = (tier::Rec *)d_seed.ensure(sizeof(tier::Rec) * std::max<uint64_t>(nrecv, 1));
+                tier::launch_seed_records(G, recv, nrecv, seed, bnd, n, stream);
                 E.bnd = bnd;
-                E.recv = recv;
-                E.recv_base_f = (int64_t)((intptr_t)recv - (intptr_t)G.core_f) / (int64_t)sizeof(tier::Rec);
-                E.recv_base_b = (int64_t)((intptr_t)recv - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
+                E.recv = seed;
+                E.recv_base_f = (int64_t)((intptr_t)seed - (intptr_t)G.core_f) / (int64_t)sizeof(tier::Rec);
+                E.recv_base_b = (int64_t)((intptr_t)seed - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
             }
             unsigned *lc = (unsigned *)(d_small + kLists);  // three u32 list counts (+ padding)
             THIP(hipEventRecord(ev0, stream));
@@ -558,9 +581,16 @@ struct ketogpu_tier {
     std::mutex mu;
     ketogpu_tier_stats st{};
 
+    uint64_t *h_gather = nullptr;  // pinned staging of the count all-gathers (RCCL)
+    static constexpr size_t kGatherMax = 80;  // values per rank (at most world + 1 = 65)
+
     ~ketogpu_tier() {
         if (pe) ketogpu_part_engine_free(pe);
         if (part) ketogpu_part_free(part);
+        if (h_gather) {
+            (void)hipStreamSynchronize(stream());
+            (void)hipHostFree(h_gather);
+        }
     }
 
     hipStream_t stream() const { return steps->stream; }
@@ -568,17 +598,23 @@ struct ketogpu_tier {
     // every rank's n u64 values -> mat (world * n, rank order)
     void gather(const uint64_t *v, size_t n) {
         mat.assign(n * world, 0);
-        if (!comm) {
+        if (!comm || world == 1) {  // a gather over one rank is the identity
             std::copy(v, v + n, mat.begin());
             return;
         }
         const auto t0 = Clock::now();
         if (comm->device) {
+            // through pinned staging: both copies are asynchronous DMA, one wait
+            if (n > kGatherMax) throw Error(KETOGPU_EINVAL, "two-tier: gather wider than its staging");
+            if (!h_gather)
+                THIP(hipHostMalloc((void **)&h_gather, 8 * kGatherMax * (world + 1), hipHostMallocDefault));
             uint64_t *d = (uint64_t *)small_d.ensure(8 * n * (world + 1));
-            THIP(hipMemcpyAsync(d, v, n * 8, hipMemcpyHostToDevice, stream()));
+            std::copy(v, v + n, h_gather);
+            THIP(hipMemcpyAsync(d, h_gather, n * 8, hipMemcpyHostToDevice, stream()));
             comm->allgather(d, d + n, n * 8, stream());
-            THIP(hipMemcpyAsync(mat.data(), d + n, n * world * 8, hipMemcpyDeviceToHost, stream()));
+            THIP(hipMemcpyAsync(h_gather + n, d + n, n * world * 8, hipMemcpyDeviceToHost, stream()));
             THIP(hipStreamSynchronize(stream()));
+            std::copy(h_gather + n, h_gather + n + n * world, mat.begin());
         } else {
             comm->allgather(v, mat.data(), n * 8, stream());
         }
@@ -627,7 +663,6 @@ struct ketogpu_tier {
         st.collectives++;
         st.exchange_ms += ms_since(t0);
         *n_in = nr / unit;
-        st.records_received += unit == sizeof(tier::Rec) ? nr / unit : 0;
         return KETOGPU_OK;
     }
 
@@ -660,16 +695,17 @@ struct ketogpu_tier {
             if (!local) {
                 for (uint64_t c : counts) out += c;
                 try {
-                    r_send.ensure(sizeof(tier::Rec) * out);
+                    r_send.ensure(sizeof(tier::Reply) * out);
                 } catch (const Error &e) {
                     local = e.code;
                 }
             }
-            if (!local) local = steps->reply_emit(r_send.as<tier::Rec>(), out);
+            if (!local) local = steps->reply_emit(r_send.as<tier::Reply>(), out);
             if (!local) st.records_sent += out;
-            code = exchange(local, counts.data(), sizeof(tier::Rec), r_send, r_recv, &nr, from);
+            code = exchange(local, counts.data(), sizeof(tier::Reply), r_send, r_recv, &nr, from);
             if (code) fail(code, local, steps->error());
-            local = steps->evaluate(roots, targets, n, r_recv.as<tier::Rec>(), nr, bits, overflow);
+            st.records_received += nr;
+            local = steps->evaluate(roots, targets, n, r_recv.as<tier::Reply>(), nr, bits, overflow);
         }
         st.evaluate_ms += ms_since(t_eval) - (st.exchange_ms - exch0);
         // every rank's status and unfinished requests (world 1: its own)

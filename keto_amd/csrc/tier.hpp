@@ -38,14 +38,21 @@ struct Rec {
 struct Query {
     uint32_t tag, node;
 };
+// a reply entry in transit (include/ketogpu.h ketogpu_tier_rec): 8 bytes; the receiver
+// turns it into a Rec with its own copy of the core
+struct Reply {
+    uint32_t node, tag;
+};
 
 // device view of one rank's graph
 struct Graph {
     uint32_t world, rank, Ni, Nx, N;  // global layout (shard.cpp)
     uint32_t Nil, Nxl, Nl;            // owned class bounds
     const Rec *core_f, *core_b;       // core rows of every interior node (replicated)
+    const uint2 *core_f_row, *core_b_row;  // [Ni] {first record, count}: a received entry's core row
     const uint64_t *lf_off, *lr_off;  // owned seed rows: fint of owned expandable, rev of owned nodes
     const Rec *lf_rec, *lr_rec;
+    const uint32_t *lf_node, *lr_node;  // the same rows' entries as plain node ids (the replies)
     int64_t lf_base, lr_base;         // lf_rec - core_f and lr_rec - core_b in records
     uint32_t both_max, seed_max;
 };
@@ -70,8 +77,10 @@ void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_li
 int stage_units_per_cu(int stage);
 
 // queries of the batch grouped by owner: count (per destination) then scatter at cursors
+// stage (may be null): the requests are also copied there (2n words: roots, then targets),
+// so later passes read them from HBM instead of host memory again
 void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
-                        unsigned long long *counts, unsigned long long *first_bad, hipStream_t s);
+                        unsigned long long *counts, unsigned long long *first_bad, uint32_t *stage, hipStream_t s);
 void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
                           unsigned long long *cursor, Query *out, hipStream_t s);
 // replies: the rows the received queries ask for, in query order (so grouped like the
@@ -80,10 +89,12 @@ void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t 
 void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *lens, unsigned long long *bad,
                           hipStream_t s);
 void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s);  // exclusive, in place, v[n] = total
-void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Rec *out, uint64_t cap,
+void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Reply *out, uint64_t cap,
                        hipStream_t s);
-// received replies -> per request seed bounds (bnd cleared by the caller)
-void launch_bounds(const Rec *recv, uint64_t n, uint4 *bnd, uint64_t nreq, hipStream_t s);
+// received replies -> seed records (the entries' core rows looked up) and per request seed
+// bounds (bnd cleared by the caller), one pass
+void launch_seed_records(const Graph &g, const Reply *recv, uint64_t n, Rec *seed, uint4 *bnd, uint64_t nreq,
+                         hipStream_t s);
 
 }  // namespace tier
 }  // namespace ketogpu

@@ -18,7 +18,7 @@ from keto_amd import _lib as L
 from tests.part_cpu import NONE, owner
 
 QUERY = np.dtype([("tag", "<u4"), ("node", "<u4")])                                  # ketogpu_tier_query
-REC = np.dtype([("node", "<u4"), ("deg", "<u4"), ("begin", "<u4"), ("tag", "<u4")])  # ketogpu_tier_rec
+REC = np.dtype([("node", "<u4"), ("tag", "<u4")])  # ketogpu_tier_rec
 
 
 class CpuTier:
@@ -60,12 +60,6 @@ class CpuTier:
         off, col = self.core["f_off"], self.core["f_col"]
         return col[off[u]:off[u + 1]]
 
-    def _rec(self, x, d, tag):
-        off = self.core["b_off" if d else "f_off"]
-        if x < self.Ni:
-            return (x, int(off[x + 1] - off[x]), int(off[x]), tag)
-        return (x, 0, 0, tag)
-
     # ------------------------------------------------------------------ steps
     def queries(self, roots, targets, send, counts):
         out = []
@@ -91,7 +85,7 @@ class CpuTier:
             k = 0
             for tag, node in q[at:at + int(frm[p])].tolist():
                 row = self._row(node, tag & 1)
-                recs += [self._rec(x, tag & 1, tag) for x in row]
+                recs += [(x, tag) for x in row]
                 k += len(row)
             counts[p] = k
             at += int(frm[p])
@@ -112,7 +106,7 @@ class CpuTier:
                 if r != NONE and t != NONE and r < self.Nx and t < self.N:
                     fint[i], rev[i] = self._row(r, 0), self._row(t, 1)
         else:
-            for node, _deg, _begin, tag in recv.tolist():
+            for node, tag in recv.tolist():
                 (rev if tag & 1 else fint)[tag >> 1].append(node)
         for i in range(n):
             r, t = int(roots[i]), int(targets[i])
