@@ -4000,16 +4000,26 @@ struct ketogpu_engine {
         std::vector<SpillStage> stages;
         for (const SpillStage &sg : cascade)
             if (sg.u <= (stages.empty() ? bidi_cfg.u : stages.back().u)) stages.push_back(sg);
-        int cur = 0, u_prev = bidi_cfg.u;
+        int u_prev = bidi_cfg.u;
         std::vector<uint32_t> fans;
-        for (size_t k = 0; k < stages.size(); k++) {
-            const SpillStage sg = stages[k];
+        for (const SpillStage &sg : stages) {
             fans.push_back((uint32_t)(u_prev / sg.u));
-            launch_stage(sg, q, list[cur], &spill_count[k], fans.back(), list[cur ^ 1], &spill_count[k + 1],
-                         st.stats + 4 * kStatSlots, k < 8 ? stage_prev[k] : ~0ull);
-            cur ^= 1;
             u_prev = sg.u;
         }
+        const int cur = (int)(stages.size() & 1);  // the list the last stage writes
+        auto launch_stages = [&](uint64_t prev0) {
+            for (size_t k = 0, c = 0; k < stages.size(); k++, c ^= 1)
+                launch_stage(stages[k], q, list[c], &spill_count[k], fans[k], list[c ^ 1], &spill_count[k + 1],
+                             st.stats + 4 * kStatSlots, k == 0 ? prev0 : k < 8 ? stage_prev[k] : ~0ull);
+        };
+        // Lazy cascade: when the previous call's first stage spilled nothing (config #2: one
+        // unit in 60k, most calls none), the spill stages are not launched up front — three
+        // empty persistent launches cost ~14 us per call — but only after the synchronization
+        // shows spills, followed by a second statistics pass, the result copies again and a
+        // second synchronization.  KETOGPU_CASCADE_EAGER=1: always up front (A/B).
+        static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
+        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0;
+        if (!lazy) launch_stages(stage_prev[0]);
         // b == nullptr (host batches): no event between the call's kernels (each costs ~6 us of
         // GPU idle between the launches it separates); one event after the last launch
         if (b) HIP_CHECK(hipEventRecord(d, stream));
@@ -4028,6 +4038,18 @@ struct ketogpu_engine {
         if (before_sync) before_sync();
         if (!b) HIP_CHECK(hipEventRecord(d, stream));
         wait_stream();
+        const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
+        size_t launched = lazy ? 1 : stages.size() + 1;
+        if (lazy && cnt[0]) {  // spilled after all: the stages now, then statistics and results again
+            d = ev();
+            launch_stages((uint64_t)cnt[0] * fans[0]);
+            KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(),
+                    d_hctr + 16, 12, E);
+            if (before_sync) before_sync();
+            HIP_CHECK(hipEventRecord(d, stream));
+            wait_stream();
+            launched = stages.size() + 2;
+        }
         unit_end = d;
         if (b) {
             unit_ev.push_back({a, b});
@@ -4037,7 +4059,6 @@ struct ketogpu_engine {
         }
         const uint64_t *t = (const uint64_t *)h_ctr + 16;
         rs.main_bytes = 16 * t[0] + 16 * t[1] + 4 * t[2] + 8 * q.n + 8 * ((q.n + 63) / 64);
-        const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
         if (cascade_log) {
             fprintf(stderr, "[cascade] units %llu, spills per stage:", (unsigned long long)bunits);
             for (size_t k = 0; k < ns; k++) fprintf(stderr, " %u", cnt[k]);
@@ -4045,8 +4066,8 @@ struct ketogpu_engine {
         }
         for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
         for (size_t k = 0; k < stages.size() && k < 8; k++) stage_prev[k] = (uint64_t)cnt[k] * fans[k];
-        rs.push_launches += ns;
-        rs.unit_launches += ns;
+        rs.push_launches += launched;
+        rs.unit_launches += launched;
         const uint64_t left = cnt[ns - 1];
         if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
         if (left && cur != 0)  // single requests for the global path, read from list[0]

@@ -198,6 +198,35 @@ def test_unit_spill_to_global_path():
     assert st["spilled_requests"] > 0  # n-wide sides exceed even a single request's table
 
 
+@pytest.mark.parametrize("plan", ["lite", "bidi"])
+def test_lazy_cascade_after_calls_without_spills(monkeypatch, plan):
+    """the spill stages are launched after the synchronization when the previous call's
+    first stage spilled nothing (device_engine.hip bidi_tail): a batch that spills right
+    after batches that did not must still get every answer, from the second pass"""
+    n = 9000
+    rows = [(1, "top", "m", None, 1, f"g{i:05d}", "m") for i in range(n)]
+    rows += [(1, f"g{i:05d}", "m", f"u{i}", None, None, None) for i in range(n)]
+    rows += [(1, f"p{i:05d}", "m", None, 1, "T", "m") for i in range(n)]
+    rows += [(1, "z", "m", None, 1, f"p{i:05d}", "m") for i in range(n)]
+    rows += [(1, "g00007", "m", None, 1, "p00007", "m")]
+    snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
+    monkeypatch.setenv("KETOGPU_UNITS", plan)
+    eng = check.Engine(snap)
+    small = [rt.InternalRelationTuple("n", "g00009", "m", rt.SubjectID("u9")),
+             rt.InternalRelationTuple("n", "g00009", "m", rt.SubjectID("u8"))] * 50
+    wide = [rt.InternalRelationTuple("n", "top", "m", rt.SubjectSet("n", "T", "m")),
+            rt.InternalRelationTuple("n", "g00009", "m", rt.SubjectSet("n", "T", "m"))] * 50
+    for _ in range(3):
+        assert eng.check_many(small) == [True, False] * 50
+        assert eng.last_stats()["spilled_units"] == 0
+    assert eng.check_many(wide) == [True, False] * 50  # spills: the lazy second pass
+    st = eng.last_stats()
+    assert st["spilled_units"] > 0
+    assert st["unit_launches"] >= 3  # first stage, then the stages and the statistics again
+    assert eng.check_many(wide) == [True, False] * 50  # spilled last time: stages up front
+    assert eng.check_many(small) == [True, False] * 50
+
+
 def test_large_forward_closure_small_backward_side():
     # a 14000-group forward closure with a 1-entry backward side: bidi expands the backward
     # side and looks the root's row up, so nothing spills; the forward-only plan spills past
