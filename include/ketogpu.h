@@ -216,6 +216,28 @@ typedef struct {
 } ketogpu_graph_view;
 int ketogpu_snapshot_graph(const ketogpu_snapshot *s, ketogpu_graph_view *out);
 
+/* Plan "core"'s record arrays (keto_amd/csrc/core_index.hpp), built on the host the way an
+ * engine builds them, for tools and tests (the engine builds its own; KETOGPU_UNITS=core).
+ * Per direction (0 forward, 1 backward) one array of 16-byte records {node, deg, begin,
+ * pad}: core rows (the rows among interior nodes), closure rows (pad bit 31: TERMINAL
+ * entries), node blocks of the seed rows (fint(v) / rev(v); the head record of node v's
+ * block {count, first record low, high, 0}) and overflow rows.  A record's deg/begin name
+ * the node's expansion row in the same array; pad bit 30 = that row is a closure row.
+ * closure_cap[d] = 0: no closure rows; block[d] = 0: block size chosen from the rows. */
+typedef struct ketogpu_core_index ketogpu_core_index;
+typedef struct {
+    const uint32_t *records; /* 4 x u32 per record */
+    uint64_t num_records;
+    uint64_t block_base;     /* record index of node 0's block */
+    uint32_t block_records;  /* records per node block: 4, 8, 16 or 32 */
+    uint64_t overflow_rows;  /* seed rows kept outside their block */
+    uint64_t closure_nodes, closure_entries;
+} ketogpu_core_records;
+int ketogpu_core_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], const uint32_t block[2],
+                             ketogpu_core_index **out);
+int ketogpu_core_index_view(const ketogpu_core_index *c, int direction, ketogpu_core_records *out);
+void ketogpu_core_index_free(ketogpu_core_index *c);
+
 /* ------------------------------------------------------------------- check */
 /* relationtuple.Subject: SubjectID{ID} or SubjectSet{Namespace, Object, Relation}
  * (internal/relationtuple/definitions.go:39-41,103-118) */
@@ -368,7 +390,8 @@ typedef struct {
     uint64_t main_bytes;        /* algorithmic HBM bytes of the first unit pass   */
     double main_ms;             /* its device time (hipEvent)                     */
     int32_t plan;               /* first stage of the run: 0 global path only, 1 bidi,
-                                 * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1.
+                                 * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1,
+                                 * 5 lite, 6 core (lite with closure rows).
                                  * KETOGPU_UNITS=auto (default) tries bidi (128- and 64-
                                  * entry pending lists), v2 and (with hubs) the global path
                                  * alone on the first two batches of
@@ -380,6 +403,13 @@ typedef struct {
     uint32_t hub_words;         /* 64-bit words per interior node of the hub closures   */
     double hub_build_ms;        /* one-time hub closure build at engine creation        */
     uint32_t plan_unit;         /* bidi: requests per first-stage unit (16 or 8)        */
+    /* plan 6 "core" (lite over its own record arrays with CLOSURE rows: an interior node
+     * whose forward / backward closure has at most cap nodes expands into all of it in one
+     * level; KETOGPU_CLOSURE="cap_f,cap_b") */
+    uint32_t closure_cap_f, closure_cap_b;  /* 0, 0 when the plan is off                */
+    uint64_t closure_nodes_f, closure_nodes_b;      /* nodes with a closure row          */
+    uint64_t closure_entries_f, closure_entries_b;  /* records in closure rows           */
+    double core_build_ms;       /* one-time build of the core arrays at engine creation */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 

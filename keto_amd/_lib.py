@@ -100,9 +100,11 @@ class RunStats(C.Structure):
         ("spilled_requests", C.c_uint64), ("unit_launches", C.c_uint64), ("main_bytes", C.c_uint64),
         ("main_ms", C.c_double), ("plan", C.c_int32), ("plan_lists", C.c_uint32),
         ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double),
-        ("plan_unit", C.c_uint32)]
+        ("plan_unit", C.c_uint32), ("closure_cap_f", C.c_uint32), ("closure_cap_b", C.c_uint32),
+        ("closure_nodes_f", C.c_uint64), ("closure_nodes_b", C.c_uint64), ("closure_entries_f", C.c_uint64),
+        ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double)]
 
-    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite"}
+    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core"}
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -135,6 +137,12 @@ class GraphView(C.Structure):
     _fields_ = [("num_nodes", C.c_uint32), ("num_expandable", C.c_uint32), ("num_interior", C.c_uint32),
                 ("fint_off", C.POINTER(C.c_uint64)), ("fint_col", C.POINTER(C.c_uint32)),
                 ("rev_off", C.POINTER(C.c_uint64)), ("rev_col", C.POINTER(C.c_uint32))]
+
+
+class CoreRecords(C.Structure):
+    _fields_ = [("records", C.POINTER(C.c_uint32)), ("num_records", C.c_uint64), ("block_base", C.c_uint64),
+                ("block_records", C.c_uint32), ("overflow_rows", C.c_uint64), ("closure_nodes", C.c_uint64),
+                ("closure_entries", C.c_uint64)]
 
 
 class TreeNode(C.Structure):
@@ -280,6 +288,9 @@ SIGNATURES = {
     "ketogpu_snapshot_free": (None, [vp]),
     "ketogpu_snapshot_stats_get": (C.c_int, [vp, C.POINTER(SnapshotStats)]),
     "ketogpu_snapshot_graph": (C.c_int, [vp, C.POINTER(GraphView)]),
+    "ketogpu_core_index_build": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]),
+    "ketogpu_core_index_view": (C.c_int, [vp, C.c_int, C.POINTER(CoreRecords)]),
+    "ketogpu_core_index_free": (None, [vp]),
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),
     "ketogpu_snapshot_apply": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(vp)]),
     "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),

@@ -43,6 +43,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "core_index.hpp"
 #include "device_util.hpp"
 #include "tier.hpp"
 #include "ketogpu_internal.hpp"
@@ -69,6 +70,10 @@ struct DevGraph {
     // arrays' base (0; a test knob, KETOGPU_TEST_BEGIN_SHIFT, that sends every begin
     // past 2^32 through the 64-bit path)
     uint64_t seed_shift;
+    // plan core: node blocks of the seed rows per direction (core_index.hpp): node v's
+    // block header is record blk[d] + (v << blk_log[d]) of that direction's array
+    uint64_t blk[2];
+    uint32_t blk_log[2];
     // hub index for the unit2 kernels (nullptr: off; see ketogpu_engine::build_hubs):
     // hub_of[v] (v < Nx) = hub number or NONE, hub_mask[v][hub_words] (v < Ni) bit h = v is
     // in the closure of hub h; forward edge records carry hub number + 1 in FRec::pad
@@ -1495,6 +1500,24 @@ __device__ __forceinline__ BidiSeed bidi_load_rows(const DevGraph &g, uint32_t r
     return s;
 }
 
+// plan core: the seed rows from the node blocks (core_index.hpp) — one 16-byte header per
+// row {count, first record (64 bits)} at the head of the node's block, a short row on the
+// header's own cache line(s) right behind it: one dependent HBM read instead of the offset
+// pair and then the records
+__device__ __forceinline__ BidiSeed core_load_rows(const DevGraph &g, const FRec *frec, const FRec *brec, uint32_t r,
+                                                   uint32_t t) {
+    BidiSeed s{t == KETOGPU_NODE_NONE ? KETOGPU_NODE_NONE : r, t, 0, 0, 0, 0};
+    if (s.r != KETOGPU_NODE_NONE && s.r < kDynBase) {
+        const FRec hf = frec[g.blk[0] + ((uint64_t)s.r << g.blk_log[0])];
+        const FRec hb = brec[g.blk[1] + ((uint64_t)t << g.blk_log[1])];
+        s.fb = (uint64_t)hf.deg | (uint64_t)hf.begin << 32;
+        s.fe = s.fb + hf.node;
+        s.rb = (uint64_t)hb.deg | (uint64_t)hb.begin << 32;
+        s.re = s.rb + hb.node;
+    }
+    return s;
+}
+
 // one unit (requests [U*unit, U*unit + U)) by the whole workgroup; `seed` as loaded by
 // bidi_load_rt + bidi_load_rows on lanes < U
 template <int U, int HLOG, int F, int BT, int LF>
@@ -1918,6 +1941,10 @@ struct LiteShared {
 };
 
 using LiteShape = LiteShared<512, kLiteF, kLiteF>;
+// plan core: closure rows keep tables and rings small (config #2: slots p99 116, rings p99
+// 35 / 57 per unit against lite's 230 / 72), so smaller shapes fit more units per CU
+using CoreShapeS = LiteShared<256, 64, 64>;
+using CoreShapeM = LiteShared<256, 64, 96>;
 // plan "lite32": 32 requests per unit, 1024 slots, 256-entry rings (26 KB: 6 units per CU)
 using LiteShape32 = LiteShared<1024, 2 * kLiteF, 2 * kLiteF, 32>;
 
@@ -1971,13 +1998,24 @@ __device__ __forceinline__ int lite_slot(uint32_t *key, uint32_t u, bool insert,
 struct LiteLevel {
     uint32_t lookup, sread;  // for the direction being expanded
     uint32_t head;           // the direction's ring: entries before it are read (ring_size check)
+    // plan core (CL): requests whose TERMINAL pushes (closure-row entries) are lookups —
+    // the other side is complete, or this level completes this side and the request
+    // closes after it (lite_unit)
+    uint32_t tlook = 0;
 };
 
-// one lane's push of node u (record fields deg / begin) in direction D
-template <class SH, int D>
+// plan core: record pad flags (core_index.hpp kRecTerminal / kRecClosure)
+constexpr uint32_t kPadTerminal = 0x80000000u, kPadClosure = 0x40000000u;
+
+// one lane's push of node u (record fields deg / begin / pad) in direction D.  CL (plan
+// core): a TERMINAL entry (of a closure row) is visited and never pending, looked up
+// under L.tlook; a pending row that is not a closure row adds its bits to nc_acc.
+template <class SH, int D, bool CL = false>
 __device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, uint32_t u, uint32_t deg,
-                                          uint32_t begin, uint32_t m, uint32_t &or_acc, uint32_t &deg_acc) {
-    const uint32_t lk = m & (L.lookup | (deg ? 0u : L.sread));
+                                          uint32_t begin, uint32_t m, uint32_t &or_acc, uint32_t &deg_acc,
+                                          uint32_t pad = 0, uint32_t *nc_acc = nullptr) {
+    const bool term = CL && (pad & kPadTerminal);
+    const uint32_t lk = m & (L.lookup | (term ? L.tlook : (deg ? 0u : L.sread)));
     int h = -1;
     bool inserted = false;
     if (want) {
@@ -2002,6 +2040,8 @@ __device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, 
             app = !((uint32_t)(o2 >> SH::psh(D)) & SH::MASK);
             or_acc |= newly;
             deg_acc += app ? deg : 0u;
+            if constexpr (CL)
+                if (!(pad & kPadClosure)) *nc_acc |= newly;
         }
     }
     const uint32_t idx = lds_append(app, &S.tail[D]);
@@ -2050,10 +2090,10 @@ __device__ __forceinline__ void lite_fetch0(SH &S, const DevGraph &g, const FRec
     if (total) lite_fetch<SH, D, SEED>(S, rec - g.seed_shift, own, my_deg, incl - my_deg, total, 0, x);
 }
 
-template <class SH, int D, bool SEED = false>
+template <class SH, int D, bool SEED = false, bool CL = false>
 __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec *rec, const LiteLevel &L,
                                             uint32_t my_deg, uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc,
-                                            uint32_t *own, const LiteEdge *pre = nullptr) {
+                                            uint32_t *own, const LiteEdge *pre = nullptr, uint32_t *nc_acc = nullptr) {
     const uint32_t lane = threadIdx.x;
     const uint32_t incl = wave_incl_sum_u32(my_deg);
     const uint32_t start = incl - my_deg;
@@ -2074,7 +2114,7 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
                 m = 0;
             }
         }
-        lite_push<SH, D>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc);
+        lite_push<SH, D, CL>(S, L, m != 0, x.rc.node, x.rc.deg, x.rc.begin, m, or_acc, deg_acc, x.rc.pad, nc_acc);
     };
     LiteEdge a{}, b{};
     if (pre) {
@@ -2107,9 +2147,10 @@ __device__ __forceinline__ void lite_expand(SH &S, const DevGraph &g, const FRec
 
 // consume direction D's ring (every pending row: one atomic reads and clears its pending
 // bits of D) and expand it
-template <class SH, int D>
+template <class SH, int D, bool CL = false>
 __device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec *rec, LiteLevel L, uint32_t open,
-                                           uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc) {
+                                           uint64_t &edges, uint32_t &or_acc, uint32_t &deg_acc,
+                                           uint32_t *nc_acc = nullptr) {
     const uint32_t lane = threadIdx.x;
     const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.head[D]);
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.tail[D]);
@@ -2130,7 +2171,7 @@ __device__ __forceinline__ void lite_level(SH &S, const DevGraph &g, const FRec 
         L.head = min(c + 64, t0);  // these entries are read: their ring slots are free
         if (lane == 0) S.head[D] = L.head;
         __syncthreads();
-        lite_expand<SH, D>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre);
+        lite_expand<SH, D, false, CL>(S, g, rec, L, deg, edges, or_acc, deg_acc, S.c_pre, nullptr, nc_acc);
         __syncthreads();
     }
 }
@@ -2144,8 +2185,13 @@ __device__ __forceinline__ uint32_t wave_sum_all(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_u32(x), 63);
 }
 
-// one 16-request unit by one wave (seed as bidi_load_rows loads it on lanes < 16)
-template <class SH>
+// one 16-request unit by one wave (seed as bidi_load_rows loads it on lanes < 16).
+// CL (plan core, core_index.hpp): records may name CLOSURE rows.  Per direction the unit
+// tracks the requests with a pending row that is not a closure row (nc); while every
+// request pending on a side has only closure rows pending there, that side alone is
+// expanded next and completes in that level, so its terminal entries are lookups for
+// the requests that close after it (the other side's seed row read).
+template <class SH, bool CL = false>
 __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *frec, const FRec *brec,
                                           const BidiSeed &seed, uint64_t *allowed, const uint64_t unit,
                                           uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats,
@@ -2222,6 +2268,9 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     // pending-row presence and degree totals per direction
     uint32_t pf = rpend, pb = tpend, sf = 0, sb = 0;
     uint32_t acc_or[2] = {0, 0}, acc_deg[2] = {0, 0};
+    // CL: requests with a pending row that is not a closure row, per direction (a pending
+    // seed row is a one-hop row)
+    uint32_t nc_f = rpend, nc_b = tpend, nc_acc[2] = {0, 0};
     for (int side = 0; side < 2; side++) {  // the pending seed rows' degrees
         const uint32_t d = (lane < SH::U && ((pend_mask[side] >> lane) & 1u)) ? (side ? tdeg : rdeg) : 0u;
         (side ? sb : sf) = wave_sum_all(d);
@@ -2239,15 +2288,20 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         // the two dependent expansions of level 0 wait for HBM once
         LiteEdge f0{};
         lite_fetch0<SH, 0, true>(S, g, frec, S.c_pre2, df, f0);
-        lite_expand<SH, 1, true>(S, g, brec, LiteLevel{0, 0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre);
+        lite_expand<SH, 1, true, CL>(S, g, brec, LiteLevel{0, 0, 0}, db, edges, acc_or[1], acc_deg[1], S.c_pre,
+                                     nullptr, &nc_acc[1]);
         __syncthreads();
-        lite_expand<SH, 0, true>(S, g, frec, LiteLevel{0, eager_mask, 0}, df, edges, acc_or[0], acc_deg[0],
-                                      S.c_pre2, &f0);
+        lite_expand<SH, 0, true, CL>(S, g, frec, LiteLevel{0, eager_mask, 0}, df, edges, acc_or[0], acc_deg[0],
+                                     S.c_pre2, &f0, &nc_acc[0]);
         __syncthreads();
         pf |= wave_or_all(acc_or[0]);
         pb |= wave_or_all(acc_or[1]);
         sf += wave_sum_all(acc_deg[0]);
         sb += wave_sum_all(acc_deg[1]);
+        if constexpr (CL) {
+            nc_f |= wave_or_all(nc_acc[0]);
+            nc_b |= wave_or_all(nc_acc[1]);
+        }
     }
     if (stamp) stamp[2] = __builtin_amdgcn_s_memtime();
     bool spilled = false;
@@ -2268,8 +2322,14 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         open &= ~closed;
         if (!open) break;
         const bool want_f = (pf & open) != 0, want_b = (pb & open) != 0;
+        // CL: a side whose open pending requests have only closure rows pending completes
+        // when expanded alone
+        const bool cf = CL && want_f && !(nc_f & open & pf), cb = CL && want_b && !(nc_b & open & pb);
         bool do_f, do_b;
-        if (want_f && want_b && sf <= g.both_max && sb <= g.both_max) {
+        if (cf || cb) {
+            do_b = cb && (!cf || sb <= sf);
+            do_f = !do_b;
+        } else if (want_f && want_b && sf <= g.both_max && sb <= g.both_max) {
             do_f = do_b = true;
         } else if (want_f && want_b) {
             do_f = sf <= sb;
@@ -2280,26 +2340,33 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
         }
         // bits of requests whose OTHER side is closed: only looked up (a meet or nothing);
         // a dead end (no row in this direction) is only looked up once the other side's
-        // seed row was read in an earlier level (it can meet nothing else)
+        // seed row was read in an earlier level (it can meet nothing else).  CL: terminal
+        // entries also of requests this level completes and closes (the side expanded
+        // alone, only closure rows pending on it, the other side's seed row read): the
+        // other side inserts nothing more for them
         n_levels++;
         if (do_f) {
-            const LiteLevel L{open & bc, ~tpend, 0};
-            acc_or[0] = acc_deg[0] = 0;
-            lite_level<SH, 0>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0]);
+            const uint32_t tl = CL && !do_b ? open & ~nc_f & ~tpend : 0u;
+            const LiteLevel L{open & bc, ~tpend, 0, (open & bc) | tl};
+            acc_or[0] = acc_deg[0] = nc_acc[0] = 0;
+            lite_level<SH, 0, CL>(S, g, frec, L, open, edges, acc_or[0], acc_deg[0], &nc_acc[0]);
         }
         if (do_b) {
-            const LiteLevel L{open & fc, ~rpend, 0};
-            acc_or[1] = acc_deg[1] = 0;
-            lite_level<SH, 1>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1]);
+            const uint32_t tl = CL && !do_f ? open & ~nc_b & ~rpend : 0u;
+            const LiteLevel L{open & fc, ~rpend, 0, (open & fc) | tl};
+            acc_or[1] = acc_deg[1] = nc_acc[1] = 0;
+            lite_level<SH, 1, CL>(S, g, brec, L, open, edges, acc_or[1], acc_deg[1], &nc_acc[1]);
         }
         if (do_f) {
             pf = wave_or_all(acc_or[0]);
             sf = wave_sum_all(acc_deg[0]);
+            if constexpr (CL) nc_f = wave_or_all(nc_acc[0]);
             rpend = 0;
         }
         if (do_b) {
             pb = wave_or_all(acc_or[1]);
             sb = wave_sum_all(acc_deg[1]);
+            if constexpr (CL) nc_b = wave_or_all(nc_acc[1]);
             tpend = 0;
         }
     }
@@ -2326,8 +2393,9 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     }
 }
 
-// plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit)
-template <class SH>
+// plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit); CL:
+// plan "core" (record arrays with closure rows, core_index.hpp)
+template <class SH, bool CL = false>
 __global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, const FRec *brec, const uint32_t *roots,
                                                   const uint32_t *targets, uint64_t n, uint64_t *allowed,
                                                   uint32_t *spill_out, unsigned int *spill_count,
@@ -2340,12 +2408,13 @@ __global__ __launch_bounds__(64) void lite_kernel(DevGraph g, const FRec *frec, 
     bidi_load_rt<SH::U>(unit, units, roots, targets, n, r, t);
     unsigned long long *stamp =
         (stamps && blockIdx.x < 65536 && threadIdx.x == 0) ? stamps + (size_t)blockIdx.x * 16 : nullptr;
-    lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, unit, spill_out, spill_count, stats, stamp);
+    lite_unit<SH, CL>(S, g, frec, brec, CL ? core_load_rows(g, frec, brec, r, t) : bidi_load_rows(g, r, t), allowed,
+                      unit, spill_out, spill_count, stats, stamp);
 }
 
 // plan "lite" first stage over pinned host requests read in place (bidi_host_kernel's
 // prologue: K units per workgroup, requests validated and stored in HBM for the spill stages)
-template <int K, class SH>
+template <int K, class SH, bool CL = false>
 __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
                                                        uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
@@ -2383,7 +2452,8 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        lite_unit<SH>(S, g, frec, brec, bidi_load_rows(g, rk, tk), allowed, unit, spill_out, spill_count, stats);
+        lite_unit<SH, CL>(S, g, frec, brec, CL ? core_load_rows(g, frec, brec, rk, tk) : bidi_load_rows(g, rk, tk),
+                          allowed, unit, spill_out, spill_count, stats);
         __syncthreads();
     }
 }
@@ -3365,6 +3435,26 @@ struct ketogpu_engine {
     bool use_v2 = true;
     bool use_bidi = true;
     bool use_lite = false;     // plan "lite" available (lite_kernel)
+    // plan "core" (lite_kernel<CL>): lite over record arrays of its own with closure rows
+    // (core_index.hpp); KETOGPU_CLOSURE="forward cap,backward cap" (0,0: the core layout
+    // without closure rows)
+    bool use_core = false;
+    const FRec *core_rec[2] = {nullptr, nullptr};
+    uint64_t core_blk[2] = {0, 0};
+    uint32_t core_blk_log[2] = {0, 0}, core_block[2] = {0, 0};  // KETOGPU_CORE_BLOCKS="forward,backward" records
+    uint64_t core_overflow[2] = {0, 0};
+    uint32_t closure_cap[2] = {64, 64};
+    int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
+    uint64_t closure_nodes[2] = {0, 0}, closure_entries[2] = {0, 0};
+    double core_build_ms = 0;
+    DevGraph gcore() const {
+        DevGraph x = g;
+        for (int d = 0; d < 2; d++) {
+            x.blk[d] = core_blk[d];
+            x.blk_log[d] = core_blk_log[d];
+        }
+        return x;
+    }
     bool frec_needed = false;  // forward edge records built (v2, bidi, lite)
     // plan "auto" (default): the first kTrialRuns batches of >= kTrialMin requests run
     // every candidate first stage back to back (each a complete evaluation, in rotating
@@ -3379,7 +3469,7 @@ struct ketogpu_engine {
         bool units = true;    // false: the global path alone (with the hub index)
         int u = 16;           // bidi: requests per first-stage unit
         int wpe = 1;          // bidi: minimum waves per SIMD of the first stage
-        int lite = 0;         // bidi: plan "lite" (lite_kernel)
+        int lite = 0;         // bidi: plan "lite" (lite_kernel); 2: plan "core"
     };
     std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
@@ -3388,7 +3478,7 @@ struct ketogpu_engine {
         int hlog, bt, f, lf;
         int u = 16;   // requests per unit (16, or 8: half the LDS per unit)
         int wpe = 1;  // minimum waves per SIMD asked of the compiler (bidi_kernel WPE)
-        int lite = 0;  // 1: plan "lite" (lite_kernel: per-unit direction, per-direction rings)
+        int lite = 0;  // 1: plan "lite" (lite_kernel: per-unit direction, per-direction rings); 2: plan "core"
         bool operator==(const BidiCfg &o) const {
             return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe &&
                    lite == o.lite;
@@ -3400,6 +3490,19 @@ struct ketogpu_engine {
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
+        if (c.lite == 2) {  // plan core: lite over the core record arrays
+#define KETO_CORE_K(SH)                                                                                       \
+    KLAUNCH((lite_kernel<SH, true>), dim3(grid), dim3(64), pad, stream, gcore(), core_rec[0], core_rec[1], q.roots, \
+            q.targets, q.n, q.allowed, out, out_count, stats, unit0, stp)
+            if (core_shape == 1)
+                KETO_CORE_K(CoreShapeS);
+            else if (core_shape == 2)
+                KETO_CORE_K(CoreShapeM);
+            else
+                KETO_CORE_K(LiteShape);
+#undef KETO_CORE_K
+            return;
+        }
         if (c.lite) {  // persistent spill stages never use the lite shape (parents / in_count unused)
             if (c.u == 32)
                 KLAUNCH((lite_kernel<LiteShape32>), dim3(grid), dim3(64), pad, stream, g, frec, brec, q.roots,
@@ -3697,7 +3800,7 @@ struct ketogpu_engine {
         const char *plan = getenv("KETOGPU_UNITS");
         std::string p = plan ? plan : "auto";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        const bool lite_req = p == "lite" || p == "lite32" || p == "auto";
+        const bool lite_req = p == "lite" || p == "lite32" || p == "core" || p == "auto";
         use_v2 = p == "v2" || p == "bidi" || lite_req;
         // Edge records carry 32-bit row begins.  Plan lite reads only INTERIOR rows through
         // records (ids below Ni come first, so their begins are the smallest) and carries
@@ -3713,6 +3816,11 @@ struct ketogpu_engine {
         };
         // bidi / lite: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_lite = lite_req && use_v2 && !s.has_ambiguous && lite_ok;
+        // plan core: not on writable snapshots (an in-place write would change closures)
+        use_core = (p == "core" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_CORE") == nullptr;
+        if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
+        if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
+        if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
         use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && small_f && small_r;
         if (use_v2 && !small_f) {
             disabled("v2", "forward rows pass 2^32 entries (32-bit record begins)");
@@ -3722,6 +3830,10 @@ struct ketogpu_engine {
             disabled("bidi", "rows pass 2^32 entries (32-bit seed begins)");
         if (lite_req && !s.has_ambiguous && !lite_ok) disabled("lite", "interior rows pass 2^32 entries");
         frec_needed = recs && (use_v2 || use_bidi || use_lite);
+        if (p == "core" && use_core) {  // forced: plan core, no trials
+            use_bidi = true;
+            bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 2};
+        }
         if ((p == "lite" || p == "lite32") && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
             bidi_cfg.lite = 1;
@@ -3748,10 +3860,11 @@ struct ketogpu_engine {
                 if (!bc) candidates.push_back({true, 9, 64, 64, 7, 0});
             }
             if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
+            if (use_core) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 2});  // plan "core"
             if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
             // batches below the trial size run lite until the trials have picked a plan
             // (round 3: lite 0.284 vs bidi 0.367 ms per 10^6 config #2 requests)
-            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 1};
+            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, use_core ? 2 : 1};
             use_bidi = use_bidi || use_lite;
         }
         if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
@@ -3818,6 +3931,7 @@ struct ketogpu_engine {
             }
             brec = up(rec);
         }
+        if (use_core) build_core(s);
 
         size_t free_b = 0, total_b = 0;
         HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -3859,6 +3973,53 @@ struct ketogpu_engine {
         owned.push_back(d_bad);
         HIP_CHECK(hipStreamSynchronize(stream));
         build_hubs(s);
+    }
+
+    // plan core's record arrays (core_index.hpp): built on the host, uploaded; the plan is
+    // dropped (with a message) when they do not fit a quarter of free HBM or pass 2^32
+    // core records
+    void build_core(const Snapshot &s) {
+        CoreIndex ci;
+        try {
+            build_core_index(s, closure_cap, core_block, ci);
+        } catch (const Error &e) {
+            fprintf(stderr, "[ketogpu] plan core disabled: %s\n", e.what());
+            drop_core();
+            return;
+        }
+        size_t free_b = 0, total_b = 0;
+        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        const uint64_t bytes = (ci.rec[0].size() + ci.rec[1].size()) * sizeof(CoreRec);
+        if (bytes > free_b / 4) {
+            fprintf(stderr, "[ketogpu] plan core disabled: %llu bytes of records, %llu free\n",
+                    (unsigned long long)bytes, (unsigned long long)free_b);
+            drop_core();
+            return;
+        }
+        for (int d = 0; d < 2; d++) {
+            CoreRec *p = dupload(ci.rec[d]);
+            owned.push_back(p);
+            core_rec[d] = reinterpret_cast<const FRec *>(p);
+            core_blk[d] = ci.block_base[d];
+            core_blk_log[d] = ci.block_log[d];
+            core_overflow[d] = ci.overflow_rows[d];
+            closure_nodes[d] = ci.closure_nodes[d];
+            closure_entries[d] = ci.closure_entries[d];
+        }
+        core_build_ms = ci.build_ms;
+        if (cascade_log)
+            fprintf(stderr, "[core] closure rows: forward %llu nodes / %llu entries, backward %llu / %llu (caps %u, %u); "
+                            "blocks of %u / %u records, %llu / %llu rows in overflow; %.2f GB; built in %.1f ms\n",
+                    (unsigned long long)closure_nodes[0], (unsigned long long)closure_entries[0],
+                    (unsigned long long)closure_nodes[1], (unsigned long long)closure_entries[1], closure_cap[0],
+                    closure_cap[1], 1u << core_blk_log[0], 1u << core_blk_log[1], (unsigned long long)core_overflow[0],
+                    (unsigned long long)core_overflow[1], (double)bytes / 1e9, core_build_ms);
+    }
+    void drop_core() {
+        use_core = false;
+        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite == 2; }),
+                         candidates.end());
+        if (bidi_cfg.lite == 2) bidi_cfg.lite = 1;
     }
 
     // Hub index.  Hubs are the interior nodes with the most interior successors; a search
@@ -4173,7 +4334,19 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite && bidi_cfg.u == 32)                                                             \
+        if (bidi_cfg.lite == 2 && core_shape == 1)                                                         \
+            KLAUNCH((lite_host_kernel<K, CoreShapeS, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
+                    0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite == 2 && core_shape == 2)                                                    \
+            KLAUNCH((lite_host_kernel<K, CoreShapeM, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
+                    0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite == 2)                                                                       \
+            KLAUNCH((lite_host_kernel<K, LiteShape, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
+                    0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite && bidi_cfg.u == 32)                                                        \
             KLAUNCH((lite_host_kernel<K, LiteShape32>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, \
                     stream, g, frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n,      \
                     q.allowed, list[0], &spill_count[0], st.stats, d_bad);                                 \
@@ -4473,12 +4646,19 @@ struct ketogpu_engine {
         Batch q = qq.batch();
         ketogpu_run_stats rs{};
         rs.checks = q.n;
-        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? (bidi_cfg.lite ? 5 : 1) : use_v2 ? 2 : 4;
+        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? (bidi_cfg.lite == 2 ? 6 : bidi_cfg.lite ? 5 : 1) : use_v2 ? 2 : 4;
         rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
         rs.plan_unit = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.u : 0;
         rs.hubs = n_hubs;
         rs.hub_words = hub_words;
         rs.hub_build_ms = hub_build_ms;
+        rs.closure_cap_f = use_core ? closure_cap[0] : 0;
+        rs.closure_cap_b = use_core ? closure_cap[1] : 0;
+        rs.closure_nodes_f = closure_nodes[0];
+        rs.closure_nodes_b = closure_nodes[1];
+        rs.closure_entries_f = closure_entries[0];
+        rs.closure_entries_b = closure_entries[1];
+        rs.core_build_ms = core_build_ms;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();

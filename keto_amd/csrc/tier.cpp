@@ -409,6 +409,12 @@ struct TierDevice : TierSteps {
         } catch (const Error &e) {
             err = std::string(what) + ": " + e.what();
             return e.code;
+        } catch (const std::bad_alloc &) {  // host allocations of a step (lists, overflow)
+            err = std::string(what) + ": out of host memory";
+            return KETOGPU_ENOMEM;
+        } catch (const std::exception &e) {
+            err = std::string(what) + ": " + e.what();
+            return KETOGPU_EDEVICE;
         }
     }
 
@@ -723,6 +729,20 @@ struct ketogpu_tier {
         if (total) fallback(roots, targets, overflow, over, total, bits);
     }
 
+    // the largest status code of every rank (0: all succeeded)
+    int agree(int rc) {
+        if (!comm || world == 1) return rc;
+        HostColl hc(comm);
+        st.collectives++;
+        return hc.agree(rc);
+    }
+    void drop_fallback() {
+        if (pe) ketogpu_part_engine_free(pe);
+        if (part) ketogpu_part_free(part);
+        pe = nullptr;
+        part = nullptr;
+    }
+
     // requests no LDS table held: every rank's, gathered, answered by the per-level engine
     // (which takes the same requests on every rank), each rank keeping its own answers
     void fallback(const uint32_t *roots, const uint32_t *targets, const std::vector<uint32_t> &mine,
@@ -756,10 +776,23 @@ struct ketogpu_tier {
             po.record_capacity = 1 << 22;
             po.max_words_per_round = 256;
             po.state_budget_bytes = fallback_bytes;
-            if (const int rc = ketogpu_part_new(shard, &po, &part)) throw Error(rc, ketogpu_last_error());
+            // each construction's status is agreed before the next collective: a rank whose
+            // device state does not fit (free HBM differs between ranks) fails every rank
+            // alike instead of leaving its peers in the engine's init gather
+            int rc = ketogpu_part_new(shard, &po, &part);
+            std::string why = rc ? std::string(ketogpu_last_error()) : std::string();
+            if (const int a = agree(rc)) {
+                drop_fallback();
+                throw Error(a, rc == a ? why : "two-tier: the fallback engine failed on another rank");
+            }
             ketogpu_part_engine_opts eo{};
             eo.direction = KETOGPU_PART_AUTO;
-            if (const int rc = ketogpu_part_engine_new(part, chandle, &eo, &pe)) throw Error(rc, ketogpu_last_error());
+            rc = ketogpu_part_engine_new(part, chandle, &eo, &pe);
+            why = rc ? std::string(ketogpu_last_error()) : std::string();
+            if (const int a = agree(rc)) {
+                drop_fallback();
+                throw Error(a, rc == a ? why : "two-tier: the fallback engine failed on another rank");
+            }
         }
         std::vector<uint64_t> ans((total + 63) / 64, 0);
         if (const int rc = ketogpu_part_check_ids(pe, r.data(), t.data(), total, ans.data()))

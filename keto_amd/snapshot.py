@@ -183,6 +183,28 @@ class Snapshot:
         rc = col(v.rev_col, int(ro[-1]))
         return {"N": n, "Nx": nx, "Ni": v.num_interior, "fint_off": fo, "fint_col": fc, "rev_off": ro, "rev_col": rc}
 
+    def core_index(self, closure_cap=(64, 64), block=(0, 0)):
+        """plan core's record arrays as the engine builds them (ketogpu_core_index_build):
+        per direction a dict with `records` (n x 4 uint32: node, deg, begin, pad),
+        block_base, block_records and the closure / overflow counts"""
+        cap = (C.c_uint32 * 2)(*closure_cap)
+        blk = (C.c_uint32 * 2)(*block)
+        h = C.c_void_p()
+        L.check(self.L.ketogpu_core_index_build(self.h, cap, blk, C.byref(h)))
+        try:
+            out = []
+            for d in (0, 1):
+                v = L.CoreRecords()
+                L.check(self.L.ketogpu_core_index_view(h, d, C.byref(v)))
+                rec = (np.ctypeslib.as_array(v.records, (v.num_records * 4,)).reshape(-1, 4).copy()
+                       if v.num_records else np.zeros((0, 4), dtype=np.uint32))
+                out.append({"records": rec, "block_base": v.block_base, "block_records": v.block_records,
+                            "overflow_rows": v.overflow_rows, "closure_nodes": v.closure_nodes,
+                            "closure_entries": v.closure_entries})
+            return out
+        finally:
+            self.L.ketogpu_core_index_free(h)
+
     def resolve(self, namespace, obj, relation, subject):
         """-> (root, target) node ids (KETOGPU_NODE_NONE when absent)"""
         req = L.CheckRequest(L.b(namespace), L.b(obj), L.b(relation), subject_struct(subject))

@@ -1,0 +1,158 @@
+"""Plan core's record arrays (keto_amd/csrc/core_index.hpp), built on the host as the
+engine builds them, against an independent decoding in Python: every node block holds
+exactly the node's seed row (fint(v) forward, rev(v) backward, in row order), every record
+names the node's expansion row, a closure row is exactly the node's closure (breadth-first
+search here over the snapshot's rows), and a node keeps its one-hop row only when its
+closure has more nodes than the cap.  CPU only (no device calls)."""
+import numpy as np
+import pytest
+
+from keto_amd.snapshot import Snapshot
+from tests import randgraph
+
+NONE = 0xFFFFFFFF
+TERMINAL, CLOSURE = 0x80000000, 0x40000000
+
+
+def interior_rows(g, d):
+    """one-hop interior rows per interior node: forward fint(v), backward the interior
+    predecessors (rev(v) below Ni)"""
+    Ni = g["Ni"]
+    out = []
+    for v in range(Ni):
+        if d == 0:
+            row = g["fint_col"][g["fint_off"][v]:g["fint_off"][v + 1]]
+        else:
+            row = g["rev_col"][g["rev_off"][v]:g["rev_off"][v + 1]]
+            row = row[row < Ni]
+        out.append([int(x) for x in row])
+    return out
+
+
+def closure(rows, v, limit):
+    """nodes reachable from v through >= 1 step, without v; None beyond `limit` nodes"""
+    seen, order, queue = {v}, [], [v]
+    while queue:
+        x = queue.pop()
+        for y in rows[x]:
+            if y not in seen:
+                seen.add(y)
+                order.append(y)
+                if len(order) > limit:
+                    return None
+                queue.append(y)
+    return sorted(order)
+
+
+def check_index(snap, cap, block=(0, 0)):
+    g = snap.graph()
+    ci = snap.core_index(cap, block)
+    Ni = g["Ni"]
+    for d in (0, 1):
+        c = ci[d]
+        R = c["records"].astype(np.uint64)
+        rows = interior_rows(g, d)
+        B = c["block_records"]
+        assert B in (4, 8, 16, 32) and c["block_base"] % B == 0
+        if block[d]:
+            assert B == block[d]
+        n_clo = n_ent = 0
+        expect = {}  # node -> expected record fields (deg/begin checked through the row they name)
+
+        def check_rec(rec):
+            u = int(rec[0])
+            deg, begin, pad = int(rec[1]), int(rec[2]), int(rec[3])
+            if u >= Ni:
+                assert (deg, begin, pad) == (0, 0, 0), rec
+                return
+            if u in expect:
+                assert expect[u] == (deg, begin, pad)
+                return
+            expect[u] = (deg, begin, pad)
+            full = closure(rows, u, max(cap[d], 0))
+            if pad & CLOSURE:
+                got = R[begin:begin + deg]
+                assert all(int(x[3]) == TERMINAL and int(x[1]) == 0 and int(x[2]) == 0 for x in got)
+                assert [int(x[0]) for x in got] == full, (d, u)
+                assert 0 < deg <= cap[d]
+            else:
+                assert pad == 0
+                got = [int(x) for x in R[begin:begin + deg, 0]]
+                assert got == rows[u], (d, u)
+                # a one-hop row only when the closure is empty or over the cap
+                assert full is None or not full or cap[d] == 0, (d, u, full)
+
+        nodes = g["Nx"] if d == 0 else g["N"]
+        off, col = (g["fint_off"], g["fint_col"]) if d == 0 else (g["rev_off"], g["rev_col"])
+        over = 0
+        for v in range(nodes):
+            h = R[c["block_base"] + v * B]
+            n, first = int(h[0]), int(h[1]) | (int(h[2]) << 32)
+            want = [int(x) for x in col[off[v]:off[v + 1]]]
+            assert n == len(want)
+            if n < B:
+                assert first == c["block_base"] + v * B + 1
+                tail = R[first + n:c["block_base"] + (v + 1) * B]
+                assert all(int(x[0]) == NONE for x in tail)
+            else:
+                over += 1
+                assert first >= c["block_base"] + nodes * B
+            got = R[first:first + n]
+            assert [int(x[0]) for x in got] == want, (d, v)
+            for rec in got:
+                check_rec(rec)
+        assert over == c["overflow_rows"]
+        for v in range(Ni):  # every core and closure row, also of nodes no seed row names
+            for rec in R[expect[v][1]:expect[v][1] + expect[v][0]] if v in expect else []:
+                if not int(rec[3]) & TERMINAL:
+                    check_rec(rec)
+        for u, (deg, begin, pad) in expect.items():
+            if pad & CLOSURE:
+                n_clo += 1
+                n_ent += deg
+        assert n_clo <= c["closure_nodes"] and n_ent <= c["closure_entries"]
+    return ci
+
+
+@pytest.mark.parametrize("seed,poison,collide", [(71, False, False), (72, True, False), (73, True, True)])
+@pytest.mark.parametrize("cap", [(64, 64), (3, 3), (0, 0), (0, 8)])
+def test_random_tables(seed, poison, collide, cap):
+    namespaces, rows = randgraph.make_graph(seed, n_rows=700, n_obj=40, n_users=40, poison=poison, collide=collide,
+                                            empty_ns=True)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=5, sort=True)
+    check_index(snap, cap)
+
+
+@pytest.mark.parametrize("block", [(4, 4), (8, 32), (32, 16)])
+def test_block_sizes(block):
+    namespaces, rows = randgraph.make_graph(74, n_rows=900, n_obj=30, n_users=60)
+    snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    ci = check_index(snap, (64, 64), block)
+    assert ci[0]["block_records"] == block[0] and ci[1]["block_records"] == block[1]
+
+
+@pytest.mark.parametrize("kind", ["rbac", "folders", "social"])
+def test_synthetic_configs(kind):
+    """small BASELINE-shaped graphs: RBAC's backward closures (ancestor groups) and the
+    folders' forward closures (parent chains) are all within the default cap"""
+    from keto_amd import synth
+    w = {"rbac": lambda: synth.rbac(users=3000, groups=300, docs=600, tuples=20000, checks=10, seed=5),
+         "folders": lambda: synth.folders(users=2000, groups=60, folders=1500, tuples=20000, checks=10, seed=5),
+         "social": lambda: synth.social(users=3000, groups=600, tuples=20000, checks=10, seed=5)}[kind]()
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    ci = check_index(snap, (64, 64))
+    if kind == "rbac":
+        assert ci[1]["closure_nodes"] > 0.9 * snap.graph()["Ni"]
+    if kind == "folders":
+        assert ci[0]["closure_nodes"] > 0.9 * snap.graph()["Ni"]
+
+
+def test_cycles():
+    """a cycle a -> b -> c -> a and a tail c -> d: the closure of a node on the cycle
+    holds the other cycle nodes and d, never the node itself"""
+    rows = [(1, "a", "m", None, 1, "b", "m"), (1, "b", "m", None, 1, "c", "m"), (1, "c", "m", None, 1, "a", "m"),
+            (1, "c", "m", None, 1, "d", "m"), (1, "d", "m", "u1", None, None, None),
+            (1, "a", "m", "u2", None, None, None)]
+    snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
+    check_index(snap, (64, 64))
+    check_index(snap, (2, 2))

@@ -47,16 +47,23 @@ def test_nil_subject_is_bad_request():
         eng.SubjectIsAllowed(rt.InternalRelationTuple("n", "o", "r", None))
 
 
-@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift", "lite32"])
+@pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift", "lite32", "core", "core-small", "core-none"])
 def unit_plan(request, monkeypatch):
     """first LDS pass of engines created while active: the default bidirectional units
     (one-wave, 512-slot tables), bidi with the wide 2048-slot table, forward-only unit2, or
     plan lite (per-unit direction) — also with every row begin carried past 2^32 through
-    its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT) — and lite with 32-request units"""
+    its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT) — lite with 32-request units, and plan core
+    (lite over its own record arrays with closure rows, core_index.hpp) with the default
+    caps, with caps of 3 (most closures dropped, mixed closure and one-hop rows) and with
+    no closure rows at all"""
     if request.param == "v2":
         monkeypatch.setenv("KETOGPU_UNITS", "v2")
     elif request.param == "lite32":
         monkeypatch.setenv("KETOGPU_UNITS", "lite32")
+    elif request.param.startswith("core"):
+        monkeypatch.setenv("KETOGPU_UNITS", "core")
+        if request.param != "core":
+            monkeypatch.setenv("KETOGPU_CLOSURE", "3,3" if request.param == "core-small" else "0,0")
     elif request.param.startswith("lite"):
         monkeypatch.setenv("KETOGPU_UNITS", "lite")
         if request.param == "lite-shift":
@@ -162,7 +169,7 @@ def test_hub_index_default_on_power_law(monkeypatch):
     roots, targets = w.resolve(snap)
     want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(
         w.requests(range(len(roots))), nthreads=8)
-    for plan in ("bidi", "v2", "lite", "auto"):
+    for plan in ("bidi", "v2", "lite", "core", "auto"):
         monkeypatch.setenv("KETOGPU_UNITS", plan)
         eng = check.Engine(snap)
         for _ in range(3 if plan == "auto" else 1):
@@ -330,12 +337,12 @@ def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
         w.requests(range(len(roots))), nthreads=8)
     eng = check.Engine(snap)
     np.testing.assert_array_equal(eng.check_ids(roots[:1000], targets[:1000]), want[:1000])
-    assert eng.last_stats()["plan"] == 5  # below the trial size: lite
+    assert eng.last_stats()["plan"] == 6  # below the trial size: core
     plans = set()
     for _ in range(4):
         np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
         plans.add(eng.last_stats()["plan"])
-    assert plans <= {0, 1, 2, 5}  # global path (with the hub index), bidi, unit2, lite
+    assert plans <= {0, 1, 2, 5, 6}  # global path (with the hub index), bidi, unit2, lite, core
     kept = eng.last_stats()["plan"]
     np.testing.assert_array_equal(eng.check_ids(roots[:5000], targets[:5000]), want[:5000])
     assert eng.last_stats()["plan"] == kept

@@ -24,6 +24,9 @@ from collections import defaultdict
 FAMILIES = [
     # host batches with pinned requests: the first stage reading its requests in place
     ("bidi_host_kernel (host batches)", r"bidi_host_kernel"),
+    # plan core: lite over the core arrays with closure rows (template argument CL = true)
+    ("core lite_host_kernel (host batches)", r"lite_host_kernel<.*, true>"),
+    ("core lite_kernel", r"\blite_kernel<.*, true>"),
     ("lite_host_kernel (host batches)", r"lite_host_kernel"),
     ("lite_kernel", r"\blite_kernel"),
     # the pipelined host-to-host first stage is its own instantiation (last template
