@@ -196,6 +196,19 @@ def main():
     t_pageable = time.perf_counter() - c0
     assert np.array_equal(got_pageable, allowed)
 
+    # the timed step's own first-stage kernel (the host-batch instantiation reading its
+    # requests from pinned memory): the same steps again with a timing event between the
+    # call's kernels, hipEvents on the engine's stream (not `value`: the events cost idle
+    # GPU time between the launches)
+    host_runs = []
+    if procs_gpus == 1:
+        eng0.set_events(True)
+        for _ in range(a.steps):
+            step()
+            host_runs.append(eng0.last_stats())
+        eng0.set_events(False)
+        assert np.array_equal(check.unpack_bits(out.array.copy(), n), allowed)
+
     # HBM-resident batch on one GPU: the traversal kernels alone (roofline source)
     b0, e0 = (check.MultiEngine.ranges(n, procs_gpus)[0] if procs_gpus > 1 else (0, n))
     q = eng0.upload(roots[b0:e0], targets[b0:e0])
@@ -215,7 +228,13 @@ def main():
         # per kernel family: algorithmic bytes (engine counters) / summed hipEvent time over
         # the timed HBM-resident runs
         plan = L.RunStats.PLANS.get(st["plan"], "unit")  # KETOGPU_UNITS=auto: the plan the engine kept
-        main = {"bidi": "bidi_kernel<16>", "lite": "lite_kernel", "v2": "unit2_kernel<16>"}.get(plan, "unit_kernel<16>")
+        # kernel families as tools/pmc_traffic.py names them (the PMC summary's keys)
+        main, host_main = {
+            "bidi": ("bidi_kernel<16>", "bidi_host_kernel (host batches)"),
+            "lite": ("lite_kernel", "lite_host_kernel (host batches)"),
+            "core": ("core lite_kernel", "core lite_host_kernel (host batches)"),
+            "label": ("label_kernel", "label_host_kernel (host batches)"),
+            "v2": ("unit2_kernel<16>", "unit2_kernel<16>")}.get(plan, ("unit_kernel<16>", "unit_kernel<16>"))
         tot = lambda k: sum(r[k] for r in runs)
         fam = {
             main: (tot("main_bytes"), tot("main_ms"), sum(1 for r in runs if r["main_ms"] > 0)),
@@ -228,9 +247,7 @@ def main():
         }
         gbps = {k: (bb / (ms * 1e-3) / 1e9 if ms > 0 else 0.0) for k, (bb, ms, _) in fam.items()}
         dominant = max(fam, key=lambda k: fam[k][1])
-        b_dom, ms_dom, n_launch = fam[dominant]
-        achieved = gbps[dominant]
-        traffic, traffic_note = None, "no PMC summary"
+        traffic_doc, traffic_note = {}, "no PMC summary"
         if os.path.exists(a.traffic):
             try:
                 tr = json.load(open(a.traffic))
@@ -241,17 +258,34 @@ def main():
                     traffic_note = (f"stale: {os.path.relpath(a.traffic, ROOT)} was profiled at kernel sources "
                                     f"{tr.get('source_hash')}, HEAD is {kernel_source_hash()}")
                 else:
-                    traffic = tr.get("kernels", {}).get(dominant, {}).get("hbm_bytes_per_launch")
+                    traffic_doc = tr.get("kernels", {})
                     traffic_note = f"{os.path.relpath(a.traffic, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
             except (OSError, ValueError):
                 traffic_note = "unreadable PMC summary"
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_note,
-                "kernel": dominant,
-                "bytes_per_launch": int(b_dom / max(n_launch, 1)), "ms_per_launch": round(ms_dom / max(n_launch, 1), 4),
-                "requests_per_launch": int(e0 - b0),
-                "kernels": {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": bb, "launches": nl}
-                            for k, (bb, ms, nl) in fam.items() if ms > 0}}
+
+        def roofline(name, b_k, ms_k, n_launch, requests, measured):
+            ach = b_k / (ms_k * 1e-3) / 1e9 if ms_k > 0 else 0.0
+            return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4),
+                    "traffic": traffic_doc.get(name, {}).get("hbm_bytes_per_launch"), "traffic_source": traffic_note,
+                    "kernel": name, "bytes_per_launch": int(b_k / max(n_launch, 1)),
+                    "ms_per_launch": round(ms_k / max(n_launch, 1), 4), "requests_per_launch": int(requests),
+                    "measured": measured}
+
+        # the line's roofline: the timed step's first stage (host batches); the HBM-resident
+        # launch of the same plan beside it
+        hbm_roof = roofline(dominant, *fam[dominant], e0 - b0,
+                            "hipEvents around the first stage of the HBM-resident runs (ketogpu_queries_run)")
+        if host_runs and all(r["main_ms"] > 0 for r in host_runs):
+            roof = roofline(host_main, sum(r["main_bytes"] for r in host_runs), sum(r["main_ms"] for r in host_runs),
+                            len(host_runs), n, "hipEvents on the engine's stream around the first stage of the "
+                                               "host-to-host step (ketogpu_engine_set_events), same steps re-run")
+            roof["hbm_resident"] = hbm_roof
+        else:
+            roof = hbm_roof
+        roof["kernels"] = {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": bb, "launches": nl}
+                           for k, (bb, ms, nl) in fam.items() if ms > 0}
+        achieved = roof["achieved"]
         stream = stream_copy_gbps(local)
         roof["stream_copy_GBps"] = round(stream, 1)  # measured device-copy bandwidth
         roof["frac_of_stream"] = round(achieved / stream, 4) if stream > 0 else None
@@ -286,10 +320,13 @@ def main():
             "hbm_resident_checks_per_s": round((e0 - b0) * a.steps / dt_res, 1),
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
             "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)"
-                            if plan in ("bidi", "lite") else ""),
+                            if plan in ("bidi", "lite", "core") else
+                            f" (mode {'BF'[st['label_mode']]}, {st['label_coverage']:.4f} of the label nodes labelled)"
+                            if plan == "label" else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
-                                          "hubs", "hub_build_ms")},
+                                          "hubs", "hub_build_ms", "closure_nodes_f", "closure_nodes_b",
+                                          "core_build_ms", "label_mode", "label_coverage", "label_build_ms")},
             "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(e0 - b0, 1), 2),
             "allowed_fraction": round(float(allowed.mean()), 4),
             "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2)},

@@ -238,6 +238,28 @@ int ketogpu_core_index_build(const ketogpu_snapshot *s, const uint32_t closure_c
 int ketogpu_core_index_view(const ketogpu_core_index *c, int direction, ketogpu_core_records *out);
 void ketogpu_core_index_free(ketogpu_core_index *c);
 
+/* Plan "label"'s closure labels (keto_amd/csrc/labels.hpp) as an engine builds them, for
+ * tools and tests.  mode 0 (B): S blocks per node t = rev(t) + the backward closures of its
+ * interior entries, P blocks per expandable r = {r} + fint(r); mode 1 (F): S blocks per
+ * expandable r = {r} + fint(r) + their forward closures, P blocks per node t = rev(t);
+ * mode -1: the better-covered one (view mode -1 when neither labels half its nodes).
+ * allowed(r, t) <=> the request's P list and S list share a node.  S blocks: 64 u32
+ * [count (0xFFFFFFFF: no label), entries ascending, 0xFFFFFFFF padding]; P blocks: pb u32
+ * [count, overflow start / 16, entries...], entries past pb - 2 at words overflow*16... */
+typedef struct ketogpu_label_index ketogpu_label_index;
+typedef struct {
+    int32_t mode;
+    uint32_t p_block_words;
+    const uint32_t *p_words, *s_words;
+    uint64_t num_p_words, num_s_words;
+    uint64_t p_nodes, s_nodes, labelled, nonempty;
+    double coverage_b, coverage_f; /* sampled labelled shares of both modes */
+} ketogpu_label_view;
+int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode,
+                              ketogpu_label_index **out);
+int ketogpu_label_index_view(const ketogpu_label_index *l, ketogpu_label_view *out);
+void ketogpu_label_index_free(ketogpu_label_index *l);
+
 /* ------------------------------------------------------------------- check */
 /* relationtuple.Subject: SubjectID{ID} or SubjectSet{Namespace, Object, Relation}
  * (internal/relationtuple/definitions.go:39-41,103-118) */
@@ -391,7 +413,7 @@ typedef struct {
     double main_ms;             /* its device time (hipEvent)                     */
     int32_t plan;               /* first stage of the run: 0 global path only, 1 bidi,
                                  * 2 forward unit2 (v2), 3 one-wave units, 4 unit v1,
-                                 * 5 lite, 6 core (lite with closure rows).
+                                 * 5 lite, 6 core (lite with closure rows), 7 label.
                                  * KETOGPU_UNITS=auto (default) tries bidi (128- and 64-
                                  * entry pending lists), v2 and (with hubs) the global path
                                  * alone on the first two batches of
@@ -410,8 +432,18 @@ typedef struct {
     uint64_t closure_nodes_f, closure_nodes_b;      /* nodes with a closure row          */
     uint64_t closure_entries_f, closure_entries_b;  /* records in closure rows           */
     double core_build_ms;       /* one-time build of the core arrays at engine creation */
+    /* plan 7 "label" (closure labels over plan core's arrays: one intersection of two short
+     * lists per request, plan core's traversal for units with an unlabelled request) */
+    int32_t label_mode;         /* 0 backward labels, 1 forward labels, -1 off         */
+    double label_coverage;      /* labelled share of the label nodes with a non-empty row */
+    double label_build_ms;
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
+/* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory) record a
+ * timing event between the call's kernels, so last_stats' main_ms is the first stage's own
+ * device time (each event pair costs a few microseconds of idle GPU between the launches);
+ * 0 (default): one event pair around the whole call (KETOGPU_EVENTS=all sets 1 at creation) */
+int ketogpu_engine_set_events(ketogpu_engine *e, int every_kernel);
 
 /* Upload the device rows patched by ketogpu_snapshot_write since the engine's last sync
  * (every check entry point also does this first).  ms: host time of the sync (may be NULL);

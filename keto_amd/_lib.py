@@ -102,9 +102,10 @@ class RunStats(C.Structure):
         ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double),
         ("plan_unit", C.c_uint32), ("closure_cap_f", C.c_uint32), ("closure_cap_b", C.c_uint32),
         ("closure_nodes_f", C.c_uint64), ("closure_nodes_b", C.c_uint64), ("closure_entries_f", C.c_uint64),
-        ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double)]
+        ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double), ("label_mode", C.c_int32),
+        ("label_coverage", C.c_double), ("label_build_ms", C.c_double)]
 
-    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core"}
+    PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core", 7: "label"}
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -143,6 +144,13 @@ class CoreRecords(C.Structure):
     _fields_ = [("records", C.POINTER(C.c_uint32)), ("num_records", C.c_uint64), ("block_base", C.c_uint64),
                 ("block_records", C.c_uint32), ("overflow_rows", C.c_uint64), ("closure_nodes", C.c_uint64),
                 ("closure_entries", C.c_uint64)]
+
+
+class LabelView(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("p_block_words", C.c_uint32), ("p_words", C.POINTER(C.c_uint32)),
+                ("s_words", C.POINTER(C.c_uint32)), ("num_p_words", C.c_uint64), ("num_s_words", C.c_uint64),
+                ("p_nodes", C.c_uint64), ("s_nodes", C.c_uint64), ("labelled", C.c_uint64), ("nonempty", C.c_uint64),
+                ("coverage_b", C.c_double), ("coverage_f", C.c_double)]
 
 
 class TreeNode(C.Structure):
@@ -291,6 +299,9 @@ SIGNATURES = {
     "ketogpu_core_index_build": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]),
     "ketogpu_core_index_view": (C.c_int, [vp, C.c_int, C.POINTER(CoreRecords)]),
     "ketogpu_core_index_free": (None, [vp]),
+    "ketogpu_label_index_build": (C.c_int, [vp, C.POINTER(u32), C.c_int, C.POINTER(vp)]),
+    "ketogpu_label_index_view": (C.c_int, [vp, C.POINTER(LabelView)]),
+    "ketogpu_label_index_free": (None, [vp]),
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),
     "ketogpu_snapshot_apply": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(vp)]),
     "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),
@@ -303,6 +314,7 @@ SIGNATURES = {
     "ketogpu_resolve_batch": (C.c_int, [vp, C.POINTER(RequestBatch), vp, vp, vp]),
     "ketogpu_engine_new": (C.c_int, [vp, C.POINTER(EngineOpts), C.POINTER(vp)]),
     "ketogpu_engine_free": (None, [vp]),
+    "ketogpu_engine_set_events": (C.c_int, [vp, C.c_int]),
     "ketogpu_check": (C.c_int, [vp, C.POINTER(CheckRequest), sz, vp, vp]),
     "ketogpu_check_ids": (C.c_int, [vp, vp, vp, sz, vp, vp]),
     "ketogpu_queries_upload": (C.c_int, [vp, vp, vp, sz, C.POINTER(vp)]),

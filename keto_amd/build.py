@@ -14,8 +14,8 @@ SYNTH_LIB = os.path.join(HERE, "libketosynth.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
 
-SOURCES = ["snapshot.cpp", "snapshot_write.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip", "comm.cpp", "part_round.cpp", "tier.cpp", "core_index.cpp"]
-HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", "part_round.hpp", "tier.hpp", "core_index.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
+SOURCES = ["snapshot.cpp", "snapshot_write.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip", "comm.cpp", "part_round.cpp", "tier.cpp", "core_index.cpp", "labels.cpp"]
+HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", "part_round.hpp", "tier.hpp", "core_index.hpp", "labels.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
 
 
 def kernel_source_hash():
@@ -24,7 +24,7 @@ def kernel_source_hash():
     hash still matches, so a stale figure never passes as current."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("device_engine.hip", "device_util.hpp", "core_index.hpp", "core_index.cpp"):
+    for f in ("device_engine.hip", "device_util.hpp", "core_index.hpp", "core_index.cpp", "labels.hpp", "labels.cpp"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

@@ -122,6 +122,11 @@ class Engine:
         L.check(self.L.ketogpu_engine_last_stats(self.h, C.byref(st)))
         return st.as_dict()
 
+    def set_events(self, every_kernel):
+        """host-to-host batches: a timing event between the call's kernels (main_ms = the
+        first stage's own time) or only around the call (default)"""
+        L.check(self.L.ketogpu_engine_set_events(self.h, 1 if every_kernel else 0))
+
 
 class PinnedBuffer:
     """pinned host memory (ketogpu_host_alloc) viewed as a numpy array: a request batch

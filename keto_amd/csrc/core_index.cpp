@@ -9,30 +9,13 @@
 
 namespace ketogpu {
 
-namespace {
-
 int build_threads() {
     if (const char *e = getenv("KETOGPU_BUILD_THREADS")) return std::max(1, atoi(e));
     // the GPU box's job quota is 16 cores (nproc shows the whole machine)
     return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
-template <class F>
-void parallel_chunks(uint64_t n, uint64_t chunk, F &&f) {
-    const int T = build_threads();
-    std::atomic<uint64_t> next{0};
-    auto work = [&](int tid) {
-        for (;;) {
-            const uint64_t b = next.fetch_add(chunk);
-            if (b >= n) return;
-            f(tid, b, std::min(n, b + chunk));
-        }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto &x : th) x.join();
-}
+namespace {
 
 // interior adjacency of one direction: forward fint(v) (interior successors), backward the
 // interior predecessors (the prefix of the sorted rev(v) below Ni)
@@ -224,6 +207,8 @@ void build_core_index(const Snapshot &s, const uint32_t cap_in[2], const uint32_
                 for (uint64_t k = n < blk ? n + 1 : 1; k < blk; k++) bl[k] = CoreRec{NONE, 0, 0, 0};
             }
         });
+        out.clo_len[d] = std::move(clen);
+        out.clo_beg[d] = std::move(kbeg);
         out.block_base[d] = bbase;
         out.block_log[d] = lg;
         out.overflow_rows[d] = nover;

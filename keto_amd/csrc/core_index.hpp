@@ -26,12 +26,36 @@
 // or outside the interior), pad flags below; unused block slots are {NONE, 0, 0, 0}.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
+#include <thread>
 #include <vector>
 
 #include "ketogpu_internal.hpp"
 
 namespace ketogpu {
+
+// host threads of the index builders (KETOGPU_BUILD_THREADS; default at most 16: the GPU
+// box's job quota, whatever nproc shows)
+int build_threads();
+
+// f(thread, begin, end) over [0, n) in chunks, on build_threads() threads
+template <class F>
+void parallel_chunks(uint64_t n, uint64_t chunk, F &&f) {
+    const int T = build_threads();
+    std::atomic<uint64_t> next{0};
+    auto work = [&](int tid) {
+        for (;;) {
+            const uint64_t b = next.fetch_add(chunk);
+            if (b >= n) return;
+            f(tid, b, std::min(n, b + chunk));
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+}
 
 struct CoreRec {
     uint32_t node, deg, begin, pad;
@@ -46,6 +70,8 @@ struct CoreIndex {
     uint64_t overflow_rows[2] = {0, 0};    // seed rows longer than a block holds
     uint64_t closure_nodes[2] = {0, 0};    // interior nodes with a closure row
     uint64_t closure_entries[2] = {0, 0};  // records in closure rows
+    // per interior node: its closure row's length and first record (NONE: none)
+    std::vector<uint32_t> clo_len[2], clo_beg[2];
     double build_ms = 0;
 };
 

@@ -45,6 +45,7 @@
 
 #include "core_index.hpp"
 #include "device_util.hpp"
+#include "labels.hpp"
 #include "tier.hpp"
 #include "ketogpu_internal.hpp"
 
@@ -1821,27 +1822,40 @@ void bidi_kernel(DevGraph g, const FRec *frec, const FRec *brec,
 // K units per workgroup, run one after the other: the requests of all K are read at the
 // start, so only the first unit waits for PCIe (a read from host memory takes several
 // times an HBM miss and every unit would wait for one).
+// The requests of a host-batch workgroup's K 16-request units, read in place from pinned
+// host memory over PCIe, returned on lanes < 16 (unit k: r[k], t[k]); ids outside the
+// snapshot are reported (first_bad) and become NONE; the validated ids go to HBM (dr, dt)
+// for the spill stages.  Every lane reads: a workgroup's 16K roots and 16K targets are two
+// contiguous runs of 64K bytes, so K = 1 / 2 take ONE wave instruction (roots on lanes
+// 0-31, targets on lanes 32-63) and K = 4 two of 256 contiguous bytes each — instead of
+// 2K instructions of 64 bytes (the in-kernel PCIe reads then ran at ~36 GB/s).
 template <int K>
-__global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
-                                                       const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
-                                                       uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
-                                                       unsigned int *spill_count, unsigned long long *stats,
-                                                       unsigned long long *first_bad) {
-    __shared__ BidiShared<16, 9, KETO_F1, 64, 7> S;
-    uint32_t r[K], t[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
-        r[k] = t[k] = KETOGPU_NODE_NONE;
-        if (threadIdx.x < 16 && c < n) {
-            r[k] = hr[c];
-            t[k] = ht[c];
+__device__ __forceinline__ void host_unit_requests(const DevGraph &g, const uint32_t *hr, const uint32_t *ht,
+                                                   uint32_t *dr, uint32_t *dt, uint64_t n,
+                                                   unsigned long long *first_bad, uint32_t (&r)[K], uint32_t (&t)[K]) {
+    static_assert(K == 1 || K == 2 || K == 4, "1, 2 or 4 units per workgroup");
+    const uint32_t lane = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * K * 16;
+    uint32_t vr = KETOGPU_NODE_NONE, vt = KETOGPU_NODE_NONE;
+    if constexpr (K == 4) {
+        if (base + lane < n) {
+            vr = hr[base + lane];
+            vt = ht[base + lane];
         }
+    } else {
+        const uint32_t j = lane & 31;
+        if (j < 16 * K && base + j < n) vr = (lane < 32 ? hr : ht)[base + j];
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * 16 + threadIdx.x;
-        if (threadIdx.x < 16 && c < n) {
+        const int src = 16 * k + (int)(lane & 15);
+        r[k] = (uint32_t)__shfl((int)vr, src, 64);
+        t[k] = (uint32_t)__shfl((int)(K == 4 ? vt : vr), K == 4 ? src : 32 + src, 64);
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t c = base + 16 * k + lane;
+        if (lane < 16 && c < n) {
             if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
                 atomicMin(first_bad, (unsigned long long)c);
                 r[k] = t[k] = KETOGPU_NODE_NONE;
@@ -1850,6 +1864,17 @@ __global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *f
             dt[c] = t[k];
         }
     }
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void bidi_host_kernel(DevGraph g, const FRec *frec, const FRec *brec,
+                                                       const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
+                                                       uint32_t *dt, uint64_t n, uint64_t *allowed, uint32_t *spill_out,
+                                                       unsigned int *spill_count, unsigned long long *stats,
+                                                       unsigned long long *first_bad) {
+    __shared__ BidiShared<16, 9, KETO_F1, 64, 7> S;
+    uint32_t r[K], t[K];
+    host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
     const uint64_t units = (n + 15) / 16;
 #pragma unroll 1
     for (int k = 0; k < K; k++) {
@@ -2029,8 +2054,11 @@ __device__ __forceinline__ void lite_push(SH &S, const LiteLevel &L, bool want, 
     bool app = false;
     if (h >= 0) {
         // one 64-bit atomic: the old word carries the other direction's visited bits, so of
-        // two pushes that complete a meet the later one sees it
-        const unsigned long long old = atomicOr(&S.st[h], (unsigned long long)m << (32 * D));
+        // two pushes that complete a meet the later one sees it.  A push whose every bit is
+        // a lookup only reads the word: lookups happen while the other direction inserts
+        // nothing more for those requests, and nothing reads a lookup's own bits later
+        const unsigned long long old = (m & ~lk) ? atomicOr(&S.st[h], (unsigned long long)m << (32 * D))
+                                                 : __atomic_load_n(&S.st[h], __ATOMIC_RELAXED);
         uint32_t newly = m & ~(uint32_t)(old >> (32 * D)) & SH::MASK;
         const uint32_t meet = newly & (uint32_t)(old >> (32 - 32 * D)) & SH::MASK;
         if (meet) atomicOr(&S.found, meet);
@@ -2422,25 +2450,23 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
                                                        unsigned long long *first_bad) {
     __shared__ SH S;
     uint32_t r[K], t[K];
+    if constexpr (SH::U == 16) {
+        host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
+    } else {  // 32-request units (plan lite32, an A/B plan): lanes < 32 read their own
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * SH::U + threadIdx.x;
-        r[k] = t[k] = KETOGPU_NODE_NONE;
-        if (threadIdx.x < SH::U && c < n) {
-            r[k] = hr[c];
-            t[k] = ht[c];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t c = ((uint64_t)blockIdx.x * K + k) * SH::U + threadIdx.x;
-        if (threadIdx.x < SH::U && c < n) {
-            if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
-                atomicMin(first_bad, (unsigned long long)c);
-                r[k] = t[k] = KETOGPU_NODE_NONE;
+        for (int k = 0; k < K; k++) {
+            const uint64_t c = ((uint64_t)blockIdx.x * K + k) * SH::U + threadIdx.x;
+            r[k] = t[k] = KETOGPU_NODE_NONE;
+            if (threadIdx.x < SH::U && c < n) {
+                r[k] = hr[c];
+                t[k] = ht[c];
+                if ((r[k] != KETOGPU_NODE_NONE && r[k] >= g.Nx) || (t[k] != KETOGPU_NODE_NONE && t[k] >= g.N)) {
+                    atomicMin(first_bad, (unsigned long long)c);
+                    r[k] = t[k] = KETOGPU_NODE_NONE;
+                }
+                dr[c] = r[k];
+                dt[c] = t[k];
             }
-            dr[c] = r[k];
-            dt[c] = t[k];
         }
     }
     const uint64_t units = (n + SH::U - 1) / SH::U;
@@ -2454,6 +2480,156 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
             if (j == k) rk = r[j], tk = t[j];
         lite_unit<SH, CL>(S, g, frec, brec, CL ? core_load_rows(g, frec, brec, rk, tk) : bidi_load_rows(g, rk, tk),
                           allowed, unit, spill_out, spill_count, stats);
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------- plan label
+// Closure labels (labels.hpp): per request one S list (sorted, <= 63 nodes) and one P list;
+// allowed <=> they share a node.  One wave per 16-request unit: four lanes per request
+// copy its S block into LDS (the second half only when the label has more than 31 nodes)
+// and hold its P block in registers; each P entry is looked up in S by a 6-step binary
+// search.  A unit with a request that has no label (or a wildcard root) runs plan core's
+// traversal (lite_unit<CL>) instead, in the same LDS.
+struct LabelGraph {
+    const uint32_t *P, *S;  // P blocks (+ overflow), S blocks (kLabelWords words each)
+    int mode;               // 0 = B (S node t, P node r), 1 = F (S node r, P node t)
+};
+constexpr int kLabelStride = 65;  // LDS words per request's S list (odd: the 16 lists start in different banks)
+union LabelShared {
+    CoreShapeM lite;
+    uint32_t S[16 * kLabelStride];
+};
+
+// number of S entries (words 1..63, ascending, padded with 0xFFFFFFFF) below x, then x found
+__device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+        if (S[pos + step] < x) pos += step;
+    return pos < 63 && S[pos + 1] == x;
+}
+
+template <int PB>
+__device__ __forceinline__ void label_unit(LabelShared &sh, const DevGraph &g, const FRec *cf, const FRec *cb,
+                                           const LabelGraph &L, uint32_t r_lane, uint32_t t_lane, uint64_t *allowed,
+                                           const uint64_t unit, uint32_t *spill_out, unsigned int *spill_count,
+                                           unsigned long long *stats) {
+    static_assert(PB == 16 || PB == 32 || PB == 64, "P blocks of 16, 32 or 64 words");
+    constexpr int PW = PB / 4;  // P words per lane
+    const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
+    const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
+    const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
+    const bool valid = some && r < kDynBase;
+    const uint32_t xs = L.mode == 0 ? t : r, xp = L.mode == 0 ? r : t;
+    uint32_t sw[8], pw[PW];
+#pragma unroll
+    for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < PW; k++) pw[k] = 0u;
+    if (valid) {  // both blocks in flight at once: one dependent HBM read per request
+        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * kLabelWords) + 2 * sub;
+        const uint4 *pb = reinterpret_cast<const uint4 *>(L.P + (uint64_t)xp * PB) + (PW / 4) * sub;
+        const uint4 a = sb[0], b = sb[1];
+        sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
+#pragma unroll
+        for (int k = 0; k < PW / 4; k++) {
+            const uint4 c = pb[k];
+            pw[4 * k] = c.x, pw[4 * k + 1] = c.y, pw[4 * k + 2] = c.z, pw[4 * k + 3] = c.w;
+        }
+    }
+    uint32_t *S = sh.S + q * kLabelStride;
+    // invalid requests (an id NONE): an empty label, so nothing is found
+    if (!valid && sub == 0) sw[0] = some ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) S[8 * sub + k] = sw[k];
+    const uint32_t ns = (uint32_t)__shfl((int)sw[0], (int)(lane & ~3u), 64);  // the label's count
+    const bool big = valid && ns != kNoLabel && ns > 31;
+    if (big) {  // entries 32..63: the block's second line
+        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * kLabelWords + 32) + 2 * sub;
+        const uint4 a = sb[0], b = sb[1];
+        sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) S[32 + 8 * sub + k] = sw[k];
+    // a request without a label (or a wildcard root): the unit runs plan core's traversal
+    if (__ballot(sub == 0 && some && (ns == kNoLabel || !valid))) {
+        __syncthreads();
+        lite_unit<CoreShapeM, true>(sh.lite, g, cf, cb, core_load_rows(g, cf, cb, r_lane, t_lane), allowed, unit,
+                                    spill_out, spill_count, stats);
+        return;
+    }
+    __syncthreads();
+    const uint32_t np = (uint32_t)__shfl((int)pw[0], (int)(lane & ~3u), 64);
+    const uint32_t ovf = (uint32_t)__shfl((int)pw[1], (int)(lane & ~3u), 64);
+    bool hit = false;
+    uint32_t looked = 0;
+#pragma unroll
+    for (int k = 0; k < PW; k++) {
+        const uint32_t w = PW * sub + k;  // the entry of word w is entry w - 2
+        if (w >= 2 && w - 2 < np) {
+            hit |= label_find(S, pw[k]);
+            looked++;
+        }
+    }
+    if (valid && np > (uint32_t)PB - 2)  // the row's entries past its block
+        for (uint32_t k = PB - 2 + sub; k < np; k += 4) {
+            hit |= label_find(S, L.P[(uint64_t)ovf * 16 + (k - (PB - 2))]);
+            looked++;
+        }
+    const uint64_t bits = __ballot(hit);
+    uint64_t rows = valid && sub == 0 ? 2 : 0, ent = looked + (valid && sub == 0 && ns != kNoLabel ? ns : 0);
+#pragma unroll
+    for (int k = 32; k; k >>= 1) {
+        rows += __shfl_down(rows, k, 64);
+        ent += __shfl_down(ent, k, 64);
+    }
+    if (lane == 0) {
+        uint32_t res = 0;
+        for (int j = 0; j < 16; j++) res |= ((bits >> (4 * j)) & 0xFull) ? 1u << j : 0u;
+        const uint64_t c0 = unit * 16;
+        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
+        atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
+        atomicAdd(&stat_slot(stats)[2], (unsigned long long)ent);  // u32 entries: 4 B each
+    }
+}
+
+template <int PB>
+__global__ __launch_bounds__(64) void label_kernel(DevGraph g, const FRec *cf, const FRec *cb, LabelGraph L,
+                                                   const uint32_t *roots, const uint32_t *targets, uint64_t n,
+                                                   uint64_t *allowed, uint32_t *spill_out, unsigned int *spill_count,
+                                                   unsigned long long *stats, uint64_t unit0) {
+    __shared__ LabelShared sh;
+    const uint64_t units = (n + 15) / 16;
+    const uint64_t unit = unit0 + blockIdx.x;
+    uint32_t r, t;
+    bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
+    label_unit<PB>(sh, g, cf, cb, L, r, t, allowed, unit, spill_out, spill_count, stats);
+}
+
+// pinned host requests read in place (lite_host_kernel's prologue)
+template <int K, int PB>
+__global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, const FRec *cf, const FRec *cb, LabelGraph L,
+                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
+                                                        uint32_t *dt, uint64_t n, uint64_t *allowed,
+                                                        uint32_t *spill_out, unsigned int *spill_count,
+                                                        unsigned long long *stats, unsigned long long *first_bad) {
+    __shared__ LabelShared sh;
+    uint32_t r[K], t[K];
+    host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
+    const uint64_t units = (n + 15) / 16;
+#pragma unroll 1
+    for (int k = 0; k < K; k++) {
+        const uint64_t unit = (uint64_t)blockIdx.x * K + k;
+        if (unit >= units) break;
+        uint32_t rk = r[0], tk = t[0];
+#pragma unroll
+        for (int j = 1; j < K; j++)
+            if (j == k) rk = r[j], tk = t[j];
+        label_unit<PB>(sh, g, cf, cb, L, rk, tk, allowed, unit, spill_out, spill_count, stats);
         __syncthreads();
     }
 }
@@ -3444,6 +3620,13 @@ struct ketogpu_engine {
     uint32_t core_blk_log[2] = {0, 0}, core_block[2] = {0, 0};  // KETOGPU_CORE_BLOCKS="forward,backward" records
     uint64_t core_overflow[2] = {0, 0};
     uint32_t closure_cap[2] = {64, 64};
+    // plan "label" (label_kernel): closure labels over plan core's arrays (labels.hpp);
+    // KETOGPU_LABEL_MODE = B / F forces a mode, default: the better-covered one (none when
+    // both label less than half of the nodes)
+    bool use_label = false;
+    LabelGraph lgraph{};
+    uint32_t label_pb = 32;
+    double label_coverage = 0, label_build_ms = 0;
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
     uint64_t closure_nodes[2] = {0, 0}, closure_entries[2] = {0, 0};
     double core_build_ms = 0;
@@ -3469,7 +3652,7 @@ struct ketogpu_engine {
         bool units = true;    // false: the global path alone (with the hub index)
         int u = 16;           // bidi: requests per first-stage unit
         int wpe = 1;          // bidi: minimum waves per SIMD of the first stage
-        int lite = 0;         // bidi: plan "lite" (lite_kernel); 2: plan "core"
+        int lite = 0;         // bidi: plan "lite" (lite_kernel); 2: plan "core"; 3: plan "label"
     };
     std::vector<Candidate> candidates;
     // first bidi pass: table log2, threads per unit, list capacity, load limit in eighths
@@ -3478,7 +3661,7 @@ struct ketogpu_engine {
         int hlog, bt, f, lf;
         int u = 16;   // requests per unit (16, or 8: half the LDS per unit)
         int wpe = 1;  // minimum waves per SIMD asked of the compiler (bidi_kernel WPE)
-        int lite = 0;  // 1: plan "lite" (lite_kernel: per-unit direction, per-direction rings); 2: plan "core"
+        int lite = 0;  // 1: plan "lite" (lite_kernel: per-unit direction, per-direction rings); 2: plan "core"; 3: "label"
         bool operator==(const BidiCfg &o) const {
             return hlog == o.hlog && bt == o.bt && f == o.f && lf == o.lf && u == o.u && wpe == o.wpe &&
                    lite == o.lite;
@@ -3490,6 +3673,19 @@ struct ketogpu_engine {
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
+        if (c.lite == 3) {  // plan label: closure labels, plan core for units without
+#define KETO_LABEL_K(PB)                                                                                          \
+    KLAUNCH((label_kernel<PB>), dim3(grid), dim3(64), pad, stream, gcore(), core_rec[0], core_rec[1], lgraph, q.roots, \
+            q.targets, q.n, q.allowed, out, out_count, stats, unit0)
+            if (label_pb == 16)
+                KETO_LABEL_K(16);
+            else if (label_pb == 32)
+                KETO_LABEL_K(32);
+            else
+                KETO_LABEL_K(64);
+#undef KETO_LABEL_K
+            return;
+        }
         if (c.lite == 2) {  // plan core: lite over the core record arrays
 #define KETO_CORE_K(SH)                                                                                       \
     KLAUNCH((lite_kernel<SH, true>), dim3(grid), dim3(64), pad, stream, gcore(), core_rec[0], core_rec[1], q.roots, \
@@ -3800,7 +3996,7 @@ struct ketogpu_engine {
         const char *plan = getenv("KETOGPU_UNITS");
         std::string p = plan ? plan : "auto";
         wave_u = p == "w4" ? 4 : p == "w8" ? 8 : p == "w16" ? 16 : 0;
-        const bool lite_req = p == "lite" || p == "lite32" || p == "core" || p == "auto";
+        const bool lite_req = p == "lite" || p == "lite32" || p == "core" || p == "label" || p == "auto";
         use_v2 = p == "v2" || p == "bidi" || lite_req;
         // Edge records carry 32-bit row begins.  Plan lite reads only INTERIOR rows through
         // records (ids below Ni come first, so their begins are the smallest) and carries
@@ -3817,7 +4013,9 @@ struct ketogpu_engine {
         // bidi / lite: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_lite = lite_req && use_v2 && !s.has_ambiguous && lite_ok;
         // plan core: not on writable snapshots (an in-place write would change closures)
-        use_core = (p == "core" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_CORE") == nullptr;
+        use_core = (p == "core" || p == "label" || p == "auto") && use_lite && !s.writable &&
+                   getenv("KETOGPU_NO_CORE") == nullptr;
+        use_label = (p == "label" || p == "auto") && use_core && getenv("KETOGPU_NO_LABEL") == nullptr;
         if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
         if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
         if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
@@ -3833,6 +4031,10 @@ struct ketogpu_engine {
         if (p == "core" && use_core) {  // forced: plan core, no trials
             use_bidi = true;
             bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 2};
+        }
+        if (p == "label" && use_label) {  // forced: plan label (falls back to core if no mode labels enough)
+            use_bidi = true;
+            bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 3};
         }
         if ((p == "lite" || p == "lite32") && use_lite) {  // forced: the lite first stage, no trials
             use_bidi = true;
@@ -3861,10 +4063,11 @@ struct ketogpu_engine {
             }
             if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
             if (use_core) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 2});  // plan "core"
+            if (use_label) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 3});  // plan "label"
             if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
             // batches below the trial size run lite until the trials have picked a plan
             // (round 3: lite 0.284 vs bidi 0.367 ms per 10^6 config #2 requests)
-            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, use_core ? 2 : 1};
+            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, use_label ? 3 : use_core ? 2 : 1};
             use_bidi = use_bidi || use_lite;
         }
         if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
@@ -4007,6 +4210,7 @@ struct ketogpu_engine {
             closure_entries[d] = ci.closure_entries[d];
         }
         core_build_ms = ci.build_ms;
+        if (use_label) build_label(s, ci, free_b - bytes);
         if (cascade_log)
             fprintf(stderr, "[core] closure rows: forward %llu nodes / %llu entries, backward %llu / %llu (caps %u, %u); "
                             "blocks of %u / %u records, %llu / %llu rows in overflow; %.2f GB; built in %.1f ms\n",
@@ -4017,9 +4221,55 @@ struct ketogpu_engine {
     }
     void drop_core() {
         use_core = false;
-        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite == 2; }),
+        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite >= 2; }),
                          candidates.end());
-        if (bidi_cfg.lite == 2) bidi_cfg.lite = 1;
+        if (bidi_cfg.lite >= 2) bidi_cfg.lite = 1;
+        drop_label();
+    }
+    void drop_label() {
+        use_label = false;
+        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite == 3; }),
+                         candidates.end());
+        if (bidi_cfg.lite == 3) bidi_cfg.lite = use_core ? 2 : 1;
+    }
+    // plan label's closure labels (labels.hpp) over the core index just built
+    void build_label(const Snapshot &s, const CoreIndex &ci, uint64_t free_b) {
+        int mode = -1;
+        if (const char *e = getenv("KETOGPU_LABEL_MODE")) mode = e[0] == 'F' || e[0] == 'f' ? 1 : 0;
+        LabelIndex li;
+        try {
+            build_labels(s, ci, mode, 0.5, li);
+        } catch (const Error &e) {
+            fprintf(stderr, "[ketogpu] plan label disabled: %s\n", e.what());
+            drop_label();
+            return;
+        }
+        label_build_ms = li.build_ms;
+        if (li.mode < 0) {
+            if (cascade_log)
+                fprintf(stderr, "[label] no mode labels half of its nodes (B %.3f, F %.3f): plan off\n", li.coverage[0],
+                        li.coverage[1]);
+            drop_label();
+            return;
+        }
+        const uint64_t bytes = 4 * (li.P.size() + li.S.size());
+        if (bytes > free_b / 4) {
+            fprintf(stderr, "[ketogpu] plan label disabled: %llu bytes of labels, %llu free\n",
+                    (unsigned long long)bytes, (unsigned long long)free_b);
+            drop_label();
+            return;
+        }
+        uint32_t *P = dupload(li.P), *S = dupload(li.S);
+        owned.push_back(P);
+        owned.push_back(S);
+        lgraph = LabelGraph{P, S, li.mode};
+        label_pb = li.pb;
+        label_coverage = li.nonempty ? (double)li.covered / (double)li.nonempty : 1.0;
+        if (cascade_log)
+            fprintf(stderr, "[label] mode %c: %llu of %llu S nodes labelled (%.4f; sampled B %.3f F %.3f), P blocks of %u "
+                            "words, %.2f GB, built in %.1f ms\n",
+                    li.mode ? 'F' : 'B', (unsigned long long)li.covered, (unsigned long long)li.nonempty,
+                    label_coverage, li.coverage[0], li.coverage[1], li.pb, (double)bytes / 1e9, li.build_ms);
     }
 
     // Hub index.  Hubs are the interior nodes with the most interior successors; a search
@@ -4334,7 +4584,19 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite == 2 && core_shape == 1)                                                         \
+        if (bidi_cfg.lite == 3 && label_pb == 16)                                                          \
+            KLAUNCH((label_host_kernel<K, 16>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
+                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite == 3 && label_pb == 32)                                                     \
+            KLAUNCH((label_host_kernel<K, 32>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
+                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite == 3)                                                                       \
+            KLAUNCH((label_host_kernel<K, 64>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
+                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
+                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+        else if (bidi_cfg.lite == 2 && core_shape == 1)                                                    \
             KLAUNCH((lite_host_kernel<K, CoreShapeS, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
                     0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
                     io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
@@ -4646,7 +4908,11 @@ struct ketogpu_engine {
         Batch q = qq.batch();
         ketogpu_run_stats rs{};
         rs.checks = q.n;
-        rs.plan = !use_units ? 0 : wave_u ? 3 : use_bidi ? (bidi_cfg.lite == 2 ? 6 : bidi_cfg.lite ? 5 : 1) : use_v2 ? 2 : 4;
+        rs.plan = !use_units ? 0
+                  : wave_u    ? 3
+                  : use_bidi  ? (bidi_cfg.lite == 3 ? 7 : bidi_cfg.lite == 2 ? 6 : bidi_cfg.lite ? 5 : 1)
+                  : use_v2    ? 2
+                              : 4;
         rs.plan_lists = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.f : 0;
         rs.plan_unit = use_units && !wave_u && use_bidi ? (uint32_t)bidi_cfg.u : 0;
         rs.hubs = n_hubs;
@@ -4659,6 +4925,9 @@ struct ketogpu_engine {
         rs.closure_entries_f = closure_entries[0];
         rs.closure_entries_b = closure_entries[1];
         rs.core_build_ms = core_build_ms;
+        rs.label_mode = use_label ? lgraph.mode : -1;
+        rs.label_coverage = label_coverage;
+        rs.label_build_ms = label_build_ms;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
@@ -5141,6 +5410,16 @@ int ketogpu_engine_check_graph(ketogpu_engine *e, uint64_t *mismatches) {
     *mismatches = bad;
     set_last_error(first);
     API_END
+}
+
+int ketogpu_engine_set_events(ketogpu_engine *e, int every_kernel) {
+    if (!e) {
+        set_last_error("null argument");
+        return KETOGPU_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->light_events = !every_kernel;
+    return KETOGPU_OK;
 }
 
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out) {

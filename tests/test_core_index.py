@@ -7,6 +7,7 @@ closure has more nodes than the cap.  CPU only (no device calls)."""
 import numpy as np
 import pytest
 
+from keto_amd import relationtuple as rt
 from keto_amd.snapshot import Snapshot
 from tests import randgraph
 
@@ -156,3 +157,76 @@ def test_cycles():
     snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
     check_index(snap, (64, 64))
     check_index(snap, (2, 2))
+
+
+# ------------------------------------------------------------------ closure labels
+def label_answer(li, r, t):
+    """allowed(r, t) from plan label's blocks (labels.hpp), or None when the request's S
+    node has no label"""
+    NONE_ = 0xFFFFFFFF
+    if r == NONE_ or t == NONE_:
+        return False
+    xs, xp = (t, r) if li["mode"] == 0 else (r, t)
+    S, P, pb = li["S"], li["P"], li["p_block_words"]
+    n = int(S[xs * 64])
+    if n == NONE_:
+        return None
+    s = S[xs * 64 + 1: xs * 64 + 1 + n]
+    assert np.all(np.diff(s.astype(np.int64)) > 0) and np.all(S[xs * 64 + 1 + n: xs * 64 + 64] == NONE_)
+    m, ovf = int(P[xp * pb]), int(P[xp * pb + 1])
+    p = list(P[xp * pb + 2: xp * pb + 2 + min(m, pb - 2)])
+    if m > pb - 2:
+        p += list(P[ovf * 16: ovf * 16 + m - (pb - 2)])
+    assert len(p) == m
+    return bool(np.isin(np.asarray(p, dtype=np.uint32), s).any())
+
+
+def check_labels(snap, reqs, want, mode):
+    li = snap.label_index((64, 64), mode)
+    if mode >= 0:
+        assert li["mode"] == mode
+    if li["mode"] < 0:
+        return li, 0
+    roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs])
+    done = 0
+    for i in range(len(reqs)):
+        got = label_answer(li, int(roots[i]), int(targets[i]))
+        if got is None:
+            continue
+        assert got == bool(want[i]), (reqs[i], got, want[i])
+        done += 1
+    return li, done
+
+
+@pytest.mark.parametrize("seed,poison", [(81, False), (82, True), (83, False)])
+@pytest.mark.parametrize("mode", [0, 1, -1])
+def test_labels_answer_like_the_oracle(seed, poison, mode):
+    """every request whose S node has a label is answered by one intersection exactly as
+    the reference's recursion (oracle), in both modes"""
+    namespaces, rows = randgraph.make_graph(seed, n_rows=900, n_obj=40, n_users=50, poison=poison)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
+    reqs = randgraph.make_requests(seed, namespaces, rows, n=1500, wildcard=False)
+    want = randgraph.oracle_store(namespaces, rows, 4).check_batch(reqs)
+    li, done = check_labels(snap, reqs, want, mode)
+    if li["mode"] >= 0:
+        assert done > 0.3 * len(reqs)
+
+
+@pytest.mark.parametrize("kind,mode", [("rbac", 0), ("folders", 1)])
+def test_labels_on_synthetic_configs(kind, mode):
+    """config #2's backward labels and config #3's forward labels: the default mode is
+    the one the generator's shape favours, nearly every request is labelled and exact"""
+    from keto_amd import synth
+    w = {"rbac": lambda: synth.rbac(users=4000, groups=400, docs=800, tuples=30000, checks=3000, seed=6),
+         "folders": lambda: synth.folders(users=3000, groups=80, folders=2000, tuples=30000, checks=3000,
+                                          seed=6)}[kind]()
+    snap = Snapshot.from_columns(w.namespaces, w.columns)
+    li = snap.label_index((64, 64), -1)
+    assert li["mode"] == mode
+    roots, targets = w.resolve(snap)
+    want = randgraph.oracle_store_columns(w.namespaces, w.columns).check_batch(w.requests(range(len(roots))),
+                                                                                 nthreads=4)
+    got = [label_answer(li, int(roots[i]), int(targets[i])) for i in range(len(roots))]
+    done = [i for i, g in enumerate(got) if g is not None]
+    assert len(done) > 0.9 * len(roots)
+    assert all(got[i] == bool(want[i]) for i in done)

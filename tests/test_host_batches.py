@@ -62,7 +62,7 @@ def _pipe_mode(monkeypatch, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("plan", ["bidi", "lite", "lite32", "core"])
+@pytest.mark.parametrize("plan", ["bidi", "lite", "lite32", "core", "label"])
 @pytest.mark.parametrize("mode", ["direct", "direct1", "direct4", "chunks"])
 @pytest.mark.parametrize("chunk", ["4096", "65536", "1048576"])
 def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, plan, monkeypatch):
