@@ -671,6 +671,16 @@ typedef struct {
 } ketogpu_transport;
 int ketogpu_comm_from_transport(const ketogpu_transport *t, ketogpu_comm **out);
 void ketogpu_comm_free(ketogpu_comm *c);
+/* RCCL calls a communicator made (counts since creation; a host transport's are 0).
+ * KETOGPU_TEST_RCCL_SELF=1 when an RCCL communicator is made (tests): at world 1 too, the
+ * all-to-alls move the rank's own segment with a grouped ncclSend/ncclRecv to itself and
+ * the two-tier count gathers run as ncclAllGather, so one GPU executes the multi-GPU
+ * data path (default: the own segment is a copy-engine DMA and world-1 gathers are skipped) */
+typedef struct {
+    int32_t rccl, loop_self;
+    uint64_t sends, recvs, allgathers, allreduces, bytes_sent;
+} ketogpu_comm_stats;
+int ketogpu_comm_stats_get(const ketogpu_comm *c, ketogpu_comm_stats *out);
 int ketogpu_comm_rank(const ketogpu_comm *c);
 int ketogpu_comm_world(const ketogpu_comm *c);
 

@@ -153,6 +153,14 @@ class LabelView(C.Structure):
                 ("coverage_b", C.c_double), ("coverage_f", C.c_double)]
 
 
+class CommStats(C.Structure):
+    _fields_ = [("rccl", C.c_int32), ("loop_self", C.c_int32)] + [(n, C.c_uint64) for n in (
+        "sends", "recvs", "allgathers", "allreduces", "bytes_sent")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class TreeNode(C.Structure):
     _fields_ = [("type", C.c_int32), ("num_children", C.c_uint32), ("subject", Subject)]
 
@@ -299,6 +307,7 @@ SIGNATURES = {
     "ketogpu_core_index_build": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(vp)]),
     "ketogpu_core_index_view": (C.c_int, [vp, C.c_int, C.POINTER(CoreRecords)]),
     "ketogpu_core_index_free": (None, [vp]),
+    "ketogpu_comm_stats_get": (C.c_int, [vp, C.POINTER(CommStats)]),
     "ketogpu_label_index_build": (C.c_int, [vp, C.POINTER(u32), C.c_int, C.POINTER(vp)]),
     "ketogpu_label_index_view": (C.c_int, [vp, C.POINTER(LabelView)]),
     "ketogpu_label_index_free": (None, [vp]),

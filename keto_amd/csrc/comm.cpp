@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -97,6 +98,7 @@ struct RcclComm : Comm {
     void allgather(const void *send, void *recv, uint64_t bytes, hipStream_t s) override {
         CHIP(hipSetDevice(dev));
         nccl_check(rccl().AllGather(send, recv, bytes, ncclUint8, comm, s), "ncclAllGather");
+        n_allgather++;
     }
     void alltoallv(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb, hipStream_t s) override {
         CHIP(hipSetDevice(dev));
@@ -104,18 +106,26 @@ struct RcclComm : Comm {
         uint64_t so = 0, ro = 0;
         for (int p = 0; p < rank; p++) so += sb[p], ro += rb[p];
         // the rank's own segment: a copy engine's DMA on the same stream (RCCL's self
-        // send/receive runs as a kernel at ~1 TB/s)
+        // send/receive runs as a kernel at ~1 TB/s); loop_self (tests): through RCCL
         if (sb[rank] != rb[rank]) throw Error(KETOGPU_EINVAL, "alltoallv: own segment sizes differ");
-        if (sb[rank])
+        if (sb[rank] && !loop_self)
             CHIP(hipMemcpyAsync((char *)recv + ro, (const char *)send + so, sb[rank], hipMemcpyDeviceToDevice, s));
-        if (world == 1) return;
+        if (world == 1 && !loop_self) return;
         nccl_check(a.GroupStart(), "ncclGroupStart");
         so = ro = 0;
         for (int p = 0; p < world; p++) {
             // one send and one receive per peer in one group: RCCL runs them concurrently,
             // one xGMI link per peer pair
-            if (p != rank && sb[p]) nccl_check(a.Send((const char *)send + so, sb[p], ncclUint8, p, comm, s), "ncclSend");
-            if (p != rank && rb[p]) nccl_check(a.Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, s), "ncclRecv");
+            const bool peer = p != rank || loop_self;
+            if (peer && sb[p]) {
+                nccl_check(a.Send((const char *)send + so, sb[p], ncclUint8, p, comm, s), "ncclSend");
+                n_send++;
+                bytes_sent += sb[p];
+            }
+            if (peer && rb[p]) {
+                nccl_check(a.Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, s), "ncclRecv");
+                n_recv++;
+            }
             so += sb[p];
             ro += rb[p];
         }
@@ -125,6 +135,7 @@ struct RcclComm : Comm {
         CHIP(hipSetDevice(dev));
         nccl_check(rccl().AllReduce(buf, buf, n, ncclUint32, op == KETOGPU_REDUCE_MIN ? ncclMin : ncclMax, comm, s),
                    "ncclAllReduce");
+        n_allreduce++;
     }
     void wait(hipStream_t s) override { CHIP(hipStreamSynchronize(s)); }
 };
@@ -189,6 +200,7 @@ int ketogpu_comm_new(const uint8_t id[KETOGPU_COMM_ID_BYTES], int32_t rank, int3
     c->world = world;
     c->device = true;
     c->dev = device;
+    c->loop_self = getenv("KETOGPU_TEST_RCCL_SELF") != nullptr;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     nccl_check(rccl().CommInitRank(&c->comm, world, u, rank), "ncclCommInitRank");
@@ -212,6 +224,22 @@ int ketogpu_comm_from_transport(const ketogpu_transport *t, ketogpu_comm **out) 
     h->c = std::move(c);
     *out = h.release();
     CAPI_END
+}
+
+int ketogpu_comm_stats_get(const ketogpu_comm *c, ketogpu_comm_stats *out) {
+    if (!c || !out) {
+        set_last_error("null argument");
+        return KETOGPU_EINVAL;
+    }
+    const Comm &m = *c->c;
+    out->rccl = m.device ? 1 : 0;
+    out->loop_self = m.loop_self ? 1 : 0;
+    out->sends = m.n_send;
+    out->recvs = m.n_recv;
+    out->allgathers = m.n_allgather;
+    out->allreduces = m.n_allreduce;
+    out->bytes_sent = m.bytes_sent;
+    return KETOGPU_OK;
 }
 
 void ketogpu_comm_free(ketogpu_comm *c) { delete c; }

@@ -2223,8 +2223,21 @@ template <class SH, bool CL = false>
 __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *frec, const FRec *brec,
                                           const BidiSeed &seed, uint64_t *allowed, const uint64_t unit,
                                           uint32_t *spill_out, unsigned int *spill_count, unsigned long long *stats,
-                                          unsigned long long *stamp = nullptr) {
+                                          unsigned long long *stamp = nullptr, uint32_t ridx = KETOGPU_NODE_NONE,
+                                          bool gathered = false) {
     const uint32_t lane = threadIdx.x;
+    // gathered (plan label's second stage): the unit's requests are scattered over the
+    // batch, lane j < U holding request j's index (ridx; NONE: no request); results and
+    // spills go per request instead of per unit
+    auto spill_unit = [&]() {
+        if (!gathered) {
+            if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        } else {
+            const bool w = lane < SH::U && ridx != KETOGPU_NODE_NONE;
+            const uint32_t at = lds_append(w, spill_count);
+            if (w) spill_out[at] = ridx;
+        }
+    };
     if (stamp) stamp[0] = __builtin_amdgcn_s_memtime();
     const uint64_t c0 = unit * SH::U;
     for (int i = lane; i < SH::H / 4; i += 64) reinterpret_cast<uint4 *>(S.key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
@@ -2248,7 +2261,7 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     }
     __syncthreads();
     if (S.spill) {
-        if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        spill_unit();
         return;
     }
     uint32_t active = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.active);
@@ -2400,7 +2413,7 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     }
     __syncthreads();
     if (spilled || S.spill) {
-        if (lane == 0) spill_out[atomicAdd(spill_count, 1u)] = (uint32_t)unit;
+        spill_unit();
         return;
     }
     if (stamp) {  // KETOGPU_STAMPS=1: phase cycles, levels and table load per unit (report_stamps)
@@ -2415,10 +2428,12 @@ __device__ __forceinline__ void lite_unit(SH &S, const DevGraph &g, const FRec *
     for (int s = 32; s; s >>= 1) rows += __shfl_down(rows, s, 64);  // edges: already the wave's
     if (lane == 0) {
         const uint32_t res = S.found & SH::MASK;
-        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
+        if (res && !gathered) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
         atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
         atomicAdd(&stat_slot(stats)[1], (unsigned long long)edges);
     }
+    if (gathered && lane < SH::U && ridx != KETOGPU_NODE_NONE && ((S.found >> lane) & 1u))
+        atomicOr((unsigned long long *)&allowed[ridx >> 6], 1ull << (ridx & 63));
 }
 
 // plan "lite" first stage over HBM-resident requests (unit0: a chunk's first unit); CL:
@@ -2489,15 +2504,26 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 // allowed <=> they share a node.  One wave per 16-request unit: four lanes per request
 // copy its S block into LDS (the second half only when the label has more than 31 nodes)
 // and hold its P block in registers; each P entry is looked up in S by a 6-step binary
-// search.  A unit with a request that has no label (or a wildcard root) runs plan core's
-// traversal (lite_unit<CL>) instead, in the same LDS.
+// search.  A request without a label (or with a wildcard root) is listed (spill_out, one
+// request index each) for the second stage, label_rest_kernel: plan core's traversal over
+// the listed requests, gathered 16 to a unit.
 struct LabelGraph {
     const uint32_t *P, *S;  // P blocks (+ overflow), S blocks (kLabelWords words each)
     int mode;               // 0 = B (S node t, P node r), 1 = F (S node r, P node t)
 };
+// The unlabelled requests' list is sharded: unit u appends to region u % kRestShards of
+// the list (region capacity `rest_cap` = 16 x ceil(units / kRestShards)) at counter
+// rest_count[(u % kRestShards) * kRestStride] — one cache line per counter, so ~15k
+// appends per 10^6 requests do not serialize on one address.  Two counter sets alternate
+// between calls: a call's first stage (workgroup 0) clears the other set for the next call.
+constexpr int kRestShards = 64, kRestStride = 32;
+struct LabelRest {
+    uint32_t *list;
+    unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
+    uint64_t cap;                      // entries per region
+};
 constexpr int kLabelStride = 65;  // LDS words per request's S list (odd: the 16 lists start in different banks)
-union LabelShared {
-    CoreShapeM lite;
+struct LabelShared {
     uint32_t S[16 * kLabelStride];
 };
 
@@ -2511,9 +2537,8 @@ __device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
 }
 
 template <int PB>
-__device__ __forceinline__ void label_unit(LabelShared &sh, const DevGraph &g, const FRec *cf, const FRec *cb,
-                                           const LabelGraph &L, uint32_t r_lane, uint32_t t_lane, uint64_t *allowed,
-                                           const uint64_t unit, uint32_t *spill_out, unsigned int *spill_count,
+__device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
+                                           uint64_t *allowed, const uint64_t unit, const LabelRest &R,
                                            unsigned long long *stats) {
     static_assert(PB == 16 || PB == 32 || PB == 64, "P blocks of 16, 32 or 64 words");
     constexpr int PW = PB / 4;  // P words per lane
@@ -2539,13 +2564,12 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const DevGraph &g, c
         }
     }
     uint32_t *S = sh.S + q * kLabelStride;
-    // invalid requests (an id NONE): an empty label, so nothing is found
-    if (!valid && sub == 0) sw[0] = some ? 0xFFFFFFFFu : 0u;
+    if (!valid && sub == 0) sw[0] = some ? kNoLabel : 0u;  // a wildcard root: no label; an id NONE: empty
 #pragma unroll
     for (int k = 0; k < 8; k++) S[8 * sub + k] = sw[k];
     const uint32_t ns = (uint32_t)__shfl((int)sw[0], (int)(lane & ~3u), 64);  // the label's count
-    const bool big = valid && ns != kNoLabel && ns > 31;
-    if (big) {  // entries 32..63: the block's second line
+    const bool labelled = valid && ns != kNoLabel;
+    if (labelled && ns > 31) {  // entries 32..63: the block's second line
         const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * kLabelWords + 32) + 2 * sub;
         const uint4 a = sb[0], b = sb[1];
         sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
@@ -2555,33 +2579,35 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const DevGraph &g, c
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) S[32 + 8 * sub + k] = sw[k];
-    // a request without a label (or a wildcard root): the unit runs plan core's traversal
-    if (__ballot(sub == 0 && some && (ns == kNoLabel || !valid))) {
-        __syncthreads();
-        lite_unit<CoreShapeM, true>(sh.lite, g, cf, cb, core_load_rows(g, cf, cb, r_lane, t_lane), allowed, unit,
-                                    spill_out, spill_count, stats);
-        return;
+    // a request without a label (or with a wildcard root): listed for the second stage
+    {
+        const bool rest = sub == 0 && some && !labelled;
+        const uint32_t shard = (uint32_t)(unit % kRestShards);
+        const uint32_t at = lds_append(rest, R.count + shard * kRestStride);
+        if (rest) R.list[shard * R.cap + at] = (uint32_t)(unit * 16 + q);
     }
     __syncthreads();
     const uint32_t np = (uint32_t)__shfl((int)pw[0], (int)(lane & ~3u), 64);
     const uint32_t ovf = (uint32_t)__shfl((int)pw[1], (int)(lane & ~3u), 64);
     bool hit = false;
     uint32_t looked = 0;
+    if (labelled) {
 #pragma unroll
-    for (int k = 0; k < PW; k++) {
-        const uint32_t w = PW * sub + k;  // the entry of word w is entry w - 2
-        if (w >= 2 && w - 2 < np) {
-            hit |= label_find(S, pw[k]);
-            looked++;
+        for (int k = 0; k < PW; k++) {
+            const uint32_t w = PW * sub + k;  // the entry of word w is entry w - 2
+            if (w >= 2 && w - 2 < np) {
+                hit |= label_find(S, pw[k]);
+                looked++;
+            }
         }
+        if (np > (uint32_t)PB - 2)  // the row's entries past its block
+            for (uint32_t k = PB - 2 + sub; k < np; k += 4) {
+                hit |= label_find(S, L.P[(uint64_t)ovf * 16 + (k - (PB - 2))]);
+                looked++;
+            }
     }
-    if (valid && np > (uint32_t)PB - 2)  // the row's entries past its block
-        for (uint32_t k = PB - 2 + sub; k < np; k += 4) {
-            hit |= label_find(S, L.P[(uint64_t)ovf * 16 + (k - (PB - 2))]);
-            looked++;
-        }
     const uint64_t bits = __ballot(hit);
-    uint64_t rows = valid && sub == 0 ? 2 : 0, ent = looked + (valid && sub == 0 && ns != kNoLabel ? ns : 0);
+    uint64_t rows = labelled && sub == 0 ? 2 : 0, ent = looked + (labelled && sub == 0 ? ns : 0);
 #pragma unroll
     for (int k = 32; k; k >>= 1) {
         rows += __shfl_down(rows, k, 64);
@@ -2597,27 +2623,32 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const DevGraph &g, c
     }
 }
 
+// the next call's rest counters, cleared by workgroup 0 of the first stage
+__device__ __forceinline__ void label_clear_next(const LabelRest &R) {
+    if (blockIdx.x == 0) R.next_count[threadIdx.x * kRestStride] = 0u;  // 64 lanes: every shard
+}
+
 template <int PB>
-__global__ __launch_bounds__(64) void label_kernel(DevGraph g, const FRec *cf, const FRec *cb, LabelGraph L,
-                                                   const uint32_t *roots, const uint32_t *targets, uint64_t n,
-                                                   uint64_t *allowed, uint32_t *spill_out, unsigned int *spill_count,
+__global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t *roots, const uint32_t *targets,
+                                                   uint64_t n, uint64_t *allowed, LabelRest R,
                                                    unsigned long long *stats, uint64_t unit0) {
     __shared__ LabelShared sh;
+    if (unit0 == 0) label_clear_next(R);
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
-    label_unit<PB>(sh, g, cf, cb, L, r, t, allowed, unit, spill_out, spill_count, stats);
+    label_unit<PB>(sh, L, r, t, allowed, unit, R, stats);
 }
 
-// pinned host requests read in place (lite_host_kernel's prologue)
+// pinned host requests read in place (host_unit_requests)
 template <int K, int PB>
-__global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, const FRec *cf, const FRec *cb, LabelGraph L,
-                                                        const uint32_t *hr, const uint32_t *ht, uint32_t *dr,
-                                                        uint32_t *dt, uint64_t n, uint64_t *allowed,
-                                                        uint32_t *spill_out, unsigned int *spill_count,
-                                                        unsigned long long *stats, unsigned long long *first_bad) {
+__global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L, const uint32_t *hr,
+                                                        const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
+                                                        uint64_t *allowed, LabelRest R, unsigned long long *stats,
+                                                        unsigned long long *first_bad) {
     __shared__ LabelShared sh;
+    label_clear_next(R);
     uint32_t r[K], t[K];
     host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
     const uint64_t units = (n + 15) / 16;
@@ -2629,7 +2660,43 @@ __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, const FRec *
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        label_unit<PB>(sh, g, cf, cb, L, rk, tk, allowed, unit, spill_out, spill_count, stats);
+        label_unit<PB>(sh, L, rk, tk, allowed, unit, R, stats);
+        __syncthreads();
+    }
+}
+
+// the second stage: plan core's traversal over the requests the labels did not answer
+// (in: request indices, *in_count of them, written by the first stage on this stream),
+// gathered 16 to a unit; persistent over the listed requests.  A unit that outgrows its
+// table lists its requests (out) for the multi-word global path.
+template <class SH>
+__global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *cf, const FRec *cb,
+                                                        const uint32_t *roots, const uint32_t *targets,
+                                                        uint64_t *allowed, LabelRest R, unsigned int *total,
+                                                        uint32_t *out, unsigned int *out_count,
+                                                        unsigned long long *stats) {
+    __shared__ SH S;
+    // the shards' counts (lane k: shard k) and their units' exclusive prefix
+    const uint32_t lane = threadIdx.x;
+    const uint32_t c = R.count[lane * kRestStride];
+    const uint32_t nu = (c + 15) / 16;
+    const uint32_t incl = wave_incl_sum_u32(nu);
+    const uint64_t units = (uint64_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (blockIdx.x == 0 && lane == 0) *total = (unsigned int)wave_sum_all(c);  // the host reads the total here
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        // the shard holding gathered unit u: the first whose inclusive prefix passes u
+        const uint32_t shard = (uint32_t)__builtin_ctzll(__ballot(incl > u));
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)(incl - nu), (int)shard);
+        const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)shard);
+        const uint64_t j = (u - first) * 16 + lane;
+        uint32_t idx = KETOGPU_NODE_NONE, r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+        if (lane < 16 && j < cs) {
+            idx = R.list[shard * R.cap + j];
+            r = roots[idx];
+            t = targets[idx];
+        }
+        lite_unit<SH, true>(S, g, cf, cb, core_load_rows(g, cf, cb, r, t), allowed, u, out, out_count, stats,
+                            nullptr, idx, true);
         __syncthreads();
     }
 }
@@ -3625,6 +3692,14 @@ struct ketogpu_engine {
     // both label less than half of the nodes)
     bool use_label = false;
     LabelGraph lgraph{};
+    unsigned int *rest_counts = nullptr;  // two sets of kRestShards counters, one cache line each
+    uint64_t label_calls = 0;             // selects the set
+    LabelRest label_rest(uint64_t n) {    // this call's rest list over requests [0, n)
+        const uint64_t units = (n + 15) / 16;
+        const unsigned set = (unsigned)(label_calls & 1);
+        return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
+                         rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
+    }
     uint32_t label_pb = 32;
     double label_coverage = 0, label_build_ms = 0;
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
@@ -3674,9 +3749,9 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite == 3) {  // plan label: closure labels, plan core for units without
-#define KETO_LABEL_K(PB)                                                                                          \
-    KLAUNCH((label_kernel<PB>), dim3(grid), dim3(64), pad, stream, gcore(), core_rec[0], core_rec[1], lgraph, q.roots, \
-            q.targets, q.n, q.allowed, out, out_count, stats, unit0)
+#define KETO_LABEL_K(PB)                                                                                   \
+    KLAUNCH((label_kernel<PB>), dim3(grid), dim3(64), pad, stream, lgraph, q.roots, q.targets, q.n, q.allowed, \
+            label_rest(q.n), stats, unit0)
             if (label_pb == 16)
                 KETO_LABEL_K(16);
             else if (label_pb == 32)
@@ -3784,6 +3859,11 @@ struct ketogpu_engine {
         case 'r':
             KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(stage_grid(prev, 1280)), dim3(64), 0, stream, g, frec,
                     brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
+            return;
+        case 'L':  // plan label's second stage: plan core over the listed requests (in: request indices)
+            KLAUNCH((label_rest_kernel<TierStage1>), dim3(stage_grid(prev / 16 + 1, 256 * 4)), dim3(64), 0, stream,
+                    gcore(), core_rec[0], core_rec[1], q.roots, q.targets, q.allowed, label_rest(q.n),
+                    const_cast<unsigned int *>(in_count), out, out_count, stats);
             return;
         default:
             KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(stage_grid(prev, 256)), dim3(256), 0, stream, g, frec,
@@ -4262,6 +4342,9 @@ struct ketogpu_engine {
         uint32_t *P = dupload(li.P), *S = dupload(li.S);
         owned.push_back(P);
         owned.push_back(S);
+        rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
+        owned.push_back(rest_counts);
+        HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
         lgraph = LabelGraph{P, S, li.mode};
         label_pb = li.pb;
         label_coverage = li.nonempty ? (double)li.covered / (double)li.nonempty : 1.0;
@@ -4370,7 +4453,8 @@ struct ketogpu_engine {
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags})
             if (p) (void)hipFree(p);
-        spill_cap = std::max<uint64_t>(n, 1024);
+        // (+ 2048: plan label's sharded rest list rounds every shard's region up to whole units)
+        spill_cap = std::max<uint64_t>(n + 2048, 1024);
         spill_units = dalloc<uint32_t>(2 * spill_cap);
         spill_roots = dalloc<uint32_t>(spill_cap);
         spill_targets = dalloc<uint32_t>(spill_cap);
@@ -4417,6 +4501,11 @@ struct ketogpu_engine {
             fans.push_back((uint32_t)(u_prev / sg.u));
             u_prev = sg.u;
         }
+        if (bidi_cfg.lite == 3) {  // plan label: the first stage lists single requests; one stage after it
+            stages.assign(1, SpillStage{1, 'L'});
+            fans.assign(1, 1u);
+            u_prev = 1;
+        }
         const int cur = (int)(stages.size() & 1);  // the list the last stage writes
         auto launch_stages = [&](uint64_t prev0) {
             for (size_t k = 0, c = 0; k < stages.size(); k++, c ^= 1)
@@ -4429,7 +4518,8 @@ struct ketogpu_engine {
         // shows spills, followed by a second statistics pass, the result copies again and a
         // second synchronization.  KETOGPU_CASCADE_EAGER=1: always up front (A/B).
         static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
-        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0;
+        // (plan label: its second stage always runs — it totals the sharded rest counts)
+        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0 && bidi_cfg.lite != 3;
         if (!lazy) launch_stages(stage_prev[0]);
         // b == nullptr (host batches): no event between the call's kernels (each costs ~6 us of
         // GPU idle between the launches it separates); one event after the last launch
@@ -4481,6 +4571,7 @@ struct ketogpu_engine {
         rs.unit_launches += launched;
         const uint64_t left = cnt[ns - 1];
         if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
+        if (bidi_cfg.lite == 3) label_calls++;  // the next call uses the other rest-counter set
         if (left && cur != 0)  // single requests for the global path, read from list[0]
             HIP_CHECK(hipMemcpyAsync(list[0], list[cur], left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
         return left;
@@ -4586,16 +4677,16 @@ struct ketogpu_engine {
     do {                                                                                                   \
         if (bidi_cfg.lite == 3 && label_pb == 16)                                                          \
             KLAUNCH((label_host_kernel<K, 16>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
-                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
+                    label_rest(q.n), st.stats, d_bad);                                                     \
         else if (bidi_cfg.lite == 3 && label_pb == 32)                                                     \
             KLAUNCH((label_host_kernel<K, 32>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
-                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
+                    label_rest(q.n), st.stats, d_bad);                                                     \
         else if (bidi_cfg.lite == 3)                                                                       \
             KLAUNCH((label_host_kernel<K, 64>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    gcore(), core_rec[0], core_rec[1], lgraph, src->roots, src->targets, io->d_roots,      \
-                    io->d_targets, q.n, q.allowed, list[0], &spill_count[0], st.stats, d_bad);              \
+                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
+                    label_rest(q.n), st.stats, d_bad);                                                     \
         else if (bidi_cfg.lite == 2 && core_shape == 1)                                                    \
             KLAUNCH((lite_host_kernel<K, CoreShapeS, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
                     0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \

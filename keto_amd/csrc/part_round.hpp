@@ -28,6 +28,13 @@ struct Comm {
     int rank = 0, world = 1;
     bool device = false;  // buffers are device memory of `dev` (RCCL) or host memory
     int dev = -1;
+    // KETOGPU_TEST_RCCL_SELF=1 when an RCCL communicator is made: even at world 1 every
+    // collective goes through RCCL (the own segment of an all-to-all as a grouped
+    // ncclSend/ncclRecv to the rank itself, the count gathers as ncclAllGather), so the
+    // data path a multi-GPU run takes is executed on one GPU
+    bool loop_self = false;
+    // RCCL calls made (ketogpu_comm_stats_get)
+    uint64_t n_send = 0, n_recv = 0, n_allgather = 0, n_allreduce = 0, bytes_sent = 0;
     virtual ~Comm() = default;
     // every rank's `bytes` bytes -> recv (world * bytes, in rank order)
     virtual void allgather(const void *send, void *recv, uint64_t bytes, hipStream_t s) = 0;

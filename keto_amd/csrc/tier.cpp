@@ -498,6 +498,12 @@ struct TierDevice : TierSteps {
             E.stats = d_small + kStats;
             E.first_bad = d_small + kFirstBad;
             if (recv) {
+                // seed bounds are u32 offsets into the received entries (tier_seed_kernel): a
+                // step past 2^32 entries fails on this rank (the code travels in the next
+                // status gather); a smaller ketogpu_tier_opts.max_batch splits it
+                if (nrecv >= (1ull << 32))
+                    throw Error(KETOGPU_ENOMEM, "two-tier: a step received 2^32 or more reply entries (" +
+                                                    std::to_string(nrecv) + "); lower max_batch");
                 uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
                 THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
                 tier::Rec *seed = (tier::Rec *)d_seed.ensure(sizeof(tier::Rec) * std::max<uint64_t>(nrecv, 1));
@@ -604,7 +610,7 @@ struct ketogpu_tier {
     // every rank's n u64 values -> mat (world * n, rank order)
     void gather(const uint64_t *v, size_t n) {
         mat.assign(n * world, 0);
-        if (!comm || world == 1) {  // a gather over one rank is the identity
+        if (!comm || (world == 1 && !comm->loop_self)) {  // a gather over one rank is the identity
             std::copy(v, v + n, mat.begin());
             return;
         }

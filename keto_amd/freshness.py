@@ -82,9 +82,11 @@ class VersionedEngine:
                 try:
                     sync_ms, rows = eng.sync()  # the patched device rows, before returning
                 except L.KetoError as err:
-                    self._recover(snap, err)
-                    self.last_write = dict(res, path="in_place+rebuild", sync_error=str(err),
-                                           ms=(time.perf_counter() - t0) * 1e3)
+                    failed = self._recover(snap, err)
+                    self.last_write = dict(res, path="in_place+rebuild" if failed is None else "in_place+failed",
+                                           sync_error=str(err), ms=(time.perf_counter() - t0) * 1e3)
+                    if failed is not None:
+                        self.last_write["engine_error"] = failed
                 else:
                     self.last_write = dict(res, path="in_place", sync_ms=sync_ms, synced_rows=rows,
                                            ms=(time.perf_counter() - t0) * 1e3)
@@ -99,13 +101,16 @@ class VersionedEngine:
         """the device sync of a committed in-place write failed: serve the written snapshot
         from a freshly built engine (a full upload of its rows).  If that fails too, the
         engine is left FAILED: every later read raises instead of answering from a device
-        copy that lacks the committed write."""
+        copy that lacks the committed write.  The transaction itself stands either way (it
+        is in the shared snapshot), so transact returns its version; returns None, or the
+        FAILED engine's error message"""
         try:
             self._install(snap.apply((), ()))
+            return None
         except L.KetoError as err2:
             self._state = (snap, _Failed(err, err2), expand.Engine(snap))
-            raise L.KetoError(err2.code, f"write committed, but no engine holds it: sync failed ({err}), "
-                                         f"rebuild failed ({err2}); checks raise until the next write") from err2
+            return (f"write committed, but no engine holds it: sync failed ({err}), rebuild failed ({err2}); "
+                    f"checks raise until the next write")
 
     def reload_namespaces(self, namespaces):
         """Keto's KeyNamespaces reload (internal/driver/config/provider.go:87-110): the next

@@ -235,6 +235,13 @@ class NativeComm:
     def handle(self):
         return self.h
 
+    def stats(self):
+        """RCCL calls this communicator made (ketogpu_comm_stats_get)"""
+        st = L.CommStats()
+        if self.h:
+            L.check(self.L.ketogpu_comm_stats_get(self.h, C.byref(st)))
+        return st.as_dict()
+
     def close(self):
         if getattr(self, "h", None):
             self.L.ketogpu_comm_free(self.h)

@@ -171,7 +171,8 @@ def test_failed_sync_after_in_place_write_still_commits(monkeypatch):
     """an in-place write is in the shared snapshot before the engine's device
     sync; a sync that raises must not turn into a failed transaction.  The engine is
     rebuilt over the written snapshot (version bumped, path reported); when the rebuild
-    fails as well, reads raise instead of answering without the committed write."""
+    fails as well, the transaction still returns its version and reads raise instead of
+    answering without the committed write."""
     from keto_amd import freshness
 
     built = []
@@ -203,9 +204,10 @@ def test_failed_sync_after_in_place_write_still_commits(monkeypatch):
     assert len(built) == 2 and built[-1].stats()["num_rows"] == 3  # rebuilt over the written rows
     StubEngine.fail_new = True
     t3 = rt.InternalRelationTuple("n", "g", "member", rt.SubjectID("u3"))
-    # the newest engine syncs fine; make the sync fail again and the rebuild fail too
-    with pytest.raises(L.KetoError, match="write committed"):
-        ve.transact(insert=[t3])
+    # the newest engine syncs fine; make the sync fail again and the rebuild fail too: the
+    # transaction is committed (its version is returned), the engine FAILED
+    assert ve.transact(insert=[t3]) == 2 and ve.version == 2
+    assert ve.last_write["path"] == "in_place+failed" and "write committed" in ve.last_write["engine_error"]
     assert ve.snapshot.stats()["num_rows"] == 4  # the write is committed in the snapshot
     with pytest.raises(L.KetoError, match="no engine holds"):
         ve.check_many([t3])

@@ -387,10 +387,14 @@ def test_wildcard_root_is_refused_not_answered_false():
 
 
 @pytest.mark.gpu
-def test_partition_device_rccl_world1_matches_oracle():
-    """the native round over a real RCCL communicator (nranks = 1: the records go through
-    grouped ncclSend/ncclRecv to itself, counts and bits through ncclAllGather), the id
-    exchange and request resolution over it too, every answer against the oracle"""
+@pytest.mark.parametrize("loop_self", [False, True])
+def test_partition_device_rccl_world1_matches_oracle(loop_self, monkeypatch):
+    """the native round over a real RCCL communicator of one rank (counts and bits through
+    ncclAllGather; the records' own segment a copy-engine DMA, or with
+    KETOGPU_TEST_RCCL_SELF=1 a grouped ncclSend/ncclRecv to the rank itself), the id exchange
+    and request resolution over it too, every answer against the oracle"""
+    if loop_self:
+        monkeypatch.setenv("KETOGPU_TEST_RCCL_SELF", "1")
     from keto_amd import synth
     from keto_amd.partition import NativeComm, PartitionedEngine, Shard
     if L.lib().ketogpu_device_count() < 1:
@@ -414,3 +418,6 @@ def test_partition_device_rccl_world1_matches_oracle():
     eng = PartitionedEngine(sh, device=0, direction="backward", comm=comm, record_capacity=4096)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     assert eng.retries > 0
+    cs = comm.stats()
+    assert cs["rccl"] == 1 and cs["allgathers"] > 0
+    assert (cs["sends"] > 0 and cs["recvs"] == cs["sends"]) if loop_self else cs["sends"] == 0

@@ -291,9 +291,16 @@ def randgraph_want(w):
 
 
 @pytest.mark.gpu
-def test_tier_device_rccl_world1_matches_oracle():
-    """a real RCCL communicator of one rank: the exchange path (queries and replies through
-    ncclSend/ncclRecv to itself, bounds from the received rows) against the oracle"""
+@pytest.mark.parametrize("loop_self", [False, True])
+def test_tier_device_rccl_world1_matches_oracle(loop_self, monkeypatch):
+    """a real RCCL communicator of one rank: the exchange path (queries, replies, seed
+    records from the received rows) against the oracle.  By default the own segment of each
+    all-to-all is a copy-engine DMA and the world-1 count gathers are skipped, so only the
+    loader's ncclAllGather runs over RCCL; with KETOGPU_TEST_RCCL_SELF=1 every exchange is a
+    grouped ncclSend/ncclRecv to the rank itself and every count gather an ncclAllGather —
+    the data path of a multi-GPU run, executed on one GPU (counted by the communicator)"""
+    if loop_self:
+        monkeypatch.setenv("KETOGPU_TEST_RCCL_SELF", "1")
     from keto_amd import synth
     from keto_amd.partition import NativeComm, Shard, TieredEngine
     _need_gpu()
@@ -310,6 +317,14 @@ def test_tier_device_rccl_world1_matches_oracle():
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     s = eng.stats()
     assert s["queries_sent"] > 0 and s["records_sent"] == s["records_received"] > 0
+    cs = comm.stats()
+    assert cs["rccl"] == 1 and cs["loop_self"] == int(loop_self) and cs["allgathers"] > 0
+    if loop_self:  # two all-to-alls (queries, replies) and their count gathers per step
+        steps = (len(roots) + 4095) // 4096
+        assert cs["sends"] >= 2 * steps and cs["recvs"] == cs["sends"] and cs["allgathers"] >= 2 * steps
+        assert cs["bytes_sent"] >= 8 * (s["queries_sent"] + s["records_sent"])
+    else:
+        assert cs["sends"] == 0 and cs["recvs"] == 0
 
 
 @pytest.mark.gpu
