@@ -1200,6 +1200,14 @@ __device__ __forceinline__ uint32_t block_scan_sh(uint32_t v, SH &S) {
     return total;
 }
 
+// one wave's LDS writes visible to its own later reads (a workgroup of several waves whose
+// waves work on their own data)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // wave-aggregated append to an LDS list: index of this lane's entry (all lanes call)
 __device__ __forceinline__ uint32_t lds_append(bool want, uint32_t *counter) {
     uint64_t bal = __ballot(want);
@@ -2536,13 +2544,15 @@ __device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
     return pos < 63 && S[pos + 1] == x;
 }
 
-template <int PB>
+// WS: the unit's wave shares its workgroup with other waves (label_host_pkernel), so its
+// own LDS hand-offs are wave-level
+template <int PB, bool WS = false>
 __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
                                            uint64_t *allowed, const uint64_t unit, const LabelRest &R,
                                            unsigned long long *stats) {
     static_assert(PB == 16 || PB == 32 || PB == 64, "P blocks of 16, 32 or 64 words");
     constexpr int PW = PB / 4;  // P words per lane
-    const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
+    const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
     const bool valid = some && r < kDynBase;
@@ -2586,7 +2596,10 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L,
         const uint32_t at = lds_append(rest, R.count + shard * kRestStride);
         if (rest) R.list[shard * R.cap + at] = (uint32_t)(unit * 16 + q);
     }
-    __syncthreads();
+    if constexpr (WS)
+        wave_sync();
+    else
+        __syncthreads();
     const uint32_t np = (uint32_t)__shfl((int)pw[0], (int)(lane & ~3u), 64);
     const uint32_t ovf = (uint32_t)__shfl((int)pw[1], (int)(lane & ~3u), 64);
     bool hit = false;
@@ -2661,6 +2674,73 @@ __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
         label_unit<PB>(sh, L, rk, tk, allowed, unit, R, stats);
+        __syncthreads();
+    }
+}
+
+// Host batches, persistent: one LOADER wave per workgroup reads the next group's requests
+// (kLabelC units) from pinned host memory over PCIe, validates them and leaves them in LDS,
+// while kLabelC CONSUMER waves answer the current group's units; one workgroup barrier per
+// group.  The consumers never have a PCIe read outstanding, so their waits on the label
+// blocks never wait for one (vector-memory counters retire in issue order); the PCIe link
+// stays busy for the whole launch instead of in bursts at each workgroup's start.
+constexpr int kLabelC = 7;  // consumer waves per workgroup (+ 1 loader: 8 waves, 4 workgroups per CU)
+template <int PB>
+__global__ __launch_bounds__(64 * (kLabelC + 1)) void label_host_pkernel(DevGraph g, LabelGraph L, const uint32_t *hr,
+                                                                         const uint32_t *ht, uint32_t *dr,
+                                                                         uint32_t *dt, uint64_t n, uint64_t *allowed,
+                                                                         LabelRest R, unsigned long long *stats,
+                                                                         unsigned long long *first_bad) {
+    __shared__ LabelShared sh[kLabelC];
+    __shared__ uint32_t ring[2][2][kLabelC * 16];  // [stage][roots, targets][request of the group]
+    constexpr uint32_t GR = kLabelC * 16;         // requests per group
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t groups = (n + GR - 1) / GR, units = (n + 15) / 16;
+    if (blockIdx.x == 0 && wave == 0) R.next_count[lane * kRestStride] = 0u;  // the next call's counters
+    // the loader: group gi's requests into ring[st] (ids outside the snapshot: first_bad,
+    // NONE), the validated ids to HBM for the spill stages
+    auto load = [&](uint64_t gi, int st) {
+        const uint64_t base = gi * GR;
+        uint32_t r[2], t[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // all four reads in flight at once
+            const uint32_t j = lane + 64 * h;
+            r[h] = t[h] = KETOGPU_NODE_NONE;
+            if (j < GR && base + j < n) {
+                r[h] = hr[base + j];
+                t[h] = ht[base + j];
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t j = lane + 64 * h;
+            if (j >= GR) continue;
+            if (base + j < n) {
+                if ((r[h] != KETOGPU_NODE_NONE && r[h] >= g.Nx) || (t[h] != KETOGPU_NODE_NONE && t[h] >= g.N)) {
+                    atomicMin(first_bad, (unsigned long long)(base + j));
+                    r[h] = t[h] = KETOGPU_NODE_NONE;
+                }
+                dr[base + j] = r[h];
+                dt[base + j] = t[h];
+            }
+            ring[st][0][j] = r[h];
+            ring[st][1][j] = t[h];
+        }
+    };
+    uint64_t gi = blockIdx.x;
+    if (wave == kLabelC && gi < groups) load(gi, 0);
+    __syncthreads();
+    for (int st = 0; gi < groups; gi += gridDim.x, st ^= 1) {
+        if (wave == kLabelC) {
+            if (gi + gridDim.x < groups) load(gi + gridDim.x, st ^ 1);
+        } else {
+            const uint64_t unit = gi * kLabelC + wave;
+            if (unit < units) {
+                const uint32_t r = lane < 16 ? ring[st][0][wave * 16 + lane] : KETOGPU_NODE_NONE;
+                const uint32_t t = lane < 16 ? ring[st][1][wave * 16 + lane] : KETOGPU_NODE_NONE;
+                label_unit<PB, true>(sh[wave], L, r, t, allowed, unit, R, stats);
+            }
+        }
         __syncthreads();
     }
 }
@@ -3165,11 +3245,6 @@ __global__ __launch_bounds__(kBlock) void stats_reduce_kernel(const unsigned lon
 // Same algorithm as unit_kernel with ONE WAVE per unit: the four waves of a workgroup
 // own four independent LDS partitions, so a BFS level needs no workgroup barrier, only
 // in-order wave execution (wave_sync orders the LDS traffic between phases).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int U, int HLOG>
 struct WaveLDS {
@@ -3702,6 +3777,24 @@ struct ketogpu_engine {
     }
     uint32_t label_pb = 32;
     double label_coverage = 0, label_build_ms = 0;
+    // plan label, host batches: the persistent loader/consumer kernel (KETOGPU_LABEL_PERSIST=0:
+    // the one-workgroup-per-units kernel, host_units units each)
+    bool label_persist = true;
+    int n_cu = 256;
+    void launch_label_persist(const Batch &q, const HostSrc *src) {
+        const uint64_t groups = (q.n + 16 * kLabelC - 1) / (16 * kLabelC);
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)n_cu * 4));
+#define KETO_LP(PB)                                                                                           \
+    KLAUNCH((label_host_pkernel<PB>), dim3(grid), dim3(64 * (kLabelC + 1)), 0, stream, g, lgraph, src->roots, \
+            src->targets, io->d_roots, io->d_targets, q.n, q.allowed, label_rest(q.n), st.stats, d_bad)
+        if (label_pb == 16)
+            KETO_LP(16);
+        else if (label_pb == 32)
+            KETO_LP(32);
+        else
+            KETO_LP(64);
+#undef KETO_LP
+    }
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
     uint64_t closure_nodes[2] = {0, 0}, closure_entries[2] = {0, 0};
     double core_build_ms = 0;
@@ -4098,6 +4191,8 @@ struct ketogpu_engine {
         use_label = (p == "label" || p == "auto") && use_core && getenv("KETOGPU_NO_LABEL") == nullptr;
         if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
         if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
+        if (const char *e = getenv("KETOGPU_LABEL_PERSIST")) label_persist = atoi(e) != 0;
+        HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
         if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
         use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && small_f && small_r;
         if (use_v2 && !small_f) {
@@ -4675,6 +4770,10 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
+        if (bidi_cfg.lite == 3 && label_persist) {                                                         \
+            launch_label_persist(q, src);                                                                  \
+            break;                                                                                         \
+        }                                                                                                  \
         if (bidi_cfg.lite == 3 && label_pb == 16)                                                          \
             KLAUNCH((label_host_kernel<K, 16>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
                     g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \

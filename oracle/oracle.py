@@ -330,7 +330,7 @@ def r2_lib():
         L.kr_add_requests.argtypes = [vp, C.c_size_t] + [vp] * 8
         L.kr_add_rows_columnar.argtypes = [vp, C.c_size_t] + [vp] * 13
         L.kr_finish.argtypes = [vp]
-        L.kr_check.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_uint64)]
+        L.kr_check.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_uint64), vp]
         L.kr_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.kr_error.restype = C.c_char_p
         L.kr_error.argtypes = [vp]
@@ -383,8 +383,10 @@ class R2Checker:
         allowed = np.zeros(max(self.n, 1), dtype=np.uint8)
         status = np.zeros(max(self.n, 1), dtype=np.int32)
         visits = C.c_uint64()
-        self.L.kr_check(self.h, nthreads, allowed.ctypes.data, status.ctypes.data, C.byref(visits))
+        closure = np.zeros(max(self.n, 1), dtype=np.uint64)
+        self.L.kr_check(self.h, nthreads, allowed.ctypes.data, status.ctypes.data, C.byref(visits), closure.ctypes.data)
         self.edge_visits = visits.value
+        self.closure_size = closure[:self.n]  # per request: the interior nodes its root reaches
         return allowed[:self.n].astype(bool), status[:self.n] == 0
 
     def stats(self):

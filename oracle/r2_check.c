@@ -370,6 +370,7 @@ int kr_finish(kr_checker *k) {
 typedef struct {
     kr_checker *k;
     uint8_t *allowed;
+    uint64_t *closure; /* NULL, or per request |X(r)| (the interior closure the check walked) */
     atomic_size_t next;
     atomic_ullong visits;
 } job_t;
@@ -433,6 +434,9 @@ static void *worker(void *arg) {
             }
             j->allowed[i] = a;
         }
+        if (j->closure)
+            for (size_t t = 0; t < nt; t++)
+                for (uint64_t m = vis[touched[t]]; m; m &= m - 1) j->closure[i0 + (size_t)__builtin_ctzll(m)]++;
         for (size_t t = 0; t < nt; t++) vis[touched[t]] = 0;
     }
     atomic_fetch_add(&j->visits, visits);
@@ -444,9 +448,11 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-int kr_check(kr_checker *k, int nthreads, uint8_t *allowed, int *status, uint64_t *edge_visits) {
+int kr_check(kr_checker *k, int nthreads, uint8_t *allowed, int *status, uint64_t *edge_visits,
+             uint64_t *closure_size) {
     if (!k->finished) return KR_EREFUSED;
-    job_t j = {.k = k, .allowed = allowed};
+    job_t j = {.k = k, .allowed = allowed, .closure = closure_size};
+    if (closure_size) memset(closure_size, 0, k->n * sizeof *closure_size);
     atomic_init(&j.next, 0);
     atomic_init(&j.visits, 0);
     memset(allowed, 0, k->n);

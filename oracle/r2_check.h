@@ -30,7 +30,9 @@ int kr_add_rows_columnar(kr_checker *k, size_t n, const int32_t *ns, const char 
                          const char *ss_rel, const uint64_t *ss_rel_off);
 int kr_finish(kr_checker *k);
 /* allowed[n] 0/1, status[n] KR_OK or KR_EREFUSED; *edge_visits: subject-set edges scanned */
-int kr_check(kr_checker *k, int nthreads, uint8_t *allowed, int *status, uint64_t *edge_visits);
+/* closure_size: NULL, or per request the number of interior nodes its root reaches (|X(r)|) */
+int kr_check(kr_checker *k, int nthreads, uint8_t *allowed, int *status, uint64_t *edge_visits,
+             uint64_t *closure_size);
 void kr_stats(const kr_checker *k, uint64_t *nodes, uint64_t *edges);
 const char *kr_error(const kr_checker *k);
 void kr_free(kr_checker *k);
