@@ -1841,11 +1841,26 @@ template <int K>
 __device__ __forceinline__ void host_unit_requests(const DevGraph &g, const uint32_t *hr, const uint32_t *ht,
                                                    uint32_t *dr, uint32_t *dt, uint64_t n,
                                                    unsigned long long *first_bad, uint32_t (&r)[K], uint32_t (&t)[K]) {
-    static_assert(K == 1 || K == 2 || K == 4, "1, 2 or 4 units per workgroup");
+    static_assert(K == 1 || K == 2 || K == 4 || K == 8, "1, 2, 4 or 8 units per workgroup");
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * K * 16;
-    uint32_t vr = KETOGPU_NODE_NONE, vt = KETOGPU_NODE_NONE;
-    if constexpr (K == 4) {
+    uint32_t vr = KETOGPU_NODE_NONE, vt = KETOGPU_NODE_NONE, vr2 = KETOGPU_NODE_NONE, vt2 = KETOGPU_NODE_NONE;
+    if constexpr (K == 8) {  // 128 roots, 128 targets: 8 bytes per lane, one instruction each
+        const uint64_t c = base + 2 * lane;
+        const bool aligned = (((uintptr_t)hr | (uintptr_t)ht) & 7) == 0;  // a caller's arrays may be 4-aligned
+        if (c + 1 < n && aligned) {
+            const uint2 a = reinterpret_cast<const uint2 *>(hr + base)[lane];  // base is a multiple of 128
+            const uint2 b = reinterpret_cast<const uint2 *>(ht + base)[lane];
+            vr = a.x, vr2 = a.y, vt = b.x, vt2 = b.y;
+        } else if (c < n) {
+            vr = hr[c];
+            vt = ht[c];
+            if (c + 1 < n) {
+                vr2 = hr[c + 1];
+                vt2 = ht[c + 1];
+            }
+        }
+    } else if constexpr (K == 4) {
         if (base + lane < n) {
             vr = hr[base + lane];
             vt = ht[base + lane];
@@ -1857,8 +1872,15 @@ __device__ __forceinline__ void host_unit_requests(const DevGraph &g, const uint
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const int src = 16 * k + (int)(lane & 15);
-        r[k] = (uint32_t)__shfl((int)vr, src, 64);
-        t[k] = (uint32_t)__shfl((int)(K == 4 ? vt : vr), K == 4 ? src : 32 + src, 64);
+        if constexpr (K == 8) {  // request i sits in lane i / 2, word i % 2
+            const uint32_t a0 = (uint32_t)__shfl((int)vr, src >> 1, 64), a1 = (uint32_t)__shfl((int)vr2, src >> 1, 64);
+            const uint32_t b0 = (uint32_t)__shfl((int)vt, src >> 1, 64), b1 = (uint32_t)__shfl((int)vt2, src >> 1, 64);
+            r[k] = src & 1 ? a1 : a0;
+            t[k] = src & 1 ? b1 : b0;
+        } else {
+            r[k] = (uint32_t)__shfl((int)vr, src, 64);
+            t[k] = (uint32_t)__shfl((int)(K == 4 ? vt : vr), K == 4 ? src : 32 + src, 64);
+        }
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -2762,7 +2784,8 @@ __global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *
     const uint32_t nu = (c + 15) / 16;
     const uint32_t incl = wave_incl_sum_u32(nu);
     const uint64_t units = (uint64_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (blockIdx.x == 0 && lane == 0) *total = (unsigned int)wave_sum_all(c);  // the host reads the total here
+    const uint32_t listed = wave_sum_all(c);  // (every lane: a wave-wide reduction)
+    if (blockIdx.x == 0 && lane == 0) *total = listed;  // the host reads the total here (grid of the next call)
     for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
         // the shard holding gathered unit u: the first whose inclusive prefix passes u
         const uint32_t shard = (uint32_t)__builtin_ctzll(__ballot(incl > u));
@@ -3779,7 +3802,9 @@ struct ketogpu_engine {
     double label_coverage = 0, label_build_ms = 0;
     // plan label, host batches: the persistent loader/consumer kernel (KETOGPU_LABEL_PERSIST=0:
     // the one-workgroup-per-units kernel, host_units units each)
-    bool label_persist = true;
+    // measured: persistent 0.209 vs K = 4 wide reads 0.172 ms per 10^6 config #2 requests
+    // (profiles/r04/ab_label5): the one-launch kernel is already at ~47 GB/s of PCIe reads
+    bool label_persist = false;
     int n_cu = 256;
     void launch_label_persist(const Batch &q, const HostSrc *src) {
         const uint64_t groups = (q.n + 16 * kLabelC - 1) / (16 * kLabelC);
@@ -4030,7 +4055,10 @@ struct ketogpu_engine {
     // pinned requests read in place by one first-stage launch (bidi_host_kernel);
     // KETOGPU_PIPE_MODE=chunks restores the chunk pipeline (load_kernel + a launch per chunk)
     bool pipe_direct = true;
-    int host_units = 2;  // units per workgroup of bidi_host_kernel (KETOGPU_HOST_UNITS: 1, 2 or 4)
+    // units per workgroup of the host-batch first stage (KETOGPU_HOST_UNITS: 1, 2 or 4; 0 = the
+    // plan's: 4 for plan label — its units are short, so its PCIe reads bound the launch and
+    // wider ones pay (0.172 vs 0.204 ms per 10^6 requests, profiles/r04/ab_label2..5) — else 2)
+    int host_units = 0;
     bool light_events = true;           // host batches: timing events only around the whole call
     hipEvent_t light_begin = nullptr;   // that call's begin event (run_once -> run_units)
     uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
@@ -4811,9 +4839,12 @@ struct ketogpu_engine {
                     frec, brec, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
                     list[0], &spill_count[0], st.stats, d_bad);                                            \
     } while (0)
-                    if (host_units == 4)
+                    const int hk = host_units ? host_units : bidi_cfg.lite == 3 ? 4 : 2;
+                    if (hk == 8 && bidi_cfg.lite == 3)
+                        KETO_HOST_K(8);
+                    else if (hk == 4)
                         KETO_HOST_K(4);
-                    else if (host_units == 2)
+                    else if (hk == 2)
                         KETO_HOST_K(2);
                     else
                         KETO_HOST_K(1);
