@@ -243,19 +243,19 @@ void ketogpu_core_index_free(ketogpu_core_index *c);
  * interior entries, P blocks per expandable r = {r} + fint(r); mode 1 (F): S blocks per
  * expandable r = {r} + fint(r) + their forward closures, P blocks per node t = rev(t);
  * mode -1: the better-covered one (view mode -1 when neither labels half its nodes).
- * allowed(r, t) <=> the request's P list and S list share a node.  S blocks: 64 u32
- * [count (0xFFFFFFFF: no label), entries ascending, 0xFFFFFFFF padding]; P blocks: pb u32
+ * allowed(r, t) <=> the request's P list and S list share a node.  S blocks: s_words u32
+ * (64 or 128) [count (0xFFFFFFFF: no label), entries ascending, 0xFFFFFFFF padding]; P blocks: pb u32
  * [count, overflow start / 16, entries...], entries past pb - 2 at words overflow*16... */
 typedef struct ketogpu_label_index ketogpu_label_index;
 typedef struct {
     int32_t mode;
-    uint32_t p_block_words;
+    uint32_t s_block_words, p_block_words;
     const uint32_t *p_words, *s_words;
     uint64_t num_p_words, num_s_words;
     uint64_t p_nodes, s_nodes, labelled, nonempty;
     double coverage_b, coverage_f; /* sampled labelled shares of both modes */
 } ketogpu_label_view;
-int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode,
+int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode, uint32_t s_words,
                               ketogpu_label_index **out);
 int ketogpu_label_index_view(const ketogpu_label_index *l, ketogpu_label_view *out);
 void ketogpu_label_index_free(ketogpu_label_index *l);
@@ -437,6 +437,7 @@ typedef struct {
     int32_t label_mode;         /* 0 backward labels, 1 forward labels, -1 off         */
     double label_coverage;      /* labelled share of the label nodes with a non-empty row */
     double label_build_ms;
+    uint32_t label_words;       /* S block words (64 / 128: labels of <= 63 / 127 nodes) */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 /* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory) record a

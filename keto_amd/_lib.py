@@ -103,7 +103,7 @@ class RunStats(C.Structure):
         ("plan_unit", C.c_uint32), ("closure_cap_f", C.c_uint32), ("closure_cap_b", C.c_uint32),
         ("closure_nodes_f", C.c_uint64), ("closure_nodes_b", C.c_uint64), ("closure_entries_f", C.c_uint64),
         ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double), ("label_mode", C.c_int32),
-        ("label_coverage", C.c_double), ("label_build_ms", C.c_double)]
+        ("label_coverage", C.c_double), ("label_build_ms", C.c_double), ("label_words", C.c_uint32)]
 
     PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core", 7: "label"}
 
@@ -147,7 +147,8 @@ class CoreRecords(C.Structure):
 
 
 class LabelView(C.Structure):
-    _fields_ = [("mode", C.c_int32), ("p_block_words", C.c_uint32), ("p_words", C.POINTER(C.c_uint32)),
+    _fields_ = [("mode", C.c_int32), ("s_block_words", C.c_uint32), ("p_block_words", C.c_uint32),
+                ("p_words", C.POINTER(C.c_uint32)),
                 ("s_words", C.POINTER(C.c_uint32)), ("num_p_words", C.c_uint64), ("num_s_words", C.c_uint64),
                 ("p_nodes", C.c_uint64), ("s_nodes", C.c_uint64), ("labelled", C.c_uint64), ("nonempty", C.c_uint64),
                 ("coverage_b", C.c_double), ("coverage_f", C.c_double)]
@@ -308,7 +309,7 @@ SIGNATURES = {
     "ketogpu_core_index_view": (C.c_int, [vp, C.c_int, C.POINTER(CoreRecords)]),
     "ketogpu_core_index_free": (None, [vp]),
     "ketogpu_comm_stats_get": (C.c_int, [vp, C.POINTER(CommStats)]),
-    "ketogpu_label_index_build": (C.c_int, [vp, C.POINTER(u32), C.c_int, C.POINTER(vp)]),
+    "ketogpu_label_index_build": (C.c_int, [vp, C.POINTER(u32), C.c_int, u32, C.POINTER(vp)]),
     "ketogpu_label_index_view": (C.c_int, [vp, C.POINTER(LabelView)]),
     "ketogpu_label_index_free": (None, [vp]),
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),

@@ -1841,26 +1841,11 @@ template <int K>
 __device__ __forceinline__ void host_unit_requests(const DevGraph &g, const uint32_t *hr, const uint32_t *ht,
                                                    uint32_t *dr, uint32_t *dt, uint64_t n,
                                                    unsigned long long *first_bad, uint32_t (&r)[K], uint32_t (&t)[K]) {
-    static_assert(K == 1 || K == 2 || K == 4 || K == 8, "1, 2, 4 or 8 units per workgroup");
+    static_assert(K == 1 || K == 2 || K == 4, "1, 2 or 4 units per workgroup");
     const uint32_t lane = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * K * 16;
-    uint32_t vr = KETOGPU_NODE_NONE, vt = KETOGPU_NODE_NONE, vr2 = KETOGPU_NODE_NONE, vt2 = KETOGPU_NODE_NONE;
-    if constexpr (K == 8) {  // 128 roots, 128 targets: 8 bytes per lane, one instruction each
-        const uint64_t c = base + 2 * lane;
-        const bool aligned = (((uintptr_t)hr | (uintptr_t)ht) & 7) == 0;  // a caller's arrays may be 4-aligned
-        if (c + 1 < n && aligned) {
-            const uint2 a = reinterpret_cast<const uint2 *>(hr + base)[lane];  // base is a multiple of 128
-            const uint2 b = reinterpret_cast<const uint2 *>(ht + base)[lane];
-            vr = a.x, vr2 = a.y, vt = b.x, vt2 = b.y;
-        } else if (c < n) {
-            vr = hr[c];
-            vt = ht[c];
-            if (c + 1 < n) {
-                vr2 = hr[c + 1];
-                vt2 = ht[c + 1];
-            }
-        }
-    } else if constexpr (K == 4) {
+    uint32_t vr = KETOGPU_NODE_NONE, vt = KETOGPU_NODE_NONE;
+    if constexpr (K == 4) {
         if (base + lane < n) {
             vr = hr[base + lane];
             vt = ht[base + lane];
@@ -1872,15 +1857,8 @@ __device__ __forceinline__ void host_unit_requests(const DevGraph &g, const uint
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const int src = 16 * k + (int)(lane & 15);
-        if constexpr (K == 8) {  // request i sits in lane i / 2, word i % 2
-            const uint32_t a0 = (uint32_t)__shfl((int)vr, src >> 1, 64), a1 = (uint32_t)__shfl((int)vr2, src >> 1, 64);
-            const uint32_t b0 = (uint32_t)__shfl((int)vt, src >> 1, 64), b1 = (uint32_t)__shfl((int)vt2, src >> 1, 64);
-            r[k] = src & 1 ? a1 : a0;
-            t[k] = src & 1 ? b1 : b0;
-        } else {
-            r[k] = (uint32_t)__shfl((int)vr, src, 64);
-            t[k] = (uint32_t)__shfl((int)(K == 4 ? vt : vr), K == 4 ? src : 32 + src, 64);
-        }
+        r[k] = (uint32_t)__shfl((int)vr, src, 64);
+        t[k] = (uint32_t)__shfl((int)(K == 4 ? vt : vr), K == 4 ? src : 32 + src, 64);
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -2538,7 +2516,7 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 // request index each) for the second stage, label_rest_kernel: plan core's traversal over
 // the listed requests, gathered 16 to a unit.
 struct LabelGraph {
-    const uint32_t *P, *S;  // P blocks (+ overflow), S blocks (kLabelWords words each)
+    const uint32_t *P, *S;  // P blocks (+ overflow), S blocks (SW words each)
     int mode;               // 0 = B (S node t, P node r), 1 = F (S node r, P node t)
 };
 // The unlabelled requests' list is sharded: unit u appends to region u % kRestShards of
@@ -2552,27 +2530,34 @@ struct LabelRest {
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
 };
-constexpr int kLabelStride = 65;  // LDS words per request's S list (odd: the 16 lists start in different banks)
+// A request's S list in LDS: the first LW words of its S block (LW + 1 words a request,
+// odd: the 16 lists start in different banks).  LW < SW (label_kernel over 128-word S
+// blocks): a label of more than LW - 1 nodes (rare) is searched in place in its block (L2)
+// instead, so label_kernel keeps the LDS footprint, and the occupancy, of 64-word blocks
+// (0.055 vs 0.095 ms per 10^6 config #2 requests); the PCIe-bound host kernel keeps whole
+// labels in LDS (LW = SW: no dependent L2 reads behind the request reads, 0.172 vs 0.190 ms)
+template <int LW>
 struct LabelShared {
-    uint32_t S[16 * kLabelStride];
+    uint32_t S[16 * (LW + 1)];
 };
 
-// number of S entries (words 1..63, ascending, padded with 0xFFFFFFFF) below x, then x found
+// number of S entries (words 1..SW-1, ascending, padded with 0xFFFFFFFF) below x, then x found
+template <int SW>
 __device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
     uint32_t pos = 0;
 #pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
+    for (uint32_t step = SW / 2; step; step >>= 1)
         if (S[pos + step] < x) pos += step;
-    return pos < 63 && S[pos + 1] == x;
+    return pos < SW - 1 && S[pos + 1] == x;
 }
 
-// WS: the unit's wave shares its workgroup with other waves (label_host_pkernel), so its
-// own LDS hand-offs are wave-level
-template <int PB, bool WS = false>
-__device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
+template <int PB, int SW, int LW>
+__device__ __forceinline__ void label_unit(LabelShared<LW> &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
                                            uint64_t *allowed, const uint64_t unit, const LabelRest &R,
                                            unsigned long long *stats) {
     static_assert(PB == 16 || PB == 32 || PB == 64, "P blocks of 16, 32 or 64 words");
+    static_assert(SW == 64 || SW == 128, "S blocks of 64 or 128 words");
+    static_assert(LW == 64 || LW == SW, "LDS lists of 64 words or whole blocks");
     constexpr int PW = PB / 4;  // P words per lane
     const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
@@ -2585,7 +2570,7 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L,
 #pragma unroll
     for (int k = 0; k < PW; k++) pw[k] = 0u;
     if (valid) {  // both blocks in flight at once: one dependent HBM read per request
-        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * kLabelWords) + 2 * sub;
+        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * SW) + 2 * sub;
         const uint4 *pb = reinterpret_cast<const uint4 *>(L.P + (uint64_t)xp * PB) + (PW / 4) * sub;
         const uint4 a = sb[0], b = sb[1];
         sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
@@ -2595,22 +2580,29 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L,
             pw[4 * k] = c.x, pw[4 * k + 1] = c.y, pw[4 * k + 2] = c.z, pw[4 * k + 3] = c.w;
         }
     }
-    uint32_t *S = sh.S + q * kLabelStride;
+    uint32_t *S = sh.S + q * (LW + 1);
     if (!valid && sub == 0) sw[0] = some ? kNoLabel : 0u;  // a wildcard root: no label; an id NONE: empty
 #pragma unroll
     for (int k = 0; k < 8; k++) S[8 * sub + k] = sw[k];
     const uint32_t ns = (uint32_t)__shfl((int)sw[0], (int)(lane & ~3u), 64);  // the label's count
     const bool labelled = valid && ns != kNoLabel;
-    if (labelled && ns > 31) {  // entries 32..63: the block's second line
-        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * kLabelWords + 32) + 2 * sub;
-        const uint4 a = sb[0], b = sb[1];
-        sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
-    } else {
+    // the block's further lines (words 32p..32p+31) only for a label of more than 32p - 1
+    // nodes; a label past the LDS list is searched in its block instead
+    const bool wide = LW < SW && labelled && ns > LW - 1;
 #pragma unroll
-        for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
+    for (int part = 1; part < LW / 32; part++) {
+        if (labelled && ns > 32 * part - 1 && !wide) {
+            const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * SW + 32 * part) + 2 * sub;
+            const uint4 a = sb[0], b = sb[1];
+            sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) S[32 * part + 8 * sub + k] = sw[k];
     }
-#pragma unroll
-    for (int k = 0; k < 8; k++) S[32 + 8 * sub + k] = sw[k];
+    const uint32_t *Sg = L.S + (uint64_t)xs * SW;
     // a request without a label (or with a wildcard root): listed for the second stage
     {
         const bool rest = sub == 0 && some && !labelled;
@@ -2618,10 +2610,7 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L,
         const uint32_t at = lds_append(rest, R.count + shard * kRestStride);
         if (rest) R.list[shard * R.cap + at] = (uint32_t)(unit * 16 + q);
     }
-    if constexpr (WS)
-        wave_sync();
-    else
-        __syncthreads();
+    __syncthreads();
     const uint32_t np = (uint32_t)__shfl((int)pw[0], (int)(lane & ~3u), 64);
     const uint32_t ovf = (uint32_t)__shfl((int)pw[1], (int)(lane & ~3u), 64);
     bool hit = false;
@@ -2631,13 +2620,14 @@ __device__ __forceinline__ void label_unit(LabelShared &sh, const LabelGraph &L,
         for (int k = 0; k < PW; k++) {
             const uint32_t w = PW * sub + k;  // the entry of word w is entry w - 2
             if (w >= 2 && w - 2 < np) {
-                hit |= label_find(S, pw[k]);
+                hit |= wide ? label_find<SW>(Sg, pw[k]) : label_find<LW>(S, pw[k]);
                 looked++;
             }
         }
         if (np > (uint32_t)PB - 2)  // the row's entries past its block
             for (uint32_t k = PB - 2 + sub; k < np; k += 4) {
-                hit |= label_find(S, L.P[(uint64_t)ovf * 16 + (k - (PB - 2))]);
+                const uint32_t x = L.P[(uint64_t)ovf * 16 + (k - (PB - 2))];
+                hit |= wide ? label_find<SW>(Sg, x) : label_find<LW>(S, x);
                 looked++;
             }
     }
@@ -2663,26 +2653,26 @@ __device__ __forceinline__ void label_clear_next(const LabelRest &R) {
     if (blockIdx.x == 0) R.next_count[threadIdx.x * kRestStride] = 0u;  // 64 lanes: every shard
 }
 
-template <int PB>
+template <int PB, int SW>
 __global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t *roots, const uint32_t *targets,
                                                    uint64_t n, uint64_t *allowed, LabelRest R,
                                                    unsigned long long *stats, uint64_t unit0) {
-    __shared__ LabelShared sh;
+    __shared__ LabelShared<64> sh;
     if (unit0 == 0) label_clear_next(R);
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
-    label_unit<PB>(sh, L, r, t, allowed, unit, R, stats);
+    label_unit<PB, SW, 64>(sh, L, r, t, allowed, unit, R, stats);
 }
 
 // pinned host requests read in place (host_unit_requests)
-template <int K, int PB>
+template <int K, int PB, int SW>
 __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L, const uint32_t *hr,
                                                         const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
                                                         uint64_t *allowed, LabelRest R, unsigned long long *stats,
                                                         unsigned long long *first_bad) {
-    __shared__ LabelShared sh;
+    __shared__ LabelShared<SW> sh;
     label_clear_next(R);
     uint32_t r[K], t[K];
     host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
@@ -2695,74 +2685,7 @@ __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        label_unit<PB>(sh, L, rk, tk, allowed, unit, R, stats);
-        __syncthreads();
-    }
-}
-
-// Host batches, persistent: one LOADER wave per workgroup reads the next group's requests
-// (kLabelC units) from pinned host memory over PCIe, validates them and leaves them in LDS,
-// while kLabelC CONSUMER waves answer the current group's units; one workgroup barrier per
-// group.  The consumers never have a PCIe read outstanding, so their waits on the label
-// blocks never wait for one (vector-memory counters retire in issue order); the PCIe link
-// stays busy for the whole launch instead of in bursts at each workgroup's start.
-constexpr int kLabelC = 7;  // consumer waves per workgroup (+ 1 loader: 8 waves, 4 workgroups per CU)
-template <int PB>
-__global__ __launch_bounds__(64 * (kLabelC + 1)) void label_host_pkernel(DevGraph g, LabelGraph L, const uint32_t *hr,
-                                                                         const uint32_t *ht, uint32_t *dr,
-                                                                         uint32_t *dt, uint64_t n, uint64_t *allowed,
-                                                                         LabelRest R, unsigned long long *stats,
-                                                                         unsigned long long *first_bad) {
-    __shared__ LabelShared sh[kLabelC];
-    __shared__ uint32_t ring[2][2][kLabelC * 16];  // [stage][roots, targets][request of the group]
-    constexpr uint32_t GR = kLabelC * 16;         // requests per group
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t groups = (n + GR - 1) / GR, units = (n + 15) / 16;
-    if (blockIdx.x == 0 && wave == 0) R.next_count[lane * kRestStride] = 0u;  // the next call's counters
-    // the loader: group gi's requests into ring[st] (ids outside the snapshot: first_bad,
-    // NONE), the validated ids to HBM for the spill stages
-    auto load = [&](uint64_t gi, int st) {
-        const uint64_t base = gi * GR;
-        uint32_t r[2], t[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {  // all four reads in flight at once
-            const uint32_t j = lane + 64 * h;
-            r[h] = t[h] = KETOGPU_NODE_NONE;
-            if (j < GR && base + j < n) {
-                r[h] = hr[base + j];
-                t[h] = ht[base + j];
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t j = lane + 64 * h;
-            if (j >= GR) continue;
-            if (base + j < n) {
-                if ((r[h] != KETOGPU_NODE_NONE && r[h] >= g.Nx) || (t[h] != KETOGPU_NODE_NONE && t[h] >= g.N)) {
-                    atomicMin(first_bad, (unsigned long long)(base + j));
-                    r[h] = t[h] = KETOGPU_NODE_NONE;
-                }
-                dr[base + j] = r[h];
-                dt[base + j] = t[h];
-            }
-            ring[st][0][j] = r[h];
-            ring[st][1][j] = t[h];
-        }
-    };
-    uint64_t gi = blockIdx.x;
-    if (wave == kLabelC && gi < groups) load(gi, 0);
-    __syncthreads();
-    for (int st = 0; gi < groups; gi += gridDim.x, st ^= 1) {
-        if (wave == kLabelC) {
-            if (gi + gridDim.x < groups) load(gi + gridDim.x, st ^ 1);
-        } else {
-            const uint64_t unit = gi * kLabelC + wave;
-            if (unit < units) {
-                const uint32_t r = lane < 16 ? ring[st][0][wave * 16 + lane] : KETOGPU_NODE_NONE;
-                const uint32_t t = lane < 16 ? ring[st][1][wave * 16 + lane] : KETOGPU_NODE_NONE;
-                label_unit<PB, true>(sh[wave], L, r, t, allowed, unit, R, stats);
-            }
-        }
+        label_unit<PB, SW, SW>(sh, L, rk, tk, allowed, unit, R, stats);
         __syncthreads();
     }
 }
@@ -3798,27 +3721,30 @@ struct ketogpu_engine {
         return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
                          rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
     }
-    uint32_t label_pb = 32;
+    uint32_t label_pb = 32, label_sw = 64;
     double label_coverage = 0, label_build_ms = 0;
-    // plan label, host batches: the persistent loader/consumer kernel (KETOGPU_LABEL_PERSIST=0:
-    // the one-workgroup-per-units kernel, host_units units each)
-    // measured: persistent 0.209 vs K = 4 wide reads 0.172 ms per 10^6 config #2 requests
-    // (profiles/r04/ab_label5): the one-launch kernel is already at ~47 GB/s of PCIe reads
-    bool label_persist = false;
-    int n_cu = 256;
-    void launch_label_persist(const Batch &q, const HostSrc *src) {
-        const uint64_t groups = (q.n + 16 * kLabelC - 1) / (16 * kLabelC);
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)n_cu * 4));
-#define KETO_LP(PB)                                                                                           \
-    KLAUNCH((label_host_pkernel<PB>), dim3(grid), dim3(64 * (kLabelC + 1)), 0, stream, g, lgraph, src->roots, \
-            src->targets, io->d_roots, io->d_targets, q.n, q.allowed, label_rest(q.n), st.stats, d_bad)
-        if (label_pb == 16)
-            KETO_LP(16);
-        else if (label_pb == 32)
-            KETO_LP(32);
-        else
-            KETO_LP(64);
-#undef KETO_LP
+    // plan label, host batches (K units per workgroup)
+    template <int K>
+    void launch_label_host(const Batch &q, const HostSrc *src, uint64_t bunits) {
+#define KETO_LH(PB, SW)                                                                                    \
+    KLAUNCH((label_host_kernel<K, PB, SW>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, lgraph, \
+            src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed, label_rest(q.n), st.stats, d_bad)
+        if (label_sw == 64) {
+            if (label_pb == 16)
+                KETO_LH(16, 64);
+            else if (label_pb == 32)
+                KETO_LH(32, 64);
+            else
+                KETO_LH(64, 64);
+        } else {
+            if (label_pb == 16)
+                KETO_LH(16, 128);
+            else if (label_pb == 32)
+                KETO_LH(32, 128);
+            else
+                KETO_LH(64, 128);
+        }
+#undef KETO_LH
     }
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
     uint64_t closure_nodes[2] = {0, 0}, closure_entries[2] = {0, 0};
@@ -3867,15 +3793,24 @@ struct ketogpu_engine {
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
         if (c.lite == 3) {  // plan label: closure labels, plan core for units without
-#define KETO_LABEL_K(PB)                                                                                   \
-    KLAUNCH((label_kernel<PB>), dim3(grid), dim3(64), pad, stream, lgraph, q.roots, q.targets, q.n, q.allowed, \
+#define KETO_LABEL_K(PB, SW)                                                                                    \
+    KLAUNCH((label_kernel<PB, SW>), dim3(grid), dim3(64), pad, stream, lgraph, q.roots, q.targets, q.n, q.allowed, \
             label_rest(q.n), stats, unit0)
-            if (label_pb == 16)
-                KETO_LABEL_K(16);
-            else if (label_pb == 32)
-                KETO_LABEL_K(32);
-            else
-                KETO_LABEL_K(64);
+            if (label_sw == 64) {
+                if (label_pb == 16)
+                    KETO_LABEL_K(16, 64);
+                else if (label_pb == 32)
+                    KETO_LABEL_K(32, 64);
+                else
+                    KETO_LABEL_K(64, 64);
+            } else {
+                if (label_pb == 16)
+                    KETO_LABEL_K(16, 128);
+                else if (label_pb == 32)
+                    KETO_LABEL_K(32, 128);
+                else
+                    KETO_LABEL_K(64, 128);
+            }
 #undef KETO_LABEL_K
             return;
         }
@@ -4219,8 +4154,6 @@ struct ketogpu_engine {
         use_label = (p == "label" || p == "auto") && use_core && getenv("KETOGPU_NO_LABEL") == nullptr;
         if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
         if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
-        if (const char *e = getenv("KETOGPU_LABEL_PERSIST")) label_persist = atoi(e) != 0;
-        HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
         if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
         use_bidi = (p == "bidi" || p == "auto") && use_v2 && !s.has_ambiguous && small_f && small_r;
         if (use_v2 && !small_f) {
@@ -4439,9 +4372,13 @@ struct ketogpu_engine {
     void build_label(const Snapshot &s, const CoreIndex &ci, uint64_t free_b) {
         int mode = -1;
         if (const char *e = getenv("KETOGPU_LABEL_MODE")) mode = e[0] == 'F' || e[0] == 'f' ? 1 : 0;
+        // S blocks of 128 words (labels of up to 127 nodes: fewer requests for the second
+        // stage) when they fit an eighth of free HBM, else 64 (KETOGPU_LABEL_WORDS)
+        uint32_t sw = (uint64_t)s.N * 512 <= free_b / 8 ? 128 : 64;
+        if (const char *e = getenv("KETOGPU_LABEL_WORDS")) sw = atoi(e) == 128 ? 128 : 64;
         LabelIndex li;
         try {
-            build_labels(s, ci, mode, 0.5, li);
+            build_labels(s, ci, mode, 0.5, li, sw);
         } catch (const Error &e) {
             fprintf(stderr, "[ketogpu] plan label disabled: %s\n", e.what());
             drop_label();
@@ -4470,12 +4407,13 @@ struct ketogpu_engine {
         HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
         lgraph = LabelGraph{P, S, li.mode};
         label_pb = li.pb;
+        label_sw = li.s_words;
         label_coverage = li.nonempty ? (double)li.covered / (double)li.nonempty : 1.0;
         if (cascade_log)
-            fprintf(stderr, "[label] mode %c: %llu of %llu S nodes labelled (%.4f; sampled B %.3f F %.3f), P blocks of %u "
-                            "words, %.2f GB, built in %.1f ms\n",
+            fprintf(stderr, "[label] mode %c: %llu of %llu S nodes labelled (%.4f; sampled B %.3f F %.3f), S blocks of %u "
+                            "words, P blocks of %u, %.2f GB, built in %.1f ms\n",
                     li.mode ? 'F' : 'B', (unsigned long long)li.covered, (unsigned long long)li.nonempty,
-                    label_coverage, li.coverage[0], li.coverage[1], li.pb, (double)bytes / 1e9, li.build_ms);
+                    label_coverage, li.coverage[0], li.coverage[1], li.s_words, li.pb, (double)bytes / 1e9, li.build_ms);
     }
 
     // Hub index.  Hubs are the interior nodes with the most interior successors; a search
@@ -4798,22 +4736,8 @@ struct ketogpu_engine {
                     // profiles/r02/ab_split.)
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
-        if (bidi_cfg.lite == 3 && label_persist) {                                                         \
-            launch_label_persist(q, src);                                                                  \
-            break;                                                                                         \
-        }                                                                                                  \
-        if (bidi_cfg.lite == 3 && label_pb == 16)                                                          \
-            KLAUNCH((label_host_kernel<K, 16>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
-                    label_rest(q.n), st.stats, d_bad);                                                     \
-        else if (bidi_cfg.lite == 3 && label_pb == 32)                                                     \
-            KLAUNCH((label_host_kernel<K, 32>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
-                    label_rest(q.n), st.stats, d_bad);                                                     \
-        else if (bidi_cfg.lite == 3)                                                                       \
-            KLAUNCH((label_host_kernel<K, 64>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, \
-                    g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed,      \
-                    label_rest(q.n), st.stats, d_bad);                                                     \
+        if (bidi_cfg.lite == 3)                                                                            \
+            launch_label_host<K>(q, src, bunits);                                                          \
         else if (bidi_cfg.lite == 2 && core_shape == 1)                                                    \
             KLAUNCH((lite_host_kernel<K, CoreShapeS, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
                     0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
@@ -4840,9 +4764,7 @@ struct ketogpu_engine {
                     list[0], &spill_count[0], st.stats, d_bad);                                            \
     } while (0)
                     const int hk = host_units ? host_units : bidi_cfg.lite == 3 ? 4 : 2;
-                    if (hk == 8 && bidi_cfg.lite == 3)
-                        KETO_HOST_K(8);
-                    else if (hk == 4)
+                    if (hk == 4)
                         KETO_HOST_K(4);
                     else if (hk == 2)
                         KETO_HOST_K(2);
@@ -5147,6 +5069,7 @@ struct ketogpu_engine {
         rs.closure_entries_b = closure_entries[1];
         rs.core_build_ms = core_build_ms;
         rs.label_mode = use_label ? lgraph.mode : -1;
+        rs.label_words = use_label ? label_sw : 0;
         rs.label_coverage = label_coverage;
         rs.label_build_ms = label_build_ms;
         ev_used = 0;

@@ -17,6 +17,7 @@ struct Ctx {
     const Snapshot &s;
     const CoreIndex &ci;
     int mode;
+    uint32_t words;  // S block words: a label holds at most words - 1 nodes
     // the S list of node x (mode B: x = t, S = rev(t) + closures of its interior entries;
     // mode F: x = r, S = {r} + fint(r) + closures of its entries); false: no label
     bool label(uint64_t x, std::vector<uint32_t> &out) const {
@@ -37,7 +38,7 @@ struct Ctx {
         }
         std::sort(out.begin(), out.end());
         out.erase(std::unique(out.begin(), out.end()), out.end());
-        return out.size() < kLabelWords;
+        return out.size() < words;
     }
     uint64_t s_nodes() const { return mode == 0 ? s.N : s.Nx; }
     bool nonempty(uint64_t x) const {
@@ -69,11 +70,14 @@ double sample_coverage(const Ctx &c, uint64_t sample) {
 
 }  // namespace
 
-void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out) {
+void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out,
+                  uint32_t s_words) {
+    if (s_words != 64 && s_words != 128) throw Error(KETOGPU_EINVAL, "plan label: S blocks of 64 or 128 words");
     const auto t0 = std::chrono::steady_clock::now();
     out = LabelIndex{};
+    out.s_words = s_words;
     for (int m = 0; m < 2; m++)
-        if (ci.clo_len[m == 0 ? 1 : 0].size() == s.Ni) out.coverage[m] = sample_coverage(Ctx{s, ci, m}, 20000);
+        if (ci.clo_len[m == 0 ? 1 : 0].size() == s.Ni) out.coverage[m] = sample_coverage(Ctx{s, ci, m, s_words}, 20000);
     if (mode < 0) {
         mode = out.coverage[0] >= out.coverage[1] ? 0 : 1;
         if (out.coverage[mode] < min_coverage) {
@@ -83,18 +87,18 @@ void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_c
     }
     if (ci.clo_len[mode == 0 ? 1 : 0].size() != s.Ni)
         throw Error(KETOGPU_EINVAL, "plan label: the core index has no closure rows in that direction");
-    const Ctx c{s, ci, mode};
+    const Ctx c{s, ci, mode, s_words};
     out.mode = mode;
     // S blocks
     const uint64_t ns = c.s_nodes();
     out.s_nodes = ns;
-    out.S.assign(ns * kLabelWords, 0xFFFFFFFFu);
+    out.S.assign(ns * s_words, 0xFFFFFFFFu);
     std::atomic<uint64_t> covered{0}, nonempty{0};
     std::vector<std::vector<uint32_t>> tmp(build_threads());
     parallel_chunks(ns, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
         uint64_t cv = 0, ne = 0;
         for (uint64_t x = b; x < e; x++) {
-            uint32_t *blk = out.S.data() + x * kLabelWords;
+            uint32_t *blk = out.S.data() + x * s_words;
             const bool has = c.nonempty(x);
             ne += has;
             if (!c.label(x, tmp[tid])) continue;  // count stays 0xFFFFFFFF: no label
@@ -168,7 +172,7 @@ struct ketogpu_label_index {
 
 extern "C" {
 
-int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode,
+int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode, uint32_t s_words,
                               ketogpu_label_index **out) {
     try {
         if (!s || !closure_cap || !out || mode < -1 || mode > 1) throw ketogpu::Error(KETOGPU_EINVAL, "bad argument");
@@ -179,7 +183,7 @@ int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_
         const uint32_t block[2] = {0, 0};
         ketogpu::build_core_index(*snap, closure_cap, block, ci);
         auto l = std::make_unique<ketogpu_label_index>();
-        ketogpu::build_labels(*snap, ci, mode, 0.5, l->li);
+        ketogpu::build_labels(*snap, ci, mode, 0.5, l->li, s_words);
         *out = l.release();
     } catch (const ketogpu::Error &e) {
         ketogpu::set_last_error(e.what());
@@ -198,6 +202,7 @@ int ketogpu_label_index_view(const ketogpu_label_index *l, ketogpu_label_view *o
     }
     const ketogpu::LabelIndex &li = l->li;
     out->mode = li.mode;
+    out->s_block_words = li.s_words;
     out->p_block_words = li.pb;
     out->p_words = li.P.data();
     out->s_words = li.S.data();

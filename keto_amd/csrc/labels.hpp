@@ -12,12 +12,12 @@
 // (a path's first interior node x1 is in fint(r) and its last one in rev(t); x1 reaches
 // x(k-1) through interior nodes, so x1 is in Anc+(x(k-1)) and x(k-1) in Desc+(x1); a path
 // of one edge has r in rev(t)).  S is a LABEL: stored sorted per node when every closure it
-// needs exists and it has at most 63 nodes; a request whose S is missing is answered by
-// plan core's traversal instead (its whole 16-request unit).
+// needs exists and it has at most s_words - 1 nodes; a request whose S is missing is
+// answered by plan core's traversal instead (a second stage over those requests).
 //
 // Storage, per mode, all u32 words:
-//   S blocks, one per S node (64 words = 256 bytes, aligned): [count, entries sorted
-//     ascending, 0xFFFFFFFF padding]; count = 0xFFFFFFFF: no label
+//   S blocks, one per S node (s_words = 64 or 128 words, 256 / 512 bytes, aligned): [count,
+//     entries sorted ascending, 0xFFFFFFFF padding]; count = 0xFFFFFFFF: no label
 //   P blocks, one per P node (pb words): [count, overflow start, entries...]; a row of more
 //     than pb - 2 entries keeps the rest at p[overflow start ...] (an overflow region after
 //     the blocks, in the same array)
@@ -30,11 +30,11 @@
 
 namespace ketogpu {
 
-constexpr uint32_t kLabelWords = 64;            // S block words (count + 63 entries)
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 
 struct LabelIndex {
     int mode = -1;                 // 0 = B, 1 = F; -1: not built
+    uint32_t s_words = 64;         // S block words (64 or 128: labels of up to 63 or 127 nodes)
     uint32_t pb = 0;               // P block words
     std::vector<uint32_t> P, S;
     uint64_t p_nodes = 0, s_nodes = 0;
@@ -46,6 +46,7 @@ struct LabelIndex {
 
 // mode: 0 / 1 forces B / F, -1 builds the mode whose labels cover more S nodes (none when
 // both cover less than min_coverage).  Needs the closure rows of ci (build_core_index).
-void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out);
+void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out,
+                  uint32_t s_words = 64);
 
 }  // namespace ketogpu

@@ -46,6 +46,31 @@ def make_graph(seed, n_rows=200, n_obj=12, n_rel=3, n_users=10, wildcard=True, p
     return namespaces, rows
 
 
+def make_family_graph(seed, families=12, chain=35, docs=3, users=300):
+    """groups in chains (family f: g{f}_0 member of g{f}_1 ... of g{f}_{chain-1}), a few
+    documents per family viewable by members of a chain group, users members of the chain
+    bottoms of 1..4 families: a user's backward label (plan label mode B) holds the chain's
+    groups of each of its families (35, 70, 105, 140 nodes), so labels of 33..63, 64..127
+    (searched in the S block in place) and none (> 127) all occur.  -> (namespaces, rows, requests)"""
+    rng = random.Random(seed)
+    rows = []
+    for f in range(families):
+        for k in range(chain - 1):
+            rows.append((1, f"g{f}_{k + 1}", "member", None, 1, f"g{f}_{k}", "member"))
+        for d in range(docs):
+            rows.append((1, f"d{f}_{d}", "view", None, 1, f"g{f}_{rng.randrange(chain)}", "member"))
+    for u in range(users):
+        for f in rng.sample(range(families), 1 + u % 4):
+            rows.append((1, f"g{f}_0", "member", f"u{u}", None, None, None))
+    reqs = []
+    for _ in range(4 * users):
+        f = rng.randrange(families)
+        o, r = (f"d{f}_{rng.randrange(docs)}", "view") if rng.random() < 0.4 else (f"g{f}_{rng.randrange(chain)}",
+                                                                                  "member")
+        reqs.append(("n", o, r, {"subject_id": f"u{rng.randrange(users)}"}))
+    return [("n", 1)], rows, reqs
+
+
 def make_requests(seed, namespaces, rows, n=300, wildcard=True):
     rng = random.Random(seed + 7)
     names = [n for n, _ in namespaces] + ["unknown"]

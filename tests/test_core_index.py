@@ -167,12 +167,12 @@ def label_answer(li, r, t):
     if r == NONE_ or t == NONE_:
         return False
     xs, xp = (t, r) if li["mode"] == 0 else (r, t)
-    S, P, pb = li["S"], li["P"], li["p_block_words"]
-    n = int(S[xs * 64])
+    S, P, pb, sw = li["S"], li["P"], li["p_block_words"], li["s_block_words"]
+    n = int(S[xs * sw])
     if n == NONE_:
         return None
-    s = S[xs * 64 + 1: xs * 64 + 1 + n]
-    assert np.all(np.diff(s.astype(np.int64)) > 0) and np.all(S[xs * 64 + 1 + n: xs * 64 + 64] == NONE_)
+    s = S[xs * sw + 1: xs * sw + 1 + n]
+    assert np.all(np.diff(s.astype(np.int64)) > 0) and np.all(S[xs * sw + 1 + n: xs * sw + sw] == NONE_)
     m, ovf = int(P[xp * pb]), int(P[xp * pb + 1])
     p = list(P[xp * pb + 2: xp * pb + 2 + min(m, pb - 2)])
     if m > pb - 2:
@@ -181,8 +181,8 @@ def label_answer(li, r, t):
     return bool(np.isin(np.asarray(p, dtype=np.uint32), s).any())
 
 
-def check_labels(snap, reqs, want, mode):
-    li = snap.label_index((64, 64), mode)
+def check_labels(snap, reqs, want, mode, s_words=64):
+    li = snap.label_index((64, 64), mode, s_words)
     if mode >= 0:
         assert li["mode"] == mode
     if li["mode"] < 0:
@@ -200,14 +200,16 @@ def check_labels(snap, reqs, want, mode):
 
 @pytest.mark.parametrize("seed,poison", [(81, False), (82, True), (83, False)])
 @pytest.mark.parametrize("mode", [0, 1, -1])
-def test_labels_answer_like_the_oracle(seed, poison, mode):
+@pytest.mark.parametrize("s_words", [64, 128])
+def test_labels_answer_like_the_oracle(seed, poison, mode, s_words):
     """every request whose S node has a label is answered by one intersection exactly as
     the reference's recursion (oracle), in both modes"""
     namespaces, rows = randgraph.make_graph(seed, n_rows=900, n_obj=40, n_users=50, poison=poison)
     snap = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
     reqs = randgraph.make_requests(seed, namespaces, rows, n=1500, wildcard=False)
     want = randgraph.oracle_store(namespaces, rows, 4).check_batch(reqs)
-    li, done = check_labels(snap, reqs, want, mode)
+    li, done = check_labels(snap, reqs, want, mode, s_words)
+    assert li["s_block_words"] == s_words
     if li["mode"] >= 0:
         assert done > 0.3 * len(reqs)
 
@@ -230,3 +232,20 @@ def test_labels_on_synthetic_configs(kind, mode):
     done = [i for i, g in enumerate(got) if g is not None]
     assert len(done) > 0.9 * len(roots)
     assert all(got[i] == bool(want[i]) for i in done)
+
+
+def test_wide_labels():
+    """labels of 64..127 nodes exist only with 128-word S blocks and answer exactly; with
+    64-word blocks those S nodes have no label"""
+    namespaces, rows, reqs = randgraph.make_family_graph(91)
+    snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    want = randgraph.oracle_store(namespaces, rows).check_batch(reqs)
+    assert any(want) and not all(want)
+    counts = {}
+    for sw in (64, 128):
+        li, done = check_labels(snap, reqs, want, 0, sw)
+        S = li["S"].reshape(-1, sw)[:, 0]
+        counts[sw] = S[S != 0xFFFFFFFF]
+        assert done > 0.2 * len(reqs)
+    assert counts[64].max() <= 63 and (counts[128] > 63).sum() > 50
+    assert len(counts[128]) > len(counts[64])

@@ -96,6 +96,30 @@ def test_random_tables_match_oracle(seed, page_size, poison, collide, empty_ns, 
     assert any(want) and not all(want)
 
 
+@pytest.mark.parametrize("words", ["64", "128"])
+def test_wide_labels_match_oracle(words, monkeypatch):
+    """plan label over labels of 33..63 nodes (two S lines in LDS), 64..127 nodes (128-word
+    blocks: searched in the block) and none (second stage), mode B, device and host batches"""
+    monkeypatch.setenv("KETOGPU_UNITS", "label")
+    monkeypatch.setenv("KETOGPU_LABEL_MODE", "B")
+    monkeypatch.setenv("KETOGPU_LABEL_WORDS", words)
+    namespaces, rows, reqs = randgraph.make_family_graph(92)
+    snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    want = randgraph.oracle_store(namespaces, rows).check_batch(reqs)
+    eng = check.Engine(snap)
+    assert eng.check_many(tuples_of(reqs)) == [bool(x) for x in want]
+    st = eng.last_stats()
+    assert st["plan"] == 7 and st["label_words"] == int(words)
+    roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(x)) for ns, o, r, x in reqs])
+    q = eng.upload(roots, targets)  # HBM-resident
+    q.run()
+    np.testing.assert_array_equal(q.download(), want)
+    pr, pt = check.pinned(roots), check.pinned(targets)  # pinned host requests read in place
+    out = check.PinnedBuffer((len(roots) + 63) // 64, np.uint64)
+    eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, len(roots), out.array.ctypes.data)
+    np.testing.assert_array_equal(check.unpack_bits(out.array.copy(), len(roots)), want)
+
+
 @pytest.fixture
 def global_path(monkeypatch):
     """engines created while active use only the global multi-word path"""
