@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--parity", choices=["full", "sample"], default="full",
                    help="full: every request of the timed batch is diffed against the oracle (about 90 s of "
                         "16-thread CPU work at config #2); sample: only the baseline sample")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03", "traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
     p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
                    help="replicated: graph on every GPU, request batches sharded (the metric's line); "
@@ -281,6 +281,13 @@ def main():
                             len(host_runs), n, "hipEvents on the engine's stream around the first stage of the "
                                                "host-to-host step (ketogpu_engine_set_events), same steps re-run")
             roof["hbm_resident"] = hbm_roof
+            # the same kernel against its real bound: 8 B of requests per check read over PCIe
+            pcie_ach = 8 * n * len(host_runs) / (sum(r["main_ms"] for r in host_runs) * 1e-3) / 1e9
+            pcie_peak = pcie_h2d_gbps(local)
+            roof["pcie"] = {"bound": "pcie (requests read in place from pinned host memory)",
+                            "achieved": round(pcie_ach, 1), "peak": round(pcie_peak, 1), "unit": "GB/s",
+                            "peak_source": "measured: pinned 64 MiB host -> HBM DMA copy (hipMemcpyAsync)",
+                            "frac": round(pcie_ach / pcie_peak, 4) if pcie_peak > 0 else None}
         else:
             roof = hbm_roof
         roof["kernels"] = {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": bb, "launches": nl}
@@ -603,6 +610,23 @@ def stream_copy_gbps(device, nbytes=1 << 30, iters=10):
     ms = e0.elapsed_time(e1)
     del a, b
     return 2 * nbytes * iters / (ms * 1e-3) / 1e9
+
+
+def pcie_h2d_gbps(device, nbytes=64 << 20, iters=10):
+    """pinned host -> HBM DMA copy bandwidth of a 64 MiB buffer: the measured PCIe ceiling
+    of a host-batch first stage that reads its requests from pinned memory"""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{device}")
+    d.copy_(h, non_blocking=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        d.copy_(h, non_blocking=True)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1)
+    del h, d
+    return nbytes * iters / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline(w, gpu_allowed, seconds, full=True, offset=0):
