@@ -252,6 +252,10 @@ def main():
                       ({"skipped": oracle_skipped} if oracle_skipped else None)},
            "peak_rss_gb": round(rss_gb(), 1),
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
+           "core_build_ms": round(rs["core_build_ms"], 1),
+           "label": ({"mode": "BF"[rs["label_mode"]], "coverage": round(rs["label_coverage"], 4),
+                      "s_block_words": rs["label_words"], "build_ms": round(rs["label_build_ms"], 1)}
+                     if rs["label_mode"] >= 0 else None),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
            "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}

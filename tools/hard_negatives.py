@@ -4,7 +4,7 @@ At 1.0e9 rows of the power-law graph (BASELINE config #4) a negative check walks
 of ~10^6 groups, so a uniform oracle sample finishes only the easy requests.  Two runs
 (each inside one gpurun time limit):
 
-    python tools/hard_negatives.py pick   OUT.json [--tuples 1e9 --candidates 20000 --keep 64]
+    python tools/hard_negatives.py pick   OUT.json [--tuples 1e9 --users 125e6 --candidates 20000 --keep 64]
         generate the graph; the independent R2 checker (oracle/r2_check.c) over a uniform
         candidate sample of the bench's requests reports each request's answer and the size
         of its root's interior closure X(r); keep the negatives with the largest closures;
@@ -59,7 +59,7 @@ def pick(a, phase):
     from keto_amd.snapshot import Snapshot
     from oracle import oracle as O
     phase[0] = "generating"
-    w = make("social", a.tuples, 1_000_000)
+    w = make("social", a.tuples, 1_000_000, a.users, a.groups)
     log(f"generated {w.counts}")
     phase[0] = "R2 checker"
     cand = np.sort(np.random.default_rng(11).permutation(w.n_checks)[:a.candidates])
@@ -76,6 +76,7 @@ def pick(a, phase):
     phase[0] = "snapshot"
     snap = Snapshot.from_columns(w.namespaces, w.columns)
     roots, targets = w.resolve(snap)
+    w_rows = w.counts["tuples"]
     del w
     phase[0] = "engine"
     eng = check.Engine(snap)
@@ -83,7 +84,7 @@ def pick(a, phase):
         got_all = eng.check_ids(roots, targets)
     st = eng.last_stats()
     got = got_all[keep]
-    out = {"tuples": a.tuples, "candidates": int(len(cand)), "keep": keep.tolist(),
+    out = {"tuples": a.tuples, "users": a.users, "groups": a.groups, "rows": int(w_rows), "candidates": int(len(cand)), "keep": keep.tolist(),
            "closure_size": size[order].astype(int).tolist(), "r2_answer": want[order].astype(int).tolist(),
            "engine_answer": got.astype(int).tolist(), "engine_plan": int(st["plan"]),
            "engine_vs_r2_mismatches": int((got != want[order]).sum()),
@@ -98,8 +99,9 @@ def oracle(a, phase):
     from tests import randgraph
     picked = json.load(open(a.out))
     phase[0] = "generating"
-    w = make("social", picked["tuples"], 1_000_000)
+    w = make("social", picked["tuples"], 1_000_000, picked.get("users"), picked.get("groups"))
     log(f"generated {w.counts}")
+    assert w.counts["tuples"] == picked.get("rows", w.counts["tuples"]), "not the picked graph"
     phase[0] = "oracle store"
     orc = randgraph.oracle_store_columns(w.namespaces, w.columns)
     keep = np.asarray(picked["keep"], dtype=np.int64)
@@ -120,7 +122,8 @@ def oracle(a, phase):
     r2 = np.asarray(picked["r2_answer"], dtype=bool)
     tried = int(min(len(keep), (k // nt + 1) * nt))
     res = {"against": "oracle/keto_oracle.c (internal/check/engine.go:33-95 restated)",
-           "graph": f"config #4 power-law, {picked['tuples']:.3g} rows", "threads": nt,
+           "graph": f"config #4 power-law, {picked.get('rows', picked['tuples']):.4g} rows"
+                    + (f", {picked['users']} users" if picked.get("users") else ""), "threads": nt,
            "request_budget_s": a.budget, "tried": tried, "finished": int(done.sum()),
            "timed_out": int(tried - done.sum()),
            "mismatches_vs_engine": int((ans[done] != eng[done]).sum()),
@@ -142,6 +145,9 @@ def main():
     p.add_argument("--tuples", type=float, default=1e9)
     p.add_argument("--candidates", type=int, default=20000)
     p.add_argument("--keep", type=int, default=64)
+    p.add_argument("--users", type=int, default=125_000_000,
+                   help="125M users x 10M groups: the generator's 1.0e9-row shape (its default 100M gives 8.1e8 rows)")
+    p.add_argument("--groups", type=int, default=10_000_000)
     p.add_argument("--budget", type=float, default=120.0)
     p.add_argument("--seconds", type=float, default=560.0, help="stop starting oracle chunks after this")
     a = p.parse_args()
