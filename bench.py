@@ -362,6 +362,16 @@ def main_partitioned(a, rank, world, local):
     all ranks / the slowest rank's time."""
     from keto_amd import synth
     from keto_amd.partition import Core, PartitionedEngine, Shard, TieredEngine
+    import threading
+    phase = ["loading the shard"]
+
+    def heartbeat():  # long loads (minutes at --scale >= 0.1) stay visibly alive
+        t_hb = time.time()
+        while phase[0]:
+            time.sleep(30)
+            if phase[0]:
+                log(f"... {phase[0]} ({time.time() - t_hb:.0f}s)")
+    threading.Thread(target=heartbeat, daemon=True).start()
     f = a.scale
     sizes = dict(users=max(1000, int(500_000_000 * f)), groups=max(100, int(10_000_000 * f)),
                  docs=max(100, int(200_000_000 * f)), tuples=max(10_000, int(5_000_000_000 * f)))
@@ -376,6 +386,7 @@ def main_partitioned(a, rank, world, local):
         ncomm = NativeComm(device=local, kind="rccl")
     sh = Shard.load(w.namespaces, lambda: w.batches(1 << 20), native_comm=ncomm)
     t_load = time.time() - t0
+    phase[0] = "building the engine, timing, parity"
     rss_load = max_rss_gb()
     sst = sh.stats()
     log(f"shard loaded in {t_load:.1f}s: {sst['rows']} rows streamed, {sst['owned_nodes']} nodes owned, "
@@ -453,9 +464,24 @@ def main_partitioned(a, rank, world, local):
     out = None
     if rank == 0:
         if tier:
+            traffic, traffic_note = None, "no PMC summary for this workload"
+            tpath = os.path.join(ROOT, "profiles", "r04", f"traffic_config5_x{f:g}.json")
+            if os.path.exists(tpath):  # tools/profile.sh with WORKLOAD=config5_partitioned_x<scale>
+                try:
+                    tr = json.load(open(tpath))
+                    if tr.get("workload") != f"config5_partitioned_x{f:g}":
+                        traffic_note = "PMC summary of another workload"
+                    elif tr.get("source_hash") != kernel_source_hash():
+                        traffic_note = (f"stale: {os.path.relpath(tpath, ROOT)} was profiled at kernel sources "
+                                        f"{tr.get('source_hash')}, HEAD is {kernel_source_hash()}")
+                    else:
+                        traffic = tr.get("kernels", {}).get("tier_eval_kernel", {}).get("hbm_bytes_per_launch")
+                        traffic_note = f"{os.path.relpath(tpath, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+                except (OSError, ValueError):
+                    traffic_note = "unreadable PMC summary"
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "traffic_source": "no PMC summary for this workload", "kernel": "tier_eval_kernel",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "traffic_source": traffic_note, "kernel": "tier_eval_kernel",
                     "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
                     "measured": "hipEvents around the first evaluation stage on the engine's stream, every timed step",
                     "bytes_formula": "16*rows_opened + 16*records_read + 8*requests + requests/8 (as the replicated "
@@ -512,6 +538,7 @@ def main_partitioned(a, rank, world, local):
                                          "native: ketogpu_part_check_ids (part_round.cpp), world 1: no exchange"),
                         "timed_pass_s": round(t_timed, 4)})
         print(json.dumps(out), flush=True)
+    phase[0] = None
     barrier(world)
     if world > 1:
         import torch.distributed as dist

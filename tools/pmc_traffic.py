@@ -54,6 +54,12 @@ FAMILIES = [
     ("part_gather_kernel", r"part_gather_kernel"),
     ("part_reset_kernel", r"part_reset_kernel"),
     ("part_pull_answer_kernel", r"part_pull_answer_kernel"),
+    # two-tier partitioned engine (config #5)
+    ("tier_eval_kernel", r"tier_eval_kernel"),
+    ("tier_cascade_kernel", r"tier_cascade_kernel"),
+    ("tier_seed_kernel", r"tier_seed_kernel"),
+    ("tier_query kernels (count + scatter)", r"tier_query_"),
+    ("tier_reply kernels (len + scan + copy)", r"tier_reply_|tier_scan_"),
 ]
 
 
