@@ -3033,46 +3033,48 @@ __global__ __launch_bounds__(kTB) void tier_reply_copy_kernel(tier::Graph G, con
 
 // received replies -> seed records (entry x: its core row in this rank's copy of the core —
 // forward entries are interior; a backward entry outside the interior is (x, 0, 0): only
-// compared with the root) and per request seed bounds (each query's row is contiguous)
-// Four consecutive entries per thread, one 8-byte {begin, count} read per entry: the
-// random reads into the core's row table are L2 requests, one per lane, and set the time.
+// compared with the root) and per request seed bounds (each query's row is contiguous).
+// Lane-consecutive entries: a wave's 64 lanes read 64 consecutive 8-byte replies and write
+// 64 consecutive 16-byte records per instruction (1 KB, whole lines; with four consecutive
+// entries per lane each store instruction wrote 16 of every 64 bytes: PMC 406 MB written
+// per 10^6 config-#5 requests for 298 MB of records).  The neighbours' tags that decide
+// the bounds come from the adjacent lanes (the wave's first / last lane reads them).  The
+// random reads into the core's row table are L2 requests, one per lane.
 constexpr int kSeedPer = 4;
 __global__ __launch_bounds__(kTB) void tier_seed_kernel(tier::Graph G, const tier::Reply *recv, uint64_t n,
                                                         tier::Rec *seed, uint4 *bnd, uint64_t nreq) {
-    for (uint64_t k0 = ((uint64_t)blockIdx.x * kTB + threadIdx.x) * kSeedPer; k0 < n;
-         k0 += (uint64_t)gridDim.x * kTB * kSeedPer) {
+    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint64_t span = (uint64_t)kTB * kSeedPer;  // entries per workgroup pass
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
         tier::Reply e[kSeedPer];
-        if (k0 + kSeedPer <= n) {  // 32-byte aligned: two 16-byte loads
-            const uint4 *v = reinterpret_cast<const uint4 *>(recv + k0);
-            const uint4 a = v[0], b = v[1];
-            e[0] = {a.x, a.y};
-            e[1] = {a.z, a.w};
-            e[2] = {b.x, b.y};
-            e[3] = {b.z, b.w};
-        } else {
-#pragma unroll
-            for (int j = 0; j < kSeedPer; j++) e[j] = k0 + j < n ? recv[k0 + j] : tier::Reply{~0u, ~0u};
-        }
-        const uint32_t prev = k0 ? recv[k0 - 1].tag : ~0u;
-        const uint32_t next = k0 + kSeedPer < n ? recv[k0 + kSeedPer].tag : ~0u;
         uint2 row[kSeedPer];
 #pragma unroll
         for (int j = 0; j < kSeedPer; j++) {
+            const uint64_t k = base + (uint64_t)j * kTB + threadIdx.x;
+            e[j] = k < n ? recv[k] : tier::Reply{~0u, ~0u};
+        }
+#pragma unroll
+        for (int j = 0; j < kSeedPer; j++) {
+            const uint64_t k = base + (uint64_t)j * kTB + threadIdx.x;
             const uint2 *rows = (e[j].tag & 1u) ? G.core_b_row : G.core_f_row;
-            const bool in = e[j].node < G.Ni && k0 + j < n;
+            const bool in = k < n && e[j].node < G.Ni;
             row[j] = in ? rows[e[j].node] : make_uint2(0u, 0u);
         }
 #pragma unroll
         for (int j = 0; j < kSeedPer; j++) {
-            const uint64_t k = k0 + j;
-            if (k >= n) break;
+            const uint64_t k = base + (uint64_t)j * kTB + threadIdx.x;
             const uint32_t tag = e[j].tag;
+            uint32_t prev = (uint32_t)__shfl_up((int)tag, 1, 64), next = (uint32_t)__shfl_down((int)tag, 1, 64);
+            if (lane == 0) prev = k && k - 1 < n ? recv[k - 1].tag : ~0u;
+            if (lane == 63) next = k + 1 < n ? recv[k + 1].tag : ~0u;
+            if (k >= n) continue;
+            if (k + 1 >= n) next = ~0u;
             seed[k] = tier::Rec{e[j].node, row[j].y, row[j].x, tag};
             const uint64_t i = tag >> 1;
             if (i >= nreq) continue;
             uint32_t *b = reinterpret_cast<uint32_t *>(&bnd[i]) + 2 * (tag & 1u);
-            if ((j ? e[j - 1].tag : prev) != tag) b[0] = (uint32_t)k;
-            if ((j + 1 < kSeedPer ? (k + 1 < n ? e[j + 1].tag : ~0u) : next) != tag) b[1] = (uint32_t)(k + 1);
+            if (prev != tag) b[0] = (uint32_t)k;
+            if (next != tag) b[1] = (uint32_t)(k + 1);
         }
     }
 }
