@@ -3,10 +3,11 @@
     python tools/timeline.py gpurun_out/<dir>/trace [--calls 2]
 
 Reads *kernel_trace.csv and *memory_copy_trace.csv, groups activity into calls (idle gaps
-of more than 200 us separate them) and prints, for the last --calls calls that contain a
-pipelined bidi chunk launch, every kernel and copy relative to the call's first event:
-where the chunked upload, the chunk launches, the spill stages and the result copy sit,
-and the GPU-idle gaps between them.
+of more than 200 us separate them) and prints, for the last --calls host-to-host calls (a
+first stage reading pinned requests in place, `*_host_kernel`, or a pipelined chunk launch),
+every kernel and copy relative to the call's first event: the clear, the first stage, the
+second / spill stages and the statistics-and-results launch, and the GPU-idle gaps between
+them.
 """
 import csv
 import glob
@@ -59,8 +60,8 @@ def main():
         last_end = max(last_end or 0, e[1])
     if cur:
         calls.append(cur)
-    piped = [c for c in calls if any(", 1>" in e[3] for e in c)]
-    if "--first" in sys.argv:  # the earliest pipelined calls (the bench's timed steps)
+    piped = [c for c in calls if any(", 1>" in e[3] or "_host_kernel" in e[3] for e in c)]
+    if "--first" in sys.argv:  # the earliest host-to-host calls (the bench's timed steps)
         piped = piped[:ncalls + 2]
     for c in piped[-ncalls:]:
         t0 = c[0][0]
