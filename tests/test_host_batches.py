@@ -91,11 +91,12 @@ def test_pipelined_check_ids_matches_oracle(rbac, chunk, mode, plan, monkeypatch
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["bidi", "label"])
 @pytest.mark.parametrize("mode", ["direct", "direct4", "chunks"])
-def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, monkeypatch):
+def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, plan, monkeypatch):
     _gpu()
     _, snap, roots, targets, want = rbac
-    monkeypatch.setenv("KETOGPU_UNITS", "bidi")
+    monkeypatch.setenv("KETOGPU_UNITS", plan)
     monkeypatch.setenv("KETOGPU_PIPE_CHUNK", "4096")
     _pipe_mode(monkeypatch, mode)
     eng = check.Engine(snap)
@@ -117,8 +118,15 @@ def test_check_ids_rejects_ids_outside_the_snapshot(rbac, mode, monkeypatch):
         assert e.value.code == L.EINVAL and f"request {bad_at} " in str(e.value)
         with pytest.raises(L.KetoError):
             eng.upload(r, t)
-    # the engine is still usable and exact afterwards
+    # the engine is still usable and exact afterwards, also for pinned batches read in place
+    # back to back (plan label: a call after a clean call skips its clear launch), a smaller
+    # batch after them and a larger one again
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    pr, pt = check.pinned(roots), check.pinned(targets)
+    for n in (len(roots), len(roots), 777, 64, len(roots)):
+        out.array[:] = 0
+        eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, n, out.array.ctypes.data)
+        np.testing.assert_array_equal(check.unpack_bits(out.array.copy(), n), want[:n])
 
 
 @pytest.mark.gpu
