@@ -4394,8 +4394,10 @@ struct ketogpu_engine {
             drop_label();
             return;
         }
+        // up to half of the HBM left after the graph and plan core (config #2's shape at 1e9
+        // rows: 63 GB of labels next to ~75 GB of graph and core records)
         const uint64_t bytes = 4 * (li.P.size() + li.S.size());
-        if (bytes > free_b / 4) {
+        if (bytes > free_b / 2) {
             fprintf(stderr, "[ketogpu] plan label disabled: %llu bytes of labels, %llu free\n",
                     (unsigned long long)bytes, (unsigned long long)free_b);
             drop_label();
