@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--parity", choices=["full", "sample"], default="full",
                    help="full: every request of the timed batch is diffed against the oracle (about 90 s of "
                         "16-thread CPU work at config #2); sample: only the baseline sample")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
     p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
                    help="replicated: graph on every GPU, request batches sharded (the metric's line); "
@@ -328,12 +328,23 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_sql": sql, "parity": parity,
             "plan": plan + (f" ({st['plan_unit']}-request units, {st['plan_lists']}-entry lists)"
                             if plan in ("bidi", "lite", "core") else
-                            f" (mode {'BF'[st['label_mode']]}, {st['label_coverage']:.4f} of the label nodes labelled)"
-                            if plan == "label" else ""),
+                            f" (2-hop labels: S heads {st['label_s_head']} words, P heads {st['label_p_head']} words, "
+                            f"{st['label_bytes'] / 1e9:.2f} GB)" if plan == "label" else ""),
             "engine": {k: st[k] for k in ("spilled_units", "unit_rows", "unit_edges", "unit_rev", "rounds", "levels",
                                           "frontier_entries", "interior_edges", "rev_edges", "touched", "ms_total",
                                           "hubs", "hub_build_ms", "closure_nodes_f", "closure_nodes_b",
-                                          "core_build_ms", "label_mode", "label_coverage", "label_build_ms")},
+                                          "core_build_ms", "label_on", "label_coverage", "label_build_ms",
+                                          "label_pll_ms", "label_bytes", "label_entries", "label_s_head",
+                                          "label_p_head")},
+            # plan label's second stage (requests without labels: plan lite over the listed
+            # requests): its share of the timed batch and its time (events between kernels)
+            "second_stage": ({"rest_requests_per_call": [int(r["rest_requests"]) for r in host_runs] or
+                              [int(st["rest_requests"])],
+                              "rest_ms_per_call": [round(r["rest_ms"], 4) for r in host_runs],
+                              "first_stage_ms_per_call": [round(r["main_ms"], 4) for r in host_runs],
+                              "note": "rest_ms = the second stage + the statistics/emit launch, timed between "
+                                      "hipEvents with KETOGPU_EVENTS between kernels"}
+                             if plan == "label" else None),
             "edges_per_check": round((st["interior_edges"] + st["rev_edges"]) / max(e0 - b0, 1), 2),
             "allowed_fraction": round(float(allowed.mean()), 4),
             "setup_s": {"generate": round(t_gen, 2), "snapshot": round(t_snap, 2)},

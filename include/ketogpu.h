@@ -33,7 +33,9 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 7 /* 7: two-tier partitioned mode (ketogpu_core_*, ketogpu_tier_*);
+#define KETOGPU_ABI_VERSION 8 /* 8: 2-hop reachability labels (plan label), run stats
+                                    label_* / rest_*;
+                                 7: two-tier partitioned mode (ketogpu_core_*, ketogpu_tier_*);
                                  6: partitioned rounds behind the C ABI (comm, part_engine);
                                  5: writable snapshots (in-place writes, engine sync);
                                  4: ketogpu_shard_*, part_new over a shard; 3: host_alloc, multi */
@@ -238,24 +240,29 @@ int ketogpu_core_index_build(const ketogpu_snapshot *s, const uint32_t closure_c
 int ketogpu_core_index_view(const ketogpu_core_index *c, int direction, ketogpu_core_records *out);
 void ketogpu_core_index_free(ketogpu_core_index *c);
 
-/* Plan "label"'s closure labels (keto_amd/csrc/labels.hpp) as an engine builds them, for
- * tools and tests.  mode 0 (B): S blocks per node t = rev(t) + the backward closures of its
- * interior entries, P blocks per expandable r = {r} + fint(r); mode 1 (F): S blocks per
- * expandable r = {r} + fint(r) + their forward closures, P blocks per node t = rev(t);
- * mode -1: the better-covered one (view mode -1 when neither labels half its nodes).
- * allowed(r, t) <=> the request's P list and S list share a node.  S blocks: s_words u32
- * (64 or 128) [count (0xFFFFFFFF: no label), entries ascending, 0xFFFFFFFF padding]; P blocks: pb u32
- * [count, overflow start / 16, entries...], entries past pb - 2 at words overflow*16... */
+/* Plan "label"'s 2-hop reachability labels (keto_amd/csrc/labels.hpp) as an engine builds
+ * them, for tools and tests.  Interior nodes are ranked; Lin(v) / Lout(v) hold the ranks of
+ * the landmarks that reach v / that v reaches (the first 64 landmarks as a bit mask), so
+ * that a ->* b <=> Lout(a) meets Lin(b).  Per request:
+ *   S(t) = Lin(v) for every interior v in rev(t), plus rev(t)'s other entries (node ids);
+ *   P(r) = Lout(r) (r interior), else {r} + Lout(c) for every c in fint(r);
+ *   allowed(r, t) <=> S(t) and P(r) share an entry or their masks share a bit.
+ * One head per node (S: every node, P: every expandable node) of s_head_words /
+ * p_head_words u32 (8, 16 or 32; 0 = chosen from the list lengths):
+ *   [count, overflow start / 16, mask lo, mask hi, entries ascending, 0xFFFFFFFF pad];
+ * a list longer than head - 4 entries lies whole at words 16 x (overflow start). */
 typedef struct ketogpu_label_index ketogpu_label_index;
 typedef struct {
-    int32_t mode;
-    uint32_t s_block_words, p_block_words;
-    const uint32_t *p_words, *s_words;
-    uint64_t num_p_words, num_s_words;
-    uint64_t p_nodes, s_nodes, labelled, nonempty;
-    double coverage_b, coverage_f; /* sampled labelled shares of both modes */
+    uint32_t s_head_words, p_head_words;
+    const uint32_t *s_words, *p_words;
+    uint64_t num_s_words, num_p_words;
+    uint64_t s_nodes, p_nodes;
+    uint64_t s_entries, p_entries;   /* list entries (masks not counted) */
+    uint64_t s_overflow, p_overflow; /* lists kept outside their head */
+    uint64_t label_entries;          /* Lin + Lout entries */
+    double pll_ms, build_ms;         /* the labels / labels and heads (host) */
 } ketogpu_label_view;
-int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode, uint32_t s_words,
+int ketogpu_label_index_build(const ketogpu_snapshot *s, uint32_t s_head_words, uint32_t p_head_words,
                               ketogpu_label_index **out);
 int ketogpu_label_index_view(const ketogpu_label_index *l, ketogpu_label_view *out);
 void ketogpu_label_index_free(ketogpu_label_index *l);
@@ -432,12 +439,20 @@ typedef struct {
     uint64_t closure_nodes_f, closure_nodes_b;      /* nodes with a closure row          */
     uint64_t closure_entries_f, closure_entries_b;  /* records in closure rows           */
     double core_build_ms;       /* one-time build of the core arrays at engine creation */
-    /* plan 7 "label" (closure labels over plan core's arrays: one intersection of two short
-     * lists per request, plan core's traversal for units with an unlabelled request) */
-    int32_t label_mode;         /* 0 backward labels, 1 forward labels, -1 off         */
-    double label_coverage;      /* labelled share of the label nodes with a non-empty row */
-    double label_build_ms;
-    uint32_t label_words;       /* S block words (64 / 128: labels of <= 63 / 127 nodes) */
+    /* plan 7 "label" (2-hop reachability labels, labels.hpp: one intersection of two short
+     * sorted lists per request; requests without labels — wildcard roots — go to a second
+     * stage, plan lite over the listed requests) */
+    int32_t label_on;           /* 1: labels built                                      */
+    double label_coverage;      /* share of the non-empty S heads with a label (1 unless
+                                 * KETOGPU_LABEL_REST_PERMILLE marks some for the second stage) */
+    double label_build_ms;      /* one-time build at engine creation (labels + heads)   */
+    uint32_t label_s_head;      /* S / P head words (8, 16 or 32)                       */
+    uint32_t label_p_head;
+    double label_pll_ms;        /* of which the 2-hop labels                            */
+    uint64_t label_bytes;       /* S + P arrays in HBM                                  */
+    uint64_t label_entries;     /* Lin + Lout entries                                   */
+    uint64_t rest_requests;     /* requests of this run answered by the second stage    */
+    double rest_ms;             /* second stage + statistics (events between kernels)   */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 /* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory) record a

@@ -102,8 +102,10 @@ class RunStats(C.Structure):
         ("hubs", C.c_uint32), ("hub_words", C.c_uint32), ("hub_build_ms", C.c_double),
         ("plan_unit", C.c_uint32), ("closure_cap_f", C.c_uint32), ("closure_cap_b", C.c_uint32),
         ("closure_nodes_f", C.c_uint64), ("closure_nodes_b", C.c_uint64), ("closure_entries_f", C.c_uint64),
-        ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double), ("label_mode", C.c_int32),
-        ("label_coverage", C.c_double), ("label_build_ms", C.c_double), ("label_words", C.c_uint32)]
+        ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double), ("label_on", C.c_int32),
+        ("label_coverage", C.c_double), ("label_build_ms", C.c_double), ("label_s_head", C.c_uint32),
+        ("label_p_head", C.c_uint32), ("label_pll_ms", C.c_double), ("label_bytes", C.c_uint64),
+        ("label_entries", C.c_uint64), ("rest_requests", C.c_uint64), ("rest_ms", C.c_double)]
 
     PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core", 7: "label"}
 
@@ -147,11 +149,11 @@ class CoreRecords(C.Structure):
 
 
 class LabelView(C.Structure):
-    _fields_ = [("mode", C.c_int32), ("s_block_words", C.c_uint32), ("p_block_words", C.c_uint32),
-                ("p_words", C.POINTER(C.c_uint32)),
-                ("s_words", C.POINTER(C.c_uint32)), ("num_p_words", C.c_uint64), ("num_s_words", C.c_uint64),
-                ("p_nodes", C.c_uint64), ("s_nodes", C.c_uint64), ("labelled", C.c_uint64), ("nonempty", C.c_uint64),
-                ("coverage_b", C.c_double), ("coverage_f", C.c_double)]
+    _fields_ = [("s_head_words", C.c_uint32), ("p_head_words", C.c_uint32),
+                ("s_words", C.POINTER(C.c_uint32)), ("p_words", C.POINTER(C.c_uint32)),
+                ("num_s_words", C.c_uint64), ("num_p_words", C.c_uint64)] + [(n, C.c_uint64) for n in (
+        "s_nodes", "p_nodes", "s_entries", "p_entries", "s_overflow", "p_overflow", "label_entries")] + [
+        ("pll_ms", C.c_double), ("build_ms", C.c_double)]
 
 
 class CommStats(C.Structure):
@@ -309,7 +311,7 @@ SIGNATURES = {
     "ketogpu_core_index_view": (C.c_int, [vp, C.c_int, C.POINTER(CoreRecords)]),
     "ketogpu_core_index_free": (None, [vp]),
     "ketogpu_comm_stats_get": (C.c_int, [vp, C.POINTER(CommStats)]),
-    "ketogpu_label_index_build": (C.c_int, [vp, C.POINTER(u32), C.c_int, u32, C.POINTER(vp)]),
+    "ketogpu_label_index_build": (C.c_int, [vp, u32, u32, C.POINTER(vp)]),
     "ketogpu_label_index_view": (C.c_int, [vp, C.POINTER(LabelView)]),
     "ketogpu_label_index_free": (None, [vp]),
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),

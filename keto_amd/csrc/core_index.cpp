@@ -80,7 +80,9 @@ struct Closer {
 
 }  // namespace
 
-void build_core_index(const Snapshot &s, const uint32_t cap_in[2], const uint32_t block_in[2], CoreIndex &out) {
+void build_core_index(const Snapshot &s, const uint32_t cap_in[2], const uint32_t block_in[2], CoreIndex &out,
+                      uint64_t max_bytes) {
+    uint64_t bytes_before = 0;  // records of the directions already laid out
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t Ni = s.Ni;
     if (s.writable) throw Error(KETOGPU_EINVAL, "plan core: writable snapshots change closures in place");
@@ -183,6 +185,10 @@ void build_core_index(const Snapshot &s, const uint32_t cap_in[2], const uint32_
         }
         const uint64_t obase = bbase + (nodes << lg);
         const uint64_t total = obase + acc;
+        if (max_bytes && (bytes_before + total) * sizeof(CoreRec) > max_bytes)
+            throw Error(KETOGPU_ENOMEM, "plan core: " + std::to_string((bytes_before + total) * sizeof(CoreRec)) +
+                                            " bytes of records, budget " + std::to_string(max_bytes));
+        bytes_before += total;
         std::vector<CoreRec> &R = out.rec[d];
         R.clear();
         R.resize(total);

@@ -79,6 +79,9 @@ struct CoreIndex {
 // records per node block (a power of two in 4..32), 0 = chosen from the row lengths (the
 // smallest block holding at least 95% of the non-empty seed rows).  Throws
 // Error(KETOGPU_EINVAL) when the core and closure rows pass 2^32 records (32-bit begins).
-void build_core_index(const Snapshot &s, const uint32_t cap[2], const uint32_t block[2], CoreIndex &out);
+// max_bytes: Error(KETOGPU_ENOMEM) when both directions' records pass it (0: no limit),
+// before the record arrays are allocated.
+void build_core_index(const Snapshot &s, const uint32_t cap[2], const uint32_t block[2], CoreIndex &out,
+                      uint64_t max_bytes = 0);
 
 }  // namespace ketogpu

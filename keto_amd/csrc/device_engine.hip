@@ -2508,102 +2508,117 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 }
 
 // ----------------------------------------------------------------------- plan label
-// Closure labels (labels.hpp): per request one S list (sorted, <= 63 nodes) and one P list;
-// allowed <=> they share a node.  One wave per 16-request unit: four lanes per request
-// copy its S block into LDS (the second half only when the label has more than 31 nodes)
-// and hold its P block in registers; each P entry is looked up in S by a 6-step binary
-// search.  A request without a label (or with a wildcard root) is listed (spill_out, one
-// request index each) for the second stage, label_rest_kernel: plan core's traversal over
-// the listed requests, gathered 16 to a unit.
+// 2-hop reachability labels (labels.hpp): per request one S list (target t) and one P list
+// (root r), each behind a fixed-size HEAD of HS / HP words [count | overflow start / 16 |
+// mask lo | mask hi | entries ascending | 0xFFFFFFFF pad]; allowed <=> the masks share a
+// bit or the lists share an entry.  One wave per 16-request unit: four lanes per request
+// read its two heads (one dependent HBM read each, both in flight at once), the S entries
+// go to LDS, and every P entry is looked up in them by a branchless binary search.  Lists
+// longer than their head lie whole in the overflow region and are searched / read there.
+// A request without labels (a wildcard root, or the KETOGPU_LABEL_REST_PERMILLE test knob)
+// is listed (one request index each) for the second stage, label_rest_kernel: plan lite's
+// traversal over the listed requests, gathered 16 to a unit.
 struct LabelGraph {
-    const uint32_t *P, *S;  // P blocks (+ overflow), S blocks (SW words each)
-    int mode;               // 0 = B (S node t, P node r), 1 = F (S node r, P node t)
+    const uint32_t *P, *S;  // head arrays (+ overflow lists)
 };
 // The unlabelled requests' list is sharded: unit u appends to region u % kRestShards of
 // the list (region capacity `rest_cap` = 16 x ceil(units / kRestShards)) at counter
-// rest_count[(u % kRestShards) * kRestStride] — one cache line per counter, so ~15k
-// appends per 10^6 requests do not serialize on one address.  Two counter sets alternate
-// between calls: a call's first stage (workgroup 0) clears the other set for the next call.
+// rest_count[(u % kRestShards) * kRestStride] — one cache line per counter, so appends do
+// not serialize on one address.  Two counter sets alternate between calls: a call's first
+// stage (workgroup 0) clears the other set for the next call.
 constexpr int kRestShards = 64, kRestStride = 32;
 struct LabelRest {
     uint32_t *list;
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
 };
-// A request's S list in LDS: the first LW words of its S block (LW + 1 words a request,
-// odd: the 16 lists start in different banks).  LW < SW (label_kernel over 128-word S
-// blocks): a label of more than LW - 1 nodes (rare) is searched in place in its block (L2)
-// instead, so label_kernel keeps the LDS footprint, and the occupancy, of 64-word blocks
-// (0.055 vs 0.095 ms per 10^6 config #2 requests); the PCIe-bound host kernel keeps whole
-// labels in LDS (LW = SW: no dependent L2 reads behind the request reads, 0.172 vs 0.190 ms)
-template <int LW>
+// A request's S entries in LDS: HS words (the head's HS - 4 inline entries, then 4 pad
+// words) + 1, odd: the 16 lists start in different banks
+template <int HS>
 struct LabelShared {
-    uint32_t S[16 * (LW + 1)];
+    uint32_t S[16 * (HS + 1)];
 };
 
-// number of S entries (words 1..SW-1, ascending, padded with 0xFFFFFFFF) below x, then x found
-template <int SW>
+// x among the W (a power of two) ascending entries of S (padded with 0xFFFFFFFF, which is
+// no entry)
+template <int W>
 __device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
     uint32_t pos = 0;
 #pragma unroll
-    for (uint32_t step = SW / 2; step; step >>= 1)
-        if (S[pos + step] < x) pos += step;
-    return pos < SW - 1 && S[pos + 1] == x;
+    for (uint32_t step = W / 2; step; step >>= 1)
+        if (S[pos + step - 1] < x) pos += step;
+    return S[pos] == x;
+}
+// x among the n ascending entries of an overflow list (global memory)
+__device__ __forceinline__ bool label_find_n(const uint32_t *S, uint32_t n, uint32_t x) {
+    const uint32_t n0 = n;
+    uint32_t lo = 0;
+    while (n) {
+        const uint32_t half = n >> 1;
+        if (S[lo + half] < x) {
+            lo += half + 1;
+            n -= half + 1;
+        } else {
+            n = half;
+        }
+    }
+    return lo < n0 && S[lo] == x;
 }
 
-template <int PB, int SW, int LW>
-__device__ __forceinline__ void label_unit(LabelShared<LW> &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
+// this lane's W words of a head (lane `sub` of the request's four: words [W sub, W sub + W))
+template <int W>
+__device__ __forceinline__ void label_head_load(const uint32_t *head, uint32_t sub, uint32_t (&w)[W]) {
+    if constexpr (W == 2) {
+        const uint2 a = reinterpret_cast<const uint2 *>(head)[sub];
+        w[0] = a.x, w[1] = a.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < W / 4; k++) {
+            const uint4 a = reinterpret_cast<const uint4 *>(head)[(W / 4) * sub + k];
+            w[4 * k] = a.x, w[4 * k + 1] = a.y, w[4 * k + 2] = a.z, w[4 * k + 3] = a.w;
+        }
+    }
+}
+// word j (< 4: count, overflow start, mask lo, mask hi) of the request's head, on every lane
+template <int W, int J>
+__device__ __forceinline__ uint32_t label_word(const uint32_t (&w)[W], uint32_t lane) {
+    return (uint32_t)__shfl((int)w[J % W], (int)((lane & ~3u) + J / W), 64);
+}
+
+template <int HS, int HP>
+__device__ __forceinline__ void label_unit(LabelShared<HS> &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
                                            uint64_t *allowed, const uint64_t unit, const LabelRest &R,
                                            unsigned long long *stats) {
-    static_assert(PB == 16 || PB == 32 || PB == 64, "P blocks of 16, 32 or 64 words");
-    static_assert(SW == 64 || SW == 128, "S blocks of 64 or 128 words");
-    static_assert(LW == 64 || LW == SW, "LDS lists of 64 words or whole blocks");
-    constexpr int PW = PB / 4;  // P words per lane
+    static_assert((HS == 8 || HS == 16 || HS == 32) && (HP == 8 || HP == 16 || HP == 32), "heads of 8, 16 or 32 words");
+    constexpr int SW = HS / 4, PW = HP / 4;  // head words per lane
     const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
     const bool valid = some && r < kDynBase;
-    const uint32_t xs = L.mode == 0 ? t : r, xp = L.mode == 0 ? r : t;
-    uint32_t sw[8], pw[PW];
+    uint32_t sw[SW], pw[PW];
 #pragma unroll
-    for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
+    for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < PW; k++) pw[k] = 0u;
-    if (valid) {  // both blocks in flight at once: one dependent HBM read per request
-        const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * SW) + 2 * sub;
-        const uint4 *pb = reinterpret_cast<const uint4 *>(L.P + (uint64_t)xp * PB) + (PW / 4) * sub;
-        const uint4 a = sb[0], b = sb[1];
-        sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
-#pragma unroll
-        for (int k = 0; k < PW / 4; k++) {
-            const uint4 c = pb[k];
-            pw[4 * k] = c.x, pw[4 * k + 1] = c.y, pw[4 * k + 2] = c.z, pw[4 * k + 3] = c.w;
-        }
+    if (valid) {  // both heads in flight at once: one dependent HBM read per request
+        label_head_load<SW>(L.S + (uint64_t)t * HS, sub, sw);
+        label_head_load<PW>(L.P + (uint64_t)r * HP, sub, pw);
     }
-    uint32_t *S = sh.S + q * (LW + 1);
-    if (!valid && sub == 0) sw[0] = some ? kNoLabel : 0u;  // a wildcard root: no label; an id NONE: empty
+    const uint32_t ns = label_word<SW, 0>(sw, lane), np = label_word<PW, 0>(pw, lane);
+    const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
+    const uint64_t smask = (uint64_t)label_word<SW, 2>(sw, lane) | (uint64_t)label_word<SW, 3>(sw, lane) << 32;
+    const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw, lane) | (uint64_t)label_word<PW, 3>(pw, lane) << 32;
+    // (the overflow starts read here: no cross-lane reads inside the divergent search below)
+    const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw, lane) * 16;
+    const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw, lane) * 16;
+    // the head's inline entries (words 4..HS-1) to LDS positions 0..HS-5, pad at HS-4..HS-1
+    uint32_t *S = sh.S + q * (HS + 1);
 #pragma unroll
-    for (int k = 0; k < 8; k++) S[8 * sub + k] = sw[k];
-    const uint32_t ns = (uint32_t)__shfl((int)sw[0], (int)(lane & ~3u), 64);  // the label's count
-    const bool labelled = valid && ns != kNoLabel;
-    // the block's further lines (words 32p..32p+31) only for a label of more than 32p - 1
-    // nodes; a label past the LDS list is searched in its block instead
-    const bool wide = LW < SW && labelled && ns > LW - 1;
-#pragma unroll
-    for (int part = 1; part < LW / 32; part++) {
-        if (labelled && ns > 32 * part - 1 && !wide) {
-            const uint4 *sb = reinterpret_cast<const uint4 *>(L.S + (uint64_t)xs * SW + 32 * part) + 2 * sub;
-            const uint4 a = sb[0], b = sb[1];
-            sw[0] = a.x, sw[1] = a.y, sw[2] = a.z, sw[3] = a.w, sw[4] = b.x, sw[5] = b.y, sw[6] = b.z, sw[7] = b.w;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; k++) sw[k] = 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) S[32 * part + 8 * sub + k] = sw[k];
+    for (int k = 0; k < SW; k++) {
+        const uint32_t w = SW * sub + k;
+        S[(w + HS - kHeadFixed) % HS] = w < kHeadFixed ? 0xFFFFFFFFu : sw[k];
     }
-    const uint32_t *Sg = L.S + (uint64_t)xs * SW;
-    // a request without a label (or with a wildcard root): listed for the second stage
+    // a request without labels (or with a wildcard root): listed for the second stage
     {
         const bool rest = sub == 0 && some && !labelled;
         const uint32_t shard = (uint32_t)(unit % kRestShards);
@@ -2611,28 +2626,30 @@ __device__ __forceinline__ void label_unit(LabelShared<LW> &sh, const LabelGraph
         if (rest) R.list[shard * R.cap + at] = (uint32_t)(unit * 16 + q);
     }
     __syncthreads();
-    const uint32_t np = (uint32_t)__shfl((int)pw[0], (int)(lane & ~3u), 64);
-    const uint32_t ovf = (uint32_t)__shfl((int)pw[1], (int)(lane & ~3u), 64);
-    bool hit = false;
+    bool hit = labelled && (smask & pmask) != 0;
     uint32_t looked = 0;
-    if (labelled) {
+    if (labelled && !hit) {
+        const bool s_in = ns <= (uint32_t)(HS - kHeadFixed);
+        auto find = [&](uint32_t x) { return s_in ? label_find<HS>(S, x) : label_find_n(Sg, ns, x); };
+        if (np <= (uint32_t)(HP - kHeadFixed)) {
 #pragma unroll
-        for (int k = 0; k < PW; k++) {
-            const uint32_t w = PW * sub + k;  // the entry of word w is entry w - 2
-            if (w >= 2 && w - 2 < np) {
-                hit |= wide ? label_find<SW>(Sg, pw[k]) : label_find<LW>(S, pw[k]);
+            for (int k = 0; k < PW; k++) {
+                const uint32_t w = PW * sub + k;  // word w holds entry w - 4
+                if (w >= kHeadFixed && w - kHeadFixed < np) {
+                    hit |= find(pw[k]);
+                    looked++;
+                }
+            }
+        } else {  // the whole P list in the overflow region
+            for (uint32_t k = sub; k < np && !hit; k += 4) {
+                hit |= find(Pg[k]);
                 looked++;
             }
         }
-        if (np > (uint32_t)PB - 2)  // the row's entries past its block
-            for (uint32_t k = PB - 2 + sub; k < np; k += 4) {
-                const uint32_t x = L.P[(uint64_t)ovf * 16 + (k - (PB - 2))];
-                hit |= wide ? label_find<SW>(Sg, x) : label_find<LW>(S, x);
-                looked++;
-            }
     }
     const uint64_t bits = __ballot(hit);
-    uint64_t rows = labelled && sub == 0 ? 2 : 0, ent = looked + (labelled && sub == 0 ? ns : 0);
+    uint64_t rows = labelled && sub == 0 ? 2 : 0;
+    uint64_t ent = looked + (labelled && sub == 0 ? ns + kHeadFixed : 0);  // + the two masks (4 words)
 #pragma unroll
     for (int k = 32; k; k >>= 1) {
         rows += __shfl_down(rows, k, 64);
@@ -2653,26 +2670,26 @@ __device__ __forceinline__ void label_clear_next(const LabelRest &R) {
     if (blockIdx.x == 0) R.next_count[threadIdx.x * kRestStride] = 0u;  // 64 lanes: every shard
 }
 
-template <int PB, int SW>
+template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t *roots, const uint32_t *targets,
                                                    uint64_t n, uint64_t *allowed, LabelRest R,
                                                    unsigned long long *stats, uint64_t unit0) {
-    __shared__ LabelShared<64> sh;
+    __shared__ LabelShared<HS> sh;
     if (unit0 == 0) label_clear_next(R);
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
-    label_unit<PB, SW, 64>(sh, L, r, t, allowed, unit, R, stats);
+    label_unit<HS, HP>(sh, L, r, t, allowed, unit, R, stats);
 }
 
 // pinned host requests read in place (host_unit_requests)
-template <int K, int PB, int SW>
+template <int K, int HS, int HP>
 __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L, const uint32_t *hr,
                                                         const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
                                                         uint64_t *allowed, LabelRest R, unsigned long long *stats,
                                                         unsigned long long *first_bad) {
-    __shared__ LabelShared<SW> sh;
+    __shared__ LabelShared<HS> sh;
     label_clear_next(R);
     uint32_t r[K], t[K];
     host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
@@ -2685,17 +2702,18 @@ __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L
 #pragma unroll
         for (int j = 1; j < K; j++)
             if (j == k) rk = r[j], tk = t[j];
-        label_unit<PB, SW, SW>(sh, L, rk, tk, allowed, unit, R, stats);
+        label_unit<HS, HP>(sh, L, rk, tk, allowed, unit, R, stats);
         __syncthreads();
     }
 }
 
-// the second stage: plan core's traversal over the requests the labels did not answer
+// the second stage: plan lite's traversal over the requests the labels did not answer
 // (in: request indices, *in_count of them, written by the first stage on this stream),
 // gathered 16 to a unit; persistent over the listed requests.  A unit that outgrows its
-// table lists its requests (out) for the multi-word global path.
+// table lists its requests (out) for the multi-word global path (which also takes the
+// wildcard roots).
 template <class SH>
-__global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *cf, const FRec *cb,
+__global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *frec, const FRec *brec,
                                                         const uint32_t *roots, const uint32_t *targets,
                                                         uint64_t *allowed, LabelRest R, unsigned int *total,
                                                         uint32_t *out, unsigned int *out_count,
@@ -2721,8 +2739,8 @@ __global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *
             r = roots[idx];
             t = targets[idx];
         }
-        lite_unit<SH, true>(S, g, cf, cb, core_load_rows(g, cf, cb, r, t), allowed, u, out, out_count, stats,
-                            nullptr, idx, true);
+        lite_unit<SH, false>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, u, out, out_count, stats, nullptr,
+                             idx, true);
         __syncthreads();
     }
 }
@@ -3710,9 +3728,9 @@ struct ketogpu_engine {
     uint32_t core_blk_log[2] = {0, 0}, core_block[2] = {0, 0};  // KETOGPU_CORE_BLOCKS="forward,backward" records
     uint64_t core_overflow[2] = {0, 0};
     uint32_t closure_cap[2] = {64, 64};
-    // plan "label" (label_kernel): closure labels over plan core's arrays (labels.hpp);
-    // KETOGPU_LABEL_MODE = B / F forces a mode, default: the better-covered one (none when
-    // both label less than half of the nodes)
+    // plan "label" (label_kernel): 2-hop reachability labels (labels.hpp), built at engine
+    // creation; when they are, plan core and the hub index are not built (nothing would use
+    // them: every request but wildcard roots is one intersection)
     bool use_label = false;
     LabelGraph lgraph{};
     unsigned int *rest_counts = nullptr;  // two sets of kRestShards counters, one cache line each
@@ -3723,30 +3741,28 @@ struct ketogpu_engine {
         return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
                          rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
     }
-    uint32_t label_pb = 32, label_sw = 64;
-    double label_coverage = 0, label_build_ms = 0;
-    // plan label, host batches (K units per workgroup)
-    template <int K>
+    uint32_t label_hs = 16, label_hp = 8;  // head words of S and P
+    double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
+    uint64_t label_bytes = 0, label_entries = 0;
+    // a head-size pair (HS, HP) as template arguments
+    template <class F>
+    void label_dispatch(F &&f) {
+        auto hp = [&](auto hs) {
+            if (label_hp == 8) f(hs, std::integral_constant<int, 8>{});
+            else if (label_hp == 16) f(hs, std::integral_constant<int, 16>{});
+            else f(hs, std::integral_constant<int, 32>{});
+        };
+        if (label_hs == 8) hp(std::integral_constant<int, 8>{});
+        else if (label_hs == 16) hp(std::integral_constant<int, 16>{});
+        else hp(std::integral_constant<int, 32>{});
+    }
+    // plan label, host batches (4 units per workgroup)
     void launch_label_host(const Batch &q, const HostSrc *src, uint64_t bunits) {
-#define KETO_LH(PB, SW)                                                                                    \
-    KLAUNCH((label_host_kernel<K, PB, SW>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), 0, stream, g, lgraph, \
-            src->roots, src->targets, io->d_roots, io->d_targets, q.n, q.allowed, label_rest(q.n), st.stats, d_bad)
-        if (label_sw == 64) {
-            if (label_pb == 16)
-                KETO_LH(16, 64);
-            else if (label_pb == 32)
-                KETO_LH(32, 64);
-            else
-                KETO_LH(64, 64);
-        } else {
-            if (label_pb == 16)
-                KETO_LH(16, 128);
-            else if (label_pb == 32)
-                KETO_LH(32, 128);
-            else
-                KETO_LH(64, 128);
-        }
-#undef KETO_LH
+        label_dispatch([&](auto hs, auto hp) {
+            KLAUNCH((label_host_kernel<4, decltype(hs)::value, decltype(hp)::value>), dim3((unsigned)((bunits + 3) / 4)),
+                    dim3(64), 0, stream, g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n,
+                    q.allowed, label_rest(q.n), st.stats, d_bad);
+        });
     }
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
     uint64_t closure_nodes[2] = {0, 0}, closure_entries[2] = {0, 0};
@@ -3794,26 +3810,11 @@ struct ketogpu_engine {
                      const unsigned int *in_count, uint32_t *out, unsigned int *out_count, unsigned long long *stats,
                      unsigned long long *stp, uint64_t unit0 = 0, hipStream_t stream = nullptr, bool chunked = false) {
         if (!stream) stream = this->stream;
-        if (c.lite == 3) {  // plan label: closure labels, plan core for units without
-#define KETO_LABEL_K(PB, SW)                                                                                    \
-    KLAUNCH((label_kernel<PB, SW>), dim3(grid), dim3(64), pad, stream, lgraph, q.roots, q.targets, q.n, q.allowed, \
-            label_rest(q.n), stats, unit0)
-            if (label_sw == 64) {
-                if (label_pb == 16)
-                    KETO_LABEL_K(16, 64);
-                else if (label_pb == 32)
-                    KETO_LABEL_K(32, 64);
-                else
-                    KETO_LABEL_K(64, 64);
-            } else {
-                if (label_pb == 16)
-                    KETO_LABEL_K(16, 128);
-                else if (label_pb == 32)
-                    KETO_LABEL_K(32, 128);
-                else
-                    KETO_LABEL_K(64, 128);
-            }
-#undef KETO_LABEL_K
+        if (c.lite == 3) {  // plan label: 2-hop labels, plan lite for requests without
+            label_dispatch([&](auto hs, auto hp) {
+                KLAUNCH((label_kernel<decltype(hs)::value, decltype(hp)::value>), dim3(grid), dim3(64), pad, stream,
+                        lgraph, q.roots, q.targets, q.n, q.allowed, label_rest(q.n), stats, unit0);
+            });
             return;
         }
         if (c.lite == 2) {  // plan core: lite over the core record arrays
@@ -3915,10 +3916,10 @@ struct ketogpu_engine {
             KLAUNCH((bidi_kernel<4, 11, 256, 64, 7>), dim3(stage_grid(prev, 1280)), dim3(64), 0, stream, g, frec,
                     brec, q.roots, q.targets, q.n, q.allowed, in, in_count, fan, out, out_count, stats, nullptr, 0);
             return;
-        case 'L':  // plan label's second stage: plan core over the listed requests (in: request indices)
-            KLAUNCH((label_rest_kernel<TierStage1>), dim3(stage_grid(prev / 16 + 1, 256 * 4)), dim3(64), 0, stream,
-                    gcore(), core_rec[0], core_rec[1], q.roots, q.targets, q.allowed, label_rest(q.n),
-                    const_cast<unsigned int *>(in_count), out, out_count, stats);
+        case 'L':  // plan label's second stage: plan lite over the listed requests (in: request indices)
+            KLAUNCH((label_rest_kernel<TierStage1>), dim3(stage_grid(prev / 16 + 1, 256 * 4)), dim3(64), 0, stream, g,
+                    frec, brec, q.roots, q.targets, q.allowed, label_rest(q.n), const_cast<unsigned int *>(in_count),
+                    out, out_count, stats);
             return;
         default:
             KLAUNCH((bidi_kernel<1, 13, 1024, 256, 7>), dim3(stage_grid(prev, 256)), dim3(256), 0, stream, g, frec,
@@ -4150,10 +4151,10 @@ struct ketogpu_engine {
         };
         // bidi / lite: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_lite = lite_req && use_v2 && !s.has_ambiguous && lite_ok;
-        // plan core: not on writable snapshots (an in-place write would change closures)
-        use_core = (p == "core" || p == "label" || p == "auto") && use_lite && !s.writable &&
-                   getenv("KETOGPU_NO_CORE") == nullptr;
-        use_label = (p == "label" || p == "auto") && use_core && getenv("KETOGPU_NO_LABEL") == nullptr;
+        // plan core and plan label: not on writable snapshots (an in-place write would change
+        // closures and labels)
+        use_core = (p == "core" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_CORE") == nullptr;
+        use_label = (p == "label" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_LABEL") == nullptr;
         if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
         if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
         if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
@@ -4170,7 +4171,7 @@ struct ketogpu_engine {
             use_bidi = true;
             bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 2};
         }
-        if (p == "label" && use_label) {  // forced: plan label (falls back to core if no mode labels enough)
+        if (p == "label" && use_label) {  // forced: plan label (falls back to lite if the labels do not fit)
             use_bidi = true;
             bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 3};
         }
@@ -4201,11 +4202,10 @@ struct ketogpu_engine {
             }
             if (use_lite) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan "lite"
             if (use_core) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 2});  // plan "core"
-            if (use_label) candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 3});  // plan "label"
             if (use_v2) candidates.push_back({false, c.hlog, c.bt, c.f, c.lf, 0});
             // batches below the trial size run lite until the trials have picked a plan
             // (round 3: lite 0.284 vs bidi 0.367 ms per 10^6 config #2 requests)
-            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, use_label ? 3 : use_core ? 2 : 1};
+            if (use_lite && !bc) bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, use_core ? 2 : 1};
             use_bidi = use_bidi || use_lite;
         }
         if (const char *cs = getenv("KETOGPU_CASCADE")) {  // spill stages, e.g. "w,q,s" (default) or "q,s"
@@ -4237,6 +4237,10 @@ struct ketogpu_engine {
         g.Ni = s.Ni;
         g.Nx = s.Nx;
         g.N = s.N;
+        // plan label first: when its labels are built every request but wildcard roots is
+        // one intersection, so neither plan core's index nor the hub index is built, and no
+        // trials run (KETOGPU_UNITS=auto)
+        if (use_label) build_label(s);
         g.both_max = kBothMax;
         g.seed_shift = 0;
         if (const char *sh = getenv("KETOGPU_TEST_BEGIN_SHIFT")) g.seed_shift = strtoull(sh, nullptr, 0);
@@ -4321,15 +4325,19 @@ struct ketogpu_engine {
     // core records
     void build_core(const Snapshot &s) {
         CoreIndex ci;
-        try {
-            build_core_index(s, closure_cap, core_block, ci);
+        size_t free_b = 0, total_b = 0;
+        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        try {  // (the record arrays' size is checked against a quarter of free HBM before allocating)
+            build_core_index(s, closure_cap, core_block, ci, free_b / 4);
         } catch (const Error &e) {
             fprintf(stderr, "[ketogpu] plan core disabled: %s\n", e.what());
             drop_core();
             return;
+        } catch (const std::bad_alloc &) {
+            fprintf(stderr, "[ketogpu] plan core disabled: out of host memory\n");
+            drop_core();
+            return;
         }
-        size_t free_b = 0, total_b = 0;
-        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
         const uint64_t bytes = (ci.rec[0].size() + ci.rec[1].size()) * sizeof(CoreRec);
         if (bytes > free_b / 4) {
             fprintf(stderr, "[ketogpu] plan core disabled: %llu bytes of records, %llu free\n",
@@ -4348,7 +4356,6 @@ struct ketogpu_engine {
             closure_entries[d] = ci.closure_entries[d];
         }
         core_build_ms = ci.build_ms;
-        if (use_label) build_label(s, ci, free_b - bytes);
         if (cascade_log)
             fprintf(stderr, "[core] closure rows: forward %llu nodes / %llu entries, backward %llu / %llu (caps %u, %u); "
                             "blocks of %u / %u records, %llu / %llu rows in overflow; %.2f GB; built in %.1f ms\n",
@@ -4357,49 +4364,38 @@ struct ketogpu_engine {
                     closure_cap[1], 1u << core_blk_log[0], 1u << core_blk_log[1], (unsigned long long)core_overflow[0],
                     (unsigned long long)core_overflow[1], (double)bytes / 1e9, core_build_ms);
     }
-    void drop_core() {
-        use_core = false;
-        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite >= 2; }),
-                         candidates.end());
-        if (bidi_cfg.lite >= 2) bidi_cfg.lite = 1;
-        drop_label();
-    }
     void drop_label() {
         use_label = false;
-        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite == 3; }),
-                         candidates.end());
         if (bidi_cfg.lite == 3) bidi_cfg.lite = use_core ? 2 : 1;
     }
-    // plan label's closure labels (labels.hpp) over the core index just built
-    void build_label(const Snapshot &s, const CoreIndex &ci, uint64_t free_b) {
-        int mode = -1;
-        if (const char *e = getenv("KETOGPU_LABEL_MODE")) mode = e[0] == 'F' || e[0] == 'f' ? 1 : 0;
-        // S blocks of 128 words (labels of up to 127 nodes: fewer requests for the second
-        // stage) when they fit an eighth of free HBM, else 64 (KETOGPU_LABEL_WORDS)
-        uint32_t sw = (uint64_t)s.N * 512 <= free_b / 8 ? 128 : 64;
-        if (const char *e = getenv("KETOGPU_LABEL_WORDS")) sw = atoi(e) == 128 ? 128 : 64;
+    void drop_core() {
+        use_core = false;
+        candidates.erase(std::remove_if(candidates.begin(), candidates.end(), [](const Candidate &c) { return c.lite == 2; }),
+                         candidates.end());
+        if (bidi_cfg.lite == 2) bidi_cfg.lite = 1;
+    }
+    // plan label's 2-hop labels and heads (labels.hpp), built on the host and uploaded; the
+    // arrays must fit half of the HBM left after the graph (and its edge records) and the
+    // host's memory (the size is known before anything is allocated).  On success the plan
+    // is label without trials, plan core and the hub index are skipped; on failure the
+    // engine goes on as if labels had not been asked for.
+    void build_label(const Snapshot &s) {
+        size_t free_b = 0, total_b = 0;
+        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        const uint64_t records = 16ull * (s.fint_col.size() + s.rev_col.size());
+        const uint64_t budget = free_b > records ? (free_b - records) / 2 : 0;
+        uint32_t hs = 0, hp = 0, permille = 0;
+        if (const char *e = getenv("KETOGPU_LABEL_HEADS")) sscanf(e, "%u,%u", &hs, &hp);
+        if (const char *e = getenv("KETOGPU_LABEL_REST_PERMILLE")) permille = (uint32_t)std::min(1000, std::max(0, atoi(e)));
         LabelIndex li;
         try {
-            build_labels(s, ci, mode, 0.5, li, sw);
+            build_labels(s, hs, hp, permille, budget, li);
         } catch (const Error &e) {
             fprintf(stderr, "[ketogpu] plan label disabled: %s\n", e.what());
             drop_label();
             return;
-        }
-        label_build_ms = li.build_ms;
-        if (li.mode < 0) {
-            if (cascade_log)
-                fprintf(stderr, "[label] no mode labels half of its nodes (B %.3f, F %.3f): plan off\n", li.coverage[0],
-                        li.coverage[1]);
-            drop_label();
-            return;
-        }
-        // up to half of the HBM left after the graph and plan core (config #2's shape at 1e9
-        // rows: 63 GB of labels next to ~75 GB of graph and core records)
-        const uint64_t bytes = 4 * (li.P.size() + li.S.size());
-        if (bytes > free_b / 2) {
-            fprintf(stderr, "[ketogpu] plan label disabled: %llu bytes of labels, %llu free\n",
-                    (unsigned long long)bytes, (unsigned long long)free_b);
+        } catch (const std::bad_alloc &) {
+            fprintf(stderr, "[ketogpu] plan label disabled: out of host memory\n");
             drop_label();
             return;
         }
@@ -4409,15 +4405,28 @@ struct ketogpu_engine {
         rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
         owned.push_back(rest_counts);
         HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
-        lgraph = LabelGraph{P, S, li.mode};
-        label_pb = li.pb;
-        label_sw = li.s_words;
-        label_coverage = li.nonempty ? (double)li.covered / (double)li.nonempty : 1.0;
+        lgraph = LabelGraph{P, S};
+        label_hs = li.hs;
+        label_hp = li.hp;
+        label_bytes = 4 * (li.P.size() + li.S.size());
+        label_entries = li.label_entries;
+        label_pll_ms = li.pll_ms;
+        uint64_t nonempty = 0;
+        for (uint64_t x = 0; x < s.N; x++) nonempty += s.rev_off[x + 1] > s.rev_off[x];
+        label_coverage = nonempty ? 1.0 - (double)li.s_nolabel / (double)nonempty : 1.0;
+        // the plan, without trials; neither plan core nor the hubs are built
+        use_core = false;
+        use_bidi = true;
+        bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 3};
+        trials_left = 0;
+        candidates.clear();
+        label_build_ms = li.build_ms;
         if (cascade_log)
-            fprintf(stderr, "[label] mode %c: %llu of %llu S nodes labelled (%.4f; sampled B %.3f F %.3f), S blocks of %u "
-                            "words, P blocks of %u, %.2f GB, built in %.1f ms\n",
-                    li.mode ? 'F' : 'B', (unsigned long long)li.covered, (unsigned long long)li.nonempty,
-                    label_coverage, li.coverage[0], li.coverage[1], li.s_words, li.pb, (double)bytes / 1e9, li.build_ms);
+            fprintf(stderr, "[label] %u landmarks, %llu label entries (%.1f ms); S heads %u words (%llu entries, %llu "
+                            "lists in overflow), P heads %u words (%llu, %llu); %.2f GB; built in %.1f ms\n",
+                    s.Ni, (unsigned long long)li.label_entries, li.pll_ms, li.hs, (unsigned long long)li.s_entries,
+                    (unsigned long long)li.s_overflow, li.hp, (unsigned long long)li.p_entries,
+                    (unsigned long long)li.p_overflow, (double)label_bytes / 1e9, li.build_ms);
     }
 
     // Hub index.  Hubs are the interior nodes with the most interior successors; a search
@@ -4434,8 +4443,10 @@ struct ketogpu_engine {
     static constexpr uint64_t kHubDeg = 8;
     std::vector<uint32_t> hub_nodes, hub_of_h;
     void choose_hubs(const Snapshot &s) {
-        // writable snapshots: an in-place write would change hub closures (no hub index)
+        // writable snapshots: an in-place write would change hub closures (no hub index);
+        // plan label answers without searches (KETOGPU_HUBS still forces the index)
         if (s.has_ambiguous || !s.Ni || s.writable) return;
+        if (use_label && !getenv("KETOGPU_HUBS")) return;
         auto deg = [&](uint32_t v) { return s.fint_off[v + 1] - s.fint_off[v]; };
         uint64_t maxdeg = 0, heavy = 0;
         for (uint32_t v = 0; v < s.Ni; v++) {
@@ -4631,6 +4642,7 @@ struct ketogpu_engine {
             fprintf(stderr, "\n");
         }
         for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
+        if (bidi_cfg.lite == 3) rs.rest_requests = cnt[0];
         for (size_t k = 0; k < stages.size() && k < 8; k++) stage_prev[k] = (uint64_t)cnt[k] * fans[k];
         rs.push_launches += launched;
         rs.unit_launches += launched;
@@ -4741,7 +4753,7 @@ struct ketogpu_engine {
 #define KETO_HOST_K(K)                                                                                     \
     do {                                                                                                   \
         if (bidi_cfg.lite == 3)                                                                            \
-            launch_label_host<K>(q, src, bunits);                                                          \
+            launch_label_host(q, src, bunits);                                                             \
         else if (bidi_cfg.lite == 2 && core_shape == 1)                                                    \
             KLAUNCH((lite_host_kernel<K, CoreShapeS, true>), dim3((unsigned)((bunits + K - 1) / K)), dim3(64), \
                     0, stream, gcore(), core_rec[0], core_rec[1], src->roots, src->targets, io->d_roots,   \
@@ -5072,10 +5084,14 @@ struct ketogpu_engine {
         rs.closure_entries_f = closure_entries[0];
         rs.closure_entries_b = closure_entries[1];
         rs.core_build_ms = core_build_ms;
-        rs.label_mode = use_label ? lgraph.mode : -1;
-        rs.label_words = use_label ? label_sw : 0;
+        rs.label_on = use_label ? 1 : 0;
+        rs.label_s_head = use_label ? label_hs : 0;
+        rs.label_p_head = use_label ? label_hp : 0;
         rs.label_coverage = label_coverage;
         rs.label_build_ms = label_build_ms;
+        rs.label_pll_ms = label_pll_ms;
+        rs.label_bytes = label_bytes;
+        rs.label_entries = label_entries;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();
@@ -5158,6 +5174,7 @@ struct ketogpu_engine {
             HIP_CHECK(hipEventElapsedTime(&ms, unit_ev[i].first, unit_ev[i].second));
             rs.ms_unit += ms;
             if (i == 0) rs.main_ms = ms;
+            if (i == 1 && use_bidi && bidi_cfg.lite == 3) rs.rest_ms = ms;
         }
         for (auto &p : push_ev) {
             HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));

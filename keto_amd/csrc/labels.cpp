@@ -1,166 +1,382 @@
-// labels.cpp — builds the closure labels of plan "label" (labels.hpp).
+// labels.cpp — builds plan "label"'s 2-hop reachability labels and head arrays (labels.hpp).
 #include "labels.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <memory>
-#include <random>
+#include <numeric>
 #include <shared_mutex>
+
+#include "core_index.hpp"  // build_threads, parallel_chunks
 
 namespace ketogpu {
 
 namespace {
 
-constexpr uint32_t kRawMax = 4096;  // a label's entries before deduplication: beyond, no label
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
 
-struct Ctx {
+// the interior graph in both directions: forward fint(v), backward the interior prefix of
+// the sorted rev(v) (the nodes of a path between interior nodes are all interior)
+struct IAdj {
+    const uint32_t *col[2] = {nullptr, nullptr};
+    std::vector<uint64_t> beg[2];
+    std::vector<uint32_t> deg[2];
+};
+
+void make_adj(const Snapshot &s, IAdj &a) {
+    const uint32_t n = s.Ni;
+    a.col[0] = s.fint_col.data();
+    a.col[1] = s.rev_col.data();
+    for (int d = 0; d < 2; d++) {
+        a.beg[d].resize(n);
+        a.deg[d].resize(n);
+    }
+    parallel_chunks(n, 1 << 16, [&](int, uint64_t b, uint64_t e) {
+        for (uint64_t v = b; v < e; v++) {
+            a.beg[0][v] = s.fint_off[v];
+            a.deg[0][v] = (uint32_t)(s.fint_off[v + 1] - s.fint_off[v]);
+            const uint32_t *rb = s.rev_col.data() + s.rev_off[v], *re = s.rev_col.data() + s.rev_off[v + 1];
+            a.beg[1][v] = s.rev_off[v];
+            a.deg[1][v] = (uint32_t)(std::lower_bound(rb, re, n) - rb);
+        }
+    });
+}
+
+// M[v] bit i = landmark order[i] reaches v along direction d (reflexive): a frontier
+// propagation of 64-bit masks, level by level, on every build thread
+void reach_masks(const IAdj &a, const std::vector<uint32_t> &order, uint32_t bits, int d, std::vector<uint64_t> &M) {
+    const uint32_t n = (uint32_t)order.size();
+    std::vector<std::atomic<uint64_t>> A(n), P(n);
+    std::vector<std::atomic<uint8_t>> inq(n);
+    parallel_chunks(n, 1 << 16, [&](int, uint64_t b, uint64_t e) {
+        for (uint64_t v = b; v < e; v++) {
+            A[v].store(0, std::memory_order_relaxed);
+            P[v].store(0, std::memory_order_relaxed);
+            inq[v].store(0, std::memory_order_relaxed);
+        }
+    });
+    std::vector<uint32_t> F;
+    for (uint32_t i = 0; i < bits; i++) {
+        const uint32_t w = order[i];
+        A[w].fetch_or(1ull << i);
+        P[w].fetch_or(1ull << i);
+        if (!inq[w].exchange(1)) F.push_back(w);
+    }
+    const int T = build_threads();
+    std::vector<std::vector<uint32_t>> nxt(T);
+    while (!F.empty()) {
+        parallel_chunks(F.size(), 256, [&](int tid, uint64_t b, uint64_t e) {
+            for (uint64_t k = b; k < e; k++) {
+                const uint32_t y = F[k];
+                inq[y].store(0);
+                const uint64_t dl = P[y].exchange(0);
+                if (!dl) continue;
+                const uint32_t *c = a.col[d] + a.beg[d][y];
+                for (uint32_t j = 0; j < a.deg[d][y]; j++) {
+                    const uint32_t z = c[j];
+                    const uint64_t nw = dl & ~A[z].fetch_or(dl);
+                    if (!nw) continue;
+                    P[z].fetch_or(nw);
+                    if (!inq[z].exchange(1)) nxt[tid].push_back(z);
+                }
+            }
+        });
+        F.clear();
+        for (auto &x : nxt) {
+            F.insert(F.end(), x.begin(), x.end());
+            x.clear();
+        }
+    }
+    M.resize(n);
+    parallel_chunks(n, 1 << 16, [&](int, uint64_t b, uint64_t e) {
+        for (uint64_t v = b; v < e; v++) M[v] = A[v].load(std::memory_order_relaxed);
+    });
+}
+
+// one build thread's search state: visit and mark stamps (landmark rank r, direction d:
+// stamp 2r + 1 + d, never 0), the queue, and the entries found in a parallel batch
+struct Searcher {
+    std::vector<uint32_t> vis, mark, q;
+    std::vector<std::pair<uint32_t, uint32_t>> add[2];  // (node, rank)
+};
+
+}  // namespace
+
+void build_reach_labels(const Snapshot &s, ReachLabels &out) {
+    const auto t0 = Clock::now();
+    out = ReachLabels{};
+    const uint32_t n = s.Ni;
+    out.n = n;
+    if (!n) return;
+    IAdj a;
+    make_adj(s, a);
+    // rank: most central first ((interior out-degree + 1) x (interior in-degree + 1))
+    out.order.resize(n);
+    std::iota(out.order.begin(), out.order.end(), 0u);
+    {
+        std::vector<uint64_t> key(n);
+        for (uint32_t v = 0; v < n; v++) key[v] = (uint64_t)(a.deg[0][v] + 1) * (a.deg[1][v] + 1);
+        std::sort(out.order.begin(), out.order.end(),
+                  [&](uint32_t x, uint32_t y) { return key[x] != key[y] ? key[x] > key[y] : x < y; });
+    }
+    const uint32_t bits = std::min<uint32_t>(n, kMaskBits);
+    out.bits = bits;
+    reach_masks(a, out.order, bits, 0, out.min);
+    reach_masks(a, out.order, bits, 1, out.mout);
+    // pruned searches of the other landmarks; L[0] = Lin, L[1] = Lout (ranks, unsorted
+    // while building: the coverage test marks one side and scans the other)
+    std::vector<std::vector<uint32_t>> L[2];
+    L[0].resize(n);
+    L[1].resize(n);
+    const int T = build_threads();
+    std::vector<Searcher> sr(T);
+    for (auto &x : sr) {
+        x.vis.assign(n, 0);
+        x.mark.assign(n, 0);
+    }
+    const std::vector<uint64_t> *mask[2] = {&out.min, &out.mout};
+    // d = 0: forward from w, entries into Lin (w ->* y); d = 1: backward, into Lout.  The
+    // search prunes at y when the labels so far answer the pair (w, y) (d = 0: Lout(w) meets
+    // Lin(y), or mout(w) meets min(y)); direct = false: entries go to the searcher's list
+    auto search = [&](Searcher &S, uint32_t r, int d, bool direct) {
+        const uint32_t w = out.order[r], st = 2 * r + 1 + (uint32_t)d;
+        for (uint32_t x : L[d ^ 1][w]) S.mark[x] = st;
+        const uint64_t wm = (*mask[d ^ 1])[w];
+        const std::vector<uint64_t> &ym = *mask[d];
+        S.q.clear();
+        S.q.push_back(w);
+        S.vis[w] = st;
+        for (size_t h = 0; h < S.q.size(); h++) {
+            const uint32_t y = S.q[h];
+            if (wm & ym[y]) continue;
+            bool cov = false;
+            for (uint32_t x : L[d][y])
+                if (S.mark[x] == st) {
+                    cov = true;
+                    break;
+                }
+            if (cov) continue;
+            if (direct)
+                L[d][y].push_back(r);
+            else
+                S.add[d].push_back({y, r});
+            const uint32_t *c = a.col[d] + a.beg[d][y];
+            for (uint32_t j = 0; j < a.deg[d][y]; j++) {
+                const uint32_t z = c[j];
+                if (S.vis[z] != st) {
+                    S.vis[z] = st;
+                    S.q.push_back(z);
+                }
+            }
+        }
+    };
+    uint32_t seq = 1024, div = 8;
+    if (const char *e = getenv("KETOGPU_LABEL_SEQ")) seq = (uint32_t)atoi(e);
+    if (const char *e = getenv("KETOGPU_LABEL_BATCH_DIV")) div = std::max(1, atoi(e));
+    uint32_t r = bits;
+    const uint32_t seq_end = (uint32_t)std::min<uint64_t>(n, (uint64_t)bits + seq);
+    for (; r < seq_end; r++) {
+        search(sr[0], r, 0, true);
+        search(sr[0], r, 1, true);
+    }
+    while (r < n) {
+        const uint32_t bs = std::max<uint32_t>((uint32_t)T * 4, r / div);
+        const uint32_t e = (uint32_t)std::min<uint64_t>(n, (uint64_t)r + bs);
+        parallel_chunks(e - r, 8, [&](int tid, uint64_t b, uint64_t f) {
+            for (uint64_t k = b; k < f; k++) {
+                search(sr[tid], r + (uint32_t)k, 0, false);
+                search(sr[tid], r + (uint32_t)k, 1, false);
+            }
+        });
+        // merge: thread t appends the entries of nodes y with y % T == t
+        parallel_chunks((uint64_t)T, 1, [&](int, uint64_t b, uint64_t f) {
+            for (uint64_t t = b; t < f; t++)
+                for (int d = 0; d < 2; d++)
+                    for (auto &x : sr)
+                        for (auto &p : x.add[d])
+                            if (p.first % (uint32_t)T == t) L[d][p.first].push_back(p.second);
+        });
+        for (auto &x : sr)
+            for (int d = 0; d < 2; d++) x.add[d].clear();
+        out.batches++;
+        r = e;
+    }
+    for (auto &x : sr) std::vector<uint32_t>().swap(x.vis), std::vector<uint32_t>().swap(x.mark);
+    // sorted CSR
+    for (int d = 0; d < 2; d++) {
+        std::vector<uint64_t> &off = d == 0 ? out.in_off : out.out_off;
+        std::vector<uint32_t> &col = d == 0 ? out.in : out.out;
+        off.assign((size_t)n + 1, 0);
+        for (uint32_t v = 0; v < n; v++) off[v + 1] = off[v] + L[d][v].size();
+        col.resize(off[n]);
+        parallel_chunks(n, 1 << 14, [&](int, uint64_t b, uint64_t e) {
+            for (uint64_t v = b; v < e; v++) {
+                std::vector<uint32_t> &l = L[d][v];
+                std::sort(l.begin(), l.end());
+                std::copy(l.begin(), l.end(), col.begin() + (ptrdiff_t)off[v]);
+                std::vector<uint32_t>().swap(l);
+            }
+        });
+    }
+    out.ms = ms_since(t0);
+}
+
+namespace {
+
+struct Lists {
     const Snapshot &s;
-    const CoreIndex &ci;
-    int mode;
-    uint32_t words;  // S block words: a label holds at most words - 1 nodes
-    // the S list of node x (mode B: x = t, S = rev(t) + closures of its interior entries;
-    // mode F: x = r, S = {r} + fint(r) + closures of its entries); false: no label
-    bool label(uint64_t x, std::vector<uint32_t> &out) const {
+    const ReachLabels &R;
+    // S(x): Lin of the interior entries of rev(x) + its other entries (raw node ids)
+    void s_list(uint64_t x, std::vector<uint32_t> &out, uint64_t &mask) const {
         out.clear();
-        const int d = mode == 0 ? 1 : 0;  // the closures' direction: backward for B, forward for F
-        const uint64_t *off = mode == 0 ? s.rev_off.data() : s.fint_off.data();
-        const uint32_t *col = mode == 0 ? s.rev_col.data() : s.fint_col.data();
-        const uint32_t *b = col + off[x], *e = col + off[x + 1];
-        if (mode == 1) out.push_back((uint32_t)x);
+        mask = 0;
+        const uint32_t *b = s.rev_col.data() + s.rev_off[x], *e = s.rev_col.data() + s.rev_off[x + 1];
         for (const uint32_t *p = b; p < e; p++) {
-            out.push_back(*p);
-            if (*p >= s.Ni) continue;  // mode B: a source entry (only r itself can be it)
-            const uint32_t n = ci.clo_len[d][*p];
-            if (n == NONE) return false;
-            if (out.size() + n > kRawMax) return false;
-            const CoreRec *c = ci.rec[d].data() + ci.clo_beg[d][*p];
-            for (uint32_t k = 0; k < n; k++) out.push_back(c[k].node);
+            const uint32_t v = *p;
+            if (v < R.n) {
+                mask |= R.min[v];
+                out.insert(out.end(), R.in.begin() + (ptrdiff_t)R.in_off[v], R.in.begin() + (ptrdiff_t)R.in_off[v + 1]);
+            } else {
+                out.push_back(v);
+            }
         }
         std::sort(out.begin(), out.end());
         out.erase(std::unique(out.begin(), out.end()), out.end());
-        return out.size() < words;
     }
-    uint64_t s_nodes() const { return mode == 0 ? s.N : s.Nx; }
-    bool nonempty(uint64_t x) const {
-        const uint64_t *off = mode == 0 ? s.rev_off.data() : s.fint_off.data();
-        return off[x + 1] > off[x];
+    // P(r): Lout(r) for an interior r, else {r} + Lout of every entry of fint(r)
+    void p_list(uint64_t r, std::vector<uint32_t> &out, uint64_t &mask) const {
+        out.clear();
+        if (r < R.n) {
+            mask = R.mout[r];
+            out.assign(R.out.begin() + (ptrdiff_t)R.out_off[r], R.out.begin() + (ptrdiff_t)R.out_off[r + 1]);
+            return;
+        }
+        mask = 0;
+        out.push_back((uint32_t)r);
+        const uint32_t *b = s.fint_col.data() + s.fint_off[r], *e = s.fint_col.data() + s.fint_off[r + 1];
+        for (const uint32_t *p = b; p < e; p++) {
+            mask |= R.mout[*p];
+            out.insert(out.end(), R.out.begin() + (ptrdiff_t)R.out_off[*p], R.out.begin() + (ptrdiff_t)R.out_off[*p + 1]);
+        }
+        std::sort(out.begin(), out.end());
+        out.erase(std::unique(out.begin(), out.end()), out.end());
     }
 };
 
-// labelled share of a sample of S nodes with a non-empty row
-double sample_coverage(const Ctx &c, uint64_t sample) {
-    const uint64_t n = c.s_nodes();
-    if (!n) return 0;
-    std::vector<uint64_t> pick;
-    std::mt19937_64 rng(0x4B45544Full);
-    for (uint64_t k = 0; k < 4 * sample && pick.size() < sample; k++) {
-        const uint64_t x = rng() % n;
-        if (c.nonempty(x)) pick.push_back(x);
+// the smallest head (8, 16 or 32 words) whose inline entries hold >= 95% of the non-empty lists
+uint32_t pick_head(const std::vector<uint32_t> &cnt) {
+    uint64_t ne = 0, fit[3] = {0, 0, 0};
+    for (uint32_t c : cnt) {
+        if (!c) continue;
+        ne++;
+        for (int k = 0; k < 3; k++) fit[k] += c <= (8u << k) - kHeadFixed;
     }
-    if (pick.empty()) return 1.0;
-    std::atomic<uint64_t> hit{0};
-    std::vector<std::vector<uint32_t>> tmp(build_threads());
-    parallel_chunks(pick.size(), 256, [&](int tid, uint64_t b, uint64_t e) {
-        uint64_t h = 0;
-        for (uint64_t i = b; i < e; i++) h += c.label(pick[i], tmp[tid]);
-        hit += h;
-    });
-    return (double)hit.load() / (double)pick.size();
+    for (int k = 0; k < 3; k++)
+        if (fit[k] * 20 >= ne * 19) return 8u << k;
+    return 32;
 }
 
 }  // namespace
 
-void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out,
-                  uint32_t s_words) {
-    if (s_words != 64 && s_words != 128) throw Error(KETOGPU_EINVAL, "plan label: S blocks of 64 or 128 words");
-    const auto t0 = std::chrono::steady_clock::now();
+void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_permille, uint64_t max_bytes,
+                  LabelIndex &out) {
+    const auto t0 = Clock::now();
+    for (uint32_t h : {hs, hp})
+        if (h && h != 8 && h != 16 && h != 32) throw Error(KETOGPU_EINVAL, "plan label: heads of 8, 16 or 32 words");
     out = LabelIndex{};
-    out.s_words = s_words;
-    for (int m = 0; m < 2; m++)
-        if (ci.clo_len[m == 0 ? 1 : 0].size() == s.Ni) out.coverage[m] = sample_coverage(Ctx{s, ci, m, s_words}, 20000);
-    if (mode < 0) {
-        mode = out.coverage[0] >= out.coverage[1] ? 0 : 1;
-        if (out.coverage[mode] < min_coverage) {
-            out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            return;
-        }
-    }
-    if (ci.clo_len[mode == 0 ? 1 : 0].size() != s.Ni)
-        throw Error(KETOGPU_EINVAL, "plan label: the core index has no closure rows in that direction");
-    const Ctx c{s, ci, mode, s_words};
-    out.mode = mode;
-    // S blocks
-    const uint64_t ns = c.s_nodes();
+    ReachLabels R;
+    build_reach_labels(s, R);
+    out.pll_ms = R.ms;
+    out.label_entries = R.in.size() + R.out.size();
+    const Lists lists{s, R};
+    const uint64_t ns = s.N, np = s.Nx;
     out.s_nodes = ns;
-    out.S.assign(ns * s_words, 0xFFFFFFFFu);
-    std::atomic<uint64_t> covered{0}, nonempty{0};
-    std::vector<std::vector<uint32_t>> tmp(build_threads());
-    parallel_chunks(ns, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
-        uint64_t cv = 0, ne = 0;
-        for (uint64_t x = b; x < e; x++) {
-            uint32_t *blk = out.S.data() + x * s_words;
-            const bool has = c.nonempty(x);
-            ne += has;
-            if (!c.label(x, tmp[tid])) continue;  // count stays 0xFFFFFFFF: no label
-            cv += has;
-            blk[0] = (uint32_t)tmp[tid].size();
-            std::copy(tmp[tid].begin(), tmp[tid].end(), blk + 1);
-        }
-        covered += cv;
-        nonempty += ne;
-    });
-    out.covered = covered;
-    out.nonempty = nonempty;
-    // P blocks: mode B {r} + fint(r) for every expandable r, mode F rev(t) for every node t
-    const uint64_t np = mode == 0 ? s.Nx : s.N;
-    const uint64_t *off = mode == 0 ? s.fint_off.data() : s.rev_off.data();
-    const uint32_t *col = mode == 0 ? s.fint_col.data() : s.rev_col.data();
-    const uint64_t extra = mode == 0 ? 1 : 0;  // r itself
-    auto plen = [&](uint64_t x) { return off[x + 1] - off[x] + extra; };
-    {  // the smallest block whose inline entries hold >= 95% of the non-empty rows
-        uint64_t fit[3] = {0, 0, 0}, ne = 0;
-        for (uint64_t x = 0; x < np; x++) {
-            const uint64_t n = plen(x);
-            if (!n) continue;
-            ne++;
-            for (int k = 0; k < 3; k++) fit[k] += n <= (16u << k) - 2;
-        }
-        out.pb = 64;
-        for (int k = 0; k < 3; k++)
-            if (fit[k] * 20 >= ne * 19) {
-                out.pb = 16u << k;
-                break;
-            }
-    }
-    const uint32_t pb = out.pb, inl = pb - 2;
     out.p_nodes = np;
-    std::vector<uint64_t> ovf(np, 0);
-    uint64_t acc = 0;
-    for (uint64_t x = 0; x < np; x++) {
-        ovf[x] = acc;
-        const uint64_t n = plen(x);
-        if (n > inl) acc += (n - inl + 15) / 16 * 16;  // 16-word aligned
-    }
-    const uint64_t obase = np * pb;  // a multiple of 16 words
-    if ((obase + acc) / 16 >= (1ull << 32)) throw Error(KETOGPU_EINVAL, "plan label: P rows pass 2^36 words");
-    out.P.assign(obase + acc, 0xFFFFFFFFu);
-    parallel_chunks(np, 1 << 15, [&](int, uint64_t b, uint64_t e) {
+    // pass 1: list lengths
+    std::vector<uint32_t> cs(ns), cp(np);
+    const int T = build_threads();
+    std::vector<std::vector<uint32_t>> tmp(T);
+    parallel_chunks(ns, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
+        uint64_t m;
         for (uint64_t x = b; x < e; x++) {
-            const uint64_t n = plen(x);
-            uint32_t *blk = out.P.data() + x * pb;
-            uint32_t *ov = out.P.data() + obase + ovf[x];
-            blk[0] = (uint32_t)n;
-            blk[1] = n > inl ? (uint32_t)((obase + ovf[x]) / 16) : 0u;
-            for (uint64_t k = 0; k < n; k++) {
-                const uint32_t v = extra && k == 0 ? (uint32_t)x : col[off[x] + k - extra];
-                if (k < inl)
-                    blk[2 + k] = v;
-                else
-                    ov[k - inl] = v;
-            }
+            lists.s_list(x, tmp[tid], m);
+            cs[x] = (uint32_t)tmp[tid].size();
         }
     });
-    out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    parallel_chunks(np, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
+        uint64_t m;
+        for (uint64_t x = b; x < e; x++) {
+            lists.p_list(x, tmp[tid], m);
+            cp[x] = (uint32_t)tmp[tid].size();
+        }
+    });
+    out.hs = hs ? hs : pick_head(cs);
+    out.hp = hp ? hp : pick_head(cp);
+    // overflow lists (whole, 16-word aligned) after the heads
+    auto layout = [](const std::vector<uint32_t> &cnt, uint32_t h, std::vector<uint64_t> &ovf, uint64_t &lists) {
+        ovf.resize(cnt.size());
+        uint64_t acc = (uint64_t)cnt.size() * h;  // a multiple of 8 words
+        acc = (acc + 15) / 16 * 16;
+        lists = 0;
+        for (size_t x = 0; x < cnt.size(); x++) {
+            ovf[x] = 0;
+            if (cnt[x] > h - kHeadFixed) {
+                ovf[x] = acc;
+                acc += ((uint64_t)cnt[x] + 15) / 16 * 16;
+                lists++;
+            }
+        }
+        return acc;
+    };
+    std::vector<uint64_t> os, op;
+    const uint64_t ws = layout(cs, out.hs, os, out.s_overflow), wp = layout(cp, out.hp, op, out.p_overflow);
+    if (ws / 16 >= (1ull << 32) || wp / 16 >= (1ull << 32))
+        throw Error(KETOGPU_EINVAL, "plan label: head arrays pass 2^36 words");
+    if (max_bytes && 4 * (ws + wp) > max_bytes)
+        throw Error(KETOGPU_ENOMEM, "plan label: " + std::to_string(4 * (ws + wp)) + " bytes of labels, budget " +
+                                        std::to_string(max_bytes));
+    out.S.assign(ws, 0xFFFFFFFFu);
+    out.P.assign(wp, 0xFFFFFFFFu);
+    // pass 2: heads and overflow lists
+    auto write = [&](std::vector<uint32_t> &A, uint32_t h, const std::vector<uint64_t> &ovf, uint64_t x,
+                     const std::vector<uint32_t> &l, uint64_t mask, bool nolabel) {
+        uint32_t *hd = A.data() + x * h;
+        hd[0] = nolabel ? kNoLabel : (uint32_t)l.size();
+        hd[1] = (uint32_t)(ovf[x] / 16);
+        hd[2] = (uint32_t)mask;
+        hd[3] = (uint32_t)(mask >> 32);
+        uint32_t *dst = l.size() > h - kHeadFixed ? A.data() + ovf[x] : hd + kHeadFixed;
+        std::copy(l.begin(), l.end(), dst);
+    };
+    std::atomic<uint64_t> es{0}, ep{0}, nl{0};
+    parallel_chunks(ns, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
+        uint64_t m, en = 0, nn = 0;
+        for (uint64_t x = b; x < e; x++) {
+            lists.s_list(x, tmp[tid], m);
+            const bool nolabel = rest_permille && cs[x] && mix64(x * 0x9E3779B97F4A7C15ull + 17) % 1000 < rest_permille;
+            write(out.S, out.hs, os, x, tmp[tid], m, nolabel);
+            en += tmp[tid].size();
+            nn += nolabel;
+        }
+        es += en;
+        nl += nn;
+    });
+    parallel_chunks(np, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {
+        uint64_t m, en = 0;
+        for (uint64_t x = b; x < e; x++) {
+            lists.p_list(x, tmp[tid], m);
+            write(out.P, out.hp, op, x, tmp[tid], m, false);
+            en += tmp[tid].size();
+        }
+        ep += en;
+    });
+    out.s_entries = es;
+    out.p_entries = ep;
+    out.s_nolabel = nl;
+    out.build_ms = ms_since(t0);
 }
 
 }  // namespace ketogpu
@@ -172,18 +388,16 @@ struct ketogpu_label_index {
 
 extern "C" {
 
-int ketogpu_label_index_build(const ketogpu_snapshot *s, const uint32_t closure_cap[2], int mode, uint32_t s_words,
+int ketogpu_label_index_build(const ketogpu_snapshot *s, uint32_t s_head_words, uint32_t p_head_words,
                               ketogpu_label_index **out) {
     try {
-        if (!s || !closure_cap || !out || mode < -1 || mode > 1) throw ketogpu::Error(KETOGPU_EINVAL, "bad argument");
+        if (!s || !out) throw ketogpu::Error(KETOGPU_EINVAL, "null argument");
         *out = nullptr;
         const auto *snap = reinterpret_cast<const ketogpu::Snapshot *>(s);
         std::shared_lock<std::shared_mutex> lk(snap->mu);
-        ketogpu::CoreIndex ci;
-        const uint32_t block[2] = {0, 0};
-        ketogpu::build_core_index(*snap, closure_cap, block, ci);
+        if (snap->writable) throw ketogpu::Error(KETOGPU_EINVAL, "plan label: a writable snapshot");
         auto l = std::make_unique<ketogpu_label_index>();
-        ketogpu::build_labels(*snap, ci, mode, 0.5, l->li, s_words);
+        ketogpu::build_labels(*snap, s_head_words, p_head_words, 0, 0, l->li);
         *out = l.release();
     } catch (const ketogpu::Error &e) {
         ketogpu::set_last_error(e.what());
@@ -201,19 +415,21 @@ int ketogpu_label_index_view(const ketogpu_label_index *l, ketogpu_label_view *o
         return KETOGPU_EINVAL;
     }
     const ketogpu::LabelIndex &li = l->li;
-    out->mode = li.mode;
-    out->s_block_words = li.s_words;
-    out->p_block_words = li.pb;
-    out->p_words = li.P.data();
+    out->s_head_words = li.hs;
+    out->p_head_words = li.hp;
     out->s_words = li.S.data();
-    out->num_p_words = li.P.size();
+    out->p_words = li.P.data();
     out->num_s_words = li.S.size();
-    out->p_nodes = li.p_nodes;
+    out->num_p_words = li.P.size();
     out->s_nodes = li.s_nodes;
-    out->labelled = li.covered;
-    out->nonempty = li.nonempty;
-    out->coverage_b = li.coverage[0];
-    out->coverage_f = li.coverage[1];
+    out->p_nodes = li.p_nodes;
+    out->s_entries = li.s_entries;
+    out->p_entries = li.p_entries;
+    out->s_overflow = li.s_overflow;
+    out->p_overflow = li.p_overflow;
+    out->label_entries = li.label_entries;
+    out->pll_ms = li.pll_ms;
+    out->build_ms = li.build_ms;
     return KETOGPU_OK;
 }
 

@@ -1,52 +1,83 @@
-// labels.hpp — closure labels of plan "label" (device_engine.hip label_unit).
+// labels.hpp — the reachability labels of plan "label" (device_engine.hip label_unit).
 //
 // The reference answers a check by the recursion of internal/check/engine.go:33-91; for a
-// request (r, t) that is R2 reachability: some row path r -> x1 -> ... -> t whose inner
-// nodes are interior (semantic contract).  With the closure rows of plan core
-// (core_index.hpp) that reachability becomes ONE intersection of two short lists per
-// request, in either of two modes:
-//   mode B (backward label):  P(r) = {r} + fint(r),  S(t) = rev(t) + Anc+(g) for every
-//                             interior g in rev(t)       allowed <=> P(r) meets S(t)
-//   mode F (forward label):   P(t) = rev(t),          S(r) = {r} + fint(r) + Desc+(h) for
-//                             every h in fint(r)         allowed <=> P(t) meets S(r)
-// (a path's first interior node x1 is in fint(r) and its last one in rev(t); x1 reaches
-// x(k-1) through interior nodes, so x1 is in Anc+(x(k-1)) and x(k-1) in Desc+(x1); a path
-// of one edge has r in rev(t)).  S is a LABEL: stored sorted per node when every closure it
-// needs exists and it has at most s_words - 1 nodes; a request whose S is missing is
-// answered by plan core's traversal instead (a second stage over those requests).
+// request (r, t) that is R2 reachability (semantic contract): some row path
+// r -> x1 -> ... -> t whose inner nodes are INTERIOR.  Plan label answers it with ONE
+// intersection of two short sorted lists per request, whatever the graph's shape.
 //
-// Storage, per mode, all u32 words:
-//   S blocks, one per S node (s_words = 64 or 128 words, 256 / 512 bytes, aligned): [count,
-//     entries sorted ascending, 0xFFFFFFFF padding]; count = 0xFFFFFFFF: no label
-//   P blocks, one per P node (pb words): [count, overflow start, entries...]; a row of more
-//     than pb - 2 entries keeps the rest at p[overflow start ...] (an overflow region after
-//     the blocks, in the same array)
+// 2-hop labels of the interior graph (pruned landmark labeling): interior nodes are ranked
+// (most central first) and every node v gets Lin(v) = landmarks w with w ->* v and
+// Lout(v) = landmarks w with v ->* w, such that for interior a, b
+//     a ->* b (reflexive)  <=>  Lout(a) and Lin(b) share a landmark.
+// The first kMaskBits landmarks are kept as a bit mask per node instead of list entries
+// (min / mout: bit i = landmark i reaches the node / the node reaches landmark i); the
+// others are processed in rank order, each a forward and a backward search that stops at
+// nodes the labels built so far already answer (landmarks of one parallel batch do not
+// prune each other: more entries, never a wrong answer).
+//
+// Per request, with rev(t) the expandable nodes whose rows hold t and fint(r) r's interior
+// successors:
+//   S(t) = Lin(v) for every interior v in rev(t)  +  the non-interior entries of rev(t)
+//   P(r) = Lout(r)                                  (r interior)
+//        = {r} + Lout(c) for every c in fint(r)     (r expandable, not interior)
+//   allowed(r, t)  <=>  P(r) and S(t) share an entry (or their masks share a bit).
+// Proof: a path's last inner node v is in rev(t) and its first one c in fint(r) (c = v
+// possible), so c ->* v; r interior: r ->* v; a one-edge path has r in rev(t) (r interior:
+// r ->* r; r not interior: the raw entry r).  Conversely a shared landmark w gives
+// r (->c) ->* w ->* v -> t, and a shared raw entry is r in rev(t).  Landmark entries are
+// RANKS (< Ni) and raw entries node ids (>= Ni): the two never collide.
+//
+// Storage (u32 words), one fixed-size HEAD per node (S: every node, P: every expandable
+// node), hs / hp words each (8, 16 or 32: the smallest whose inline entries hold >= 95% of
+// the non-empty lists):
+//   [count | overflow start / 16 | mask lo | mask hi | entries ascending ... | 0xFFFFFFFF pad]
+// a list of more than head - 4 entries is kept whole at words 16 x (overflow start) (after
+// the heads, in the same array); count = kNoLabel: the request goes to the second stage.
 #pragma once
 
 #include <cstdint>
 #include <vector>
 
-#include "core_index.hpp"
+#include "ketogpu_internal.hpp"
 
 namespace ketogpu {
 
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
+constexpr uint32_t kMaskBits = 64;   // landmarks kept as a bit mask
+constexpr uint32_t kHeadFixed = 4;   // count, overflow start, mask (2 words)
 
-struct LabelIndex {
-    int mode = -1;                 // 0 = B, 1 = F; -1: not built
-    uint32_t s_words = 64;         // S block words (64 or 128: labels of up to 63 or 127 nodes)
-    uint32_t pb = 0;               // P block words
-    std::vector<uint32_t> P, S;
-    uint64_t p_nodes = 0, s_nodes = 0;
-    uint64_t covered = 0;          // S nodes with a label (of those with a non-empty row)
-    uint64_t nonempty = 0;
-    double coverage[2] = {0, 0};   // per mode: labelled share of the S nodes with a non-empty row
-    double build_ms = 0;
+// the 2-hop labels of the interior graph
+struct ReachLabels {
+    uint32_t n = 0;                      // interior nodes
+    uint32_t bits = 0;                   // landmarks in the masks (min(n, kMaskBits))
+    std::vector<uint32_t> order;         // rank -> interior node
+    std::vector<uint64_t> min, mout;     // per node
+    std::vector<uint64_t> in_off, out_off;
+    std::vector<uint32_t> in, out;       // ranks >= bits, ascending per node
+    uint64_t batches = 0;                // parallel batches of the pruned searches
+    double ms = 0;
 };
 
-// mode: 0 / 1 forces B / F, -1 builds the mode whose labels cover more S nodes (none when
-// both cover less than min_coverage).  Needs the closure rows of ci (build_core_index).
-void build_labels(const Snapshot &s, const CoreIndex &ci, int mode, double min_coverage, LabelIndex &out,
-                  uint32_t s_words = 64);
+// KETOGPU_LABEL_SEQ: landmarks searched one at a time after the masked ones (default 1024);
+// later ones run in parallel batches of rank / KETOGPU_LABEL_BATCH_DIV (default 8)
+void build_reach_labels(const Snapshot &s, ReachLabels &out);
+
+struct LabelIndex {
+    uint32_t hs = 16, hp = 8;            // head words of S and P
+    std::vector<uint32_t> S, P;          // heads then overflow lists
+    uint64_t s_nodes = 0, p_nodes = 0;
+    uint64_t s_entries = 0, p_entries = 0;    // list entries (masks not counted)
+    uint64_t s_overflow = 0, p_overflow = 0;  // lists kept outside their head
+    uint64_t s_nolabel = 0;                   // heads marked kNoLabel (test knob)
+    uint64_t label_entries = 0;               // Lin + Lout entries
+    double pll_ms = 0, build_ms = 0;
+};
+
+// Builds the labels and both head arrays.  hs / hp = 0: chosen from the list lengths.
+// rest_permille > 0 (test knob): that share of the S heads (by node hash) is marked
+// kNoLabel.  max_bytes: the arrays must fit (KETOGPU_ENOMEM before anything is allocated
+// otherwise).
+void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_permille, uint64_t max_bytes,
+                  LabelIndex &out);
 
 }  // namespace ketogpu

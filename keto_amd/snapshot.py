@@ -205,19 +205,19 @@ class Snapshot:
         finally:
             self.L.ketogpu_core_index_free(h)
 
-    def label_index(self, closure_cap=(64, 64), mode=-1, s_words=64):
-        """plan label's closure labels as the engine builds them (ketogpu_label_index_build):
-        dict with mode (0 B, 1 F, -1 none), p_block_words, P and S word arrays and counts"""
-        cap = (C.c_uint32 * 2)(*closure_cap)
+    def label_index(self, s_head_words=0, p_head_words=0):
+        """plan label's 2-hop labels and head arrays as the engine builds them
+        (ketogpu_label_index_build, labels.hpp): dict with the S and P word arrays, the head
+        sizes and the counts"""
         h = C.c_void_p()
-        L.check(self.L.ketogpu_label_index_build(self.h, cap, mode, s_words, C.byref(h)))
+        L.check(self.L.ketogpu_label_index_build(self.h, s_head_words, p_head_words, C.byref(h)))
         try:
             v = L.LabelView()
             L.check(self.L.ketogpu_label_index_view(h, C.byref(v)))
             arr = lambda p, n: np.ctypeslib.as_array(p, (n,)).copy() if n else np.zeros(0, dtype=np.uint32)
-            return {"mode": v.mode, "s_block_words": v.s_block_words, "p_block_words": v.p_block_words, "P": arr(v.p_words, v.num_p_words),
-                    "S": arr(v.s_words, v.num_s_words), "p_nodes": v.p_nodes, "s_nodes": v.s_nodes,
-                    "labelled": v.labelled, "nonempty": v.nonempty, "coverage": (v.coverage_b, v.coverage_f)}
+            d = {k: getattr(v, k) for k, _ in v._fields_ if k not in ("s_words", "p_words")}
+            d["S"], d["P"] = arr(v.s_words, v.num_s_words), arr(v.p_words, v.num_p_words)
+            return d
         finally:
             self.L.ketogpu_label_index_free(h)
 

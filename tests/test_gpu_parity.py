@@ -48,7 +48,7 @@ def test_nil_subject_is_bad_request():
 
 
 @pytest.fixture(params=["bidi", "bidi-wide", "v2", "lite", "lite-shift", "lite32", "core", "core-small", "core-none",
-                        "label-B", "label-F"])
+                        "label", "label-small", "label-rest"])
 def unit_plan(request, monkeypatch):
     """first LDS pass of engines created while active: the default bidirectional units
     (one-wave, 512-slot tables), bidi with the wide 2048-slot table, forward-only unit2, or
@@ -56,14 +56,19 @@ def unit_plan(request, monkeypatch):
     its 64-bit path (KETOGPU_TEST_BEGIN_SHIFT) — lite with 32-request units, and plan core
     (lite over its own record arrays with closure rows, core_index.hpp) with the default
     caps, with caps of 3 (most closures dropped, mixed closure and one-hop rows) and with
-    no closure rows at all"""
+    no closure rows at all; plan label (2-hop labels) with the chosen heads, with 8-word heads
+    (most lists in the overflow region) and with 40% of the S heads marked unlabelled (the
+    second stage, plan lite over the listed requests)"""
     if request.param == "v2":
         monkeypatch.setenv("KETOGPU_UNITS", "v2")
     elif request.param == "lite32":
         monkeypatch.setenv("KETOGPU_UNITS", "lite32")
-    elif request.param.startswith("label"):  # plan label in each mode (units without labels: plan core)
+    elif request.param.startswith("label"):  # plan label (requests without labels: plan lite)
         monkeypatch.setenv("KETOGPU_UNITS", "label")
-        monkeypatch.setenv("KETOGPU_LABEL_MODE", request.param[-1])
+        if request.param == "label-small":
+            monkeypatch.setenv("KETOGPU_LABEL_HEADS", "8,8")
+        elif request.param == "label-rest":
+            monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", "400")
     elif request.param.startswith("core"):
         monkeypatch.setenv("KETOGPU_UNITS", "core")
         if request.param != "core":
@@ -96,24 +101,29 @@ def test_random_tables_match_oracle(seed, page_size, poison, collide, empty_ns, 
     assert any(want) and not all(want)
 
 
-@pytest.mark.parametrize("words", ["64", "128"])
-def test_wide_labels_match_oracle(words, monkeypatch):
-    """plan label over labels of 33..63 nodes (two S lines in LDS), 64..127 nodes (128-word
-    blocks: searched in the block) and none (second stage), mode B, device and host batches"""
+@pytest.mark.parametrize("heads,permille", [("0,0", 0), ("8,8", 0), ("16,8", 0), ("32,32", 0), ("8,16", 250)])
+def test_label_heads_match_oracle(heads, permille, monkeypatch):
+    """plan label over lists of up to hundreds of entries (the family graph's wide closures):
+    every head size pair (8-word heads: most lists in the overflow region), with a share of
+    the S heads marked unlabelled (the second stage), on device, HBM-resident and pinned
+    host batches"""
     monkeypatch.setenv("KETOGPU_UNITS", "label")
-    monkeypatch.setenv("KETOGPU_LABEL_MODE", "B")
-    monkeypatch.setenv("KETOGPU_LABEL_WORDS", words)
+    monkeypatch.setenv("KETOGPU_LABEL_HEADS", heads)
+    monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", str(permille))
     namespaces, rows, reqs = randgraph.make_family_graph(92)
     snap = Snapshot.from_rows(namespaces, rows, sort=True)
     want = randgraph.oracle_store(namespaces, rows).check_batch(reqs)
     eng = check.Engine(snap)
     assert eng.check_many(tuples_of(reqs)) == [bool(x) for x in want]
     st = eng.last_stats()
-    assert st["plan"] == 7 and st["label_words"] == int(words)
+    assert st["plan"] == 7 and st["label_on"] == 1
+    if heads != "0,0":
+        assert f'{st["label_s_head"]},{st["label_p_head"]}' == heads
     roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(x)) for ns, o, r, x in reqs])
     q = eng.upload(roots, targets)  # HBM-resident
     q.run()
     np.testing.assert_array_equal(q.download(), want)
+    assert (eng.last_stats()["rest_requests"] > 0) == (permille > 0)
     pr, pt = check.pinned(roots), check.pinned(targets)  # pinned host requests read in place
     out = check.PinnedBuffer((len(roots) + 63) // 64, np.uint64)
     eng.check_ids_raw(pr.array.ctypes.data, pt.array.ctypes.data, len(roots), out.array.ctypes.data)
@@ -202,7 +212,11 @@ def test_hub_index_default_on_power_law(monkeypatch):
         eng = check.Engine(snap)
         for _ in range(3 if plan == "auto" else 1):
             np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
-        assert eng.last_stats()["hubs"] > 0
+        st = eng.last_stats()
+        if plan in ("label", "auto"):  # the labels answer without searches: no hub index built
+            assert st["plan"] == 7 and st["label_on"] == 1 and st["hubs"] == 0
+        else:
+            assert st["hubs"] > 0
 
 
 def test_unit_spill_to_global_path():
@@ -351,11 +365,16 @@ def test_loaded_snapshot_answers_identically(tmp_path):
 
 
 @pytest.mark.parametrize("kind", ["rbac", "folders"])
-def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
-    """KETOGPU_UNITS=auto (default): the first two batches of >= 65536 requests run both
-    first stages (bidi and v2) and the engine keeps the faster; every call is exact"""
+@pytest.mark.parametrize("labels", [True, False])
+def test_auto_plan_trials_then_keeps_one(kind, labels, monkeypatch):
+    """KETOGPU_UNITS=auto (default): with plan label's labels built, every call runs plan
+    label (no trials); without them (KETOGPU_NO_LABEL) the first two batches of >= 65536
+    requests run every candidate first stage and the engine keeps the faster; every call is
+    exact"""
     from keto_amd import synth
     monkeypatch.delenv("KETOGPU_UNITS", raising=False)
+    if not labels:
+        monkeypatch.setenv("KETOGPU_NO_LABEL", "1")
     w = {"rbac": lambda: synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=70000, seed=9),
          "folders": lambda: synth.folders(users=8000, groups=300, folders=12000, tuples=150000, checks=70000,
                                           seed=9)}[kind]()
@@ -365,12 +384,13 @@ def test_auto_plan_trials_then_keeps_one(kind, monkeypatch):
         w.requests(range(len(roots))), nthreads=8)
     eng = check.Engine(snap)
     np.testing.assert_array_equal(eng.check_ids(roots[:1000], targets[:1000]), want[:1000])
-    assert eng.last_stats()["plan"] in (6, 7)  # below the trial size: label (or core when labels cover too little)
+    assert eng.last_stats()["plan"] == (7 if labels else 6)  # below the trial size: label, else core
     plans = set()
     for _ in range(4):
         np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
         plans.add(eng.last_stats()["plan"])
-    assert plans <= {0, 1, 2, 5, 6, 7}  # global path (with the hub index), bidi, unit2, lite, core, label
+    # label; else the global path (with the hub index), bidi, unit2, lite, core
+    assert plans == {7} if labels else plans <= {0, 1, 2, 5, 6}
     kept = eng.last_stats()["plan"]
     np.testing.assert_array_equal(eng.check_ids(roots[:5000], targets[:5000]), want[:5000])
     assert eng.last_stats()["plan"] == kept

@@ -253,9 +253,11 @@ def main():
            "peak_rss_gb": round(rss_gb(), 1),
            "plan": check_plan(rs["plan"]), "hubs": rs["hubs"], "hub_build_ms": round(rs["hub_build_ms"], 1),
            "core_build_ms": round(rs["core_build_ms"], 1),
-           "label": ({"mode": "BF"[rs["label_mode"]], "coverage": round(rs["label_coverage"], 4),
-                      "s_block_words": rs["label_words"], "build_ms": round(rs["label_build_ms"], 1)}
-                     if rs["label_mode"] >= 0 else None),
+           "label": ({"s_head_words": rs["label_s_head"], "p_head_words": rs["label_p_head"],
+                      "bytes": rs["label_bytes"], "label_entries": rs["label_entries"],
+                      "coverage": round(rs["label_coverage"], 4), "build_ms": round(rs["label_build_ms"], 1),
+                      "pll_ms": round(rs["label_pll_ms"], 1), "rest_requests": rs["rest_requests"]}
+                     if rs["label_on"] else None),
            "expand": dict(exp, roots=len(expand_roots), engine="host DFS over the ordered snapshot (host_engine.cpp)"),
            "setup_s": {"generate": round(t_gen, 1), "snapshot": round(t_snap, 1), "engine_upload": round(t_up, 1)},
            "snapshot": {k: v for k, v in st.items() if k.startswith("num_")}}
