@@ -468,6 +468,11 @@ int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows);
 /* Test hook: the engine's device rows and edge records compared entry by entry with the
  * snapshot's host rows (after a sync); mismatches = entries that differ. */
 int ketogpu_engine_check_graph(ketogpu_engine *e, uint64_t *mismatches);
+/* Test hook: plan label's S (side 0) or P (side 1) head array as the engine built it on the
+ * device (the layout of ketogpu_label_view); *words = its length in u32 words (0: no
+ * labels), *head_words its head size; copied into out when capacity >= *words. */
+int ketogpu_engine_label_heads(ketogpu_engine *e, int side, uint32_t *out, uint64_t capacity, uint64_t *words,
+                               uint32_t *head_words);
 
 /* ----------------------------------------------- partition-aware loader */
 /* BASELINE config #5 (SURVEY.md 8(e) "Partitioned"): a graph that fits neither one GPU nor

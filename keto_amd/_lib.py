@@ -314,6 +314,8 @@ SIGNATURES = {
     "ketogpu_label_index_build": (C.c_int, [vp, u32, u32, C.POINTER(vp)]),
     "ketogpu_label_index_view": (C.c_int, [vp, C.POINTER(LabelView)]),
     "ketogpu_label_index_free": (None, [vp]),
+    "ketogpu_engine_label_heads": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint32)]),
     "ketogpu_snapshot_save": (C.c_int, [vp, C.c_char_p]),
     "ketogpu_snapshot_apply": (C.c_int, [vp, C.POINTER(RowBatch), C.POINTER(RowBatch), C.POINTER(vp)]),
     "ketogpu_snapshot_load": (C.c_int, [C.c_char_p, C.POINTER(vp)]),

@@ -110,6 +110,18 @@ class Engine:
         self.check_graph_first = self.L.ketogpu_last_error().decode("utf-8", "replace") if bad.value else ""
         return bad.value
 
+    def label_heads(self, side):
+        """test hook (ketogpu_engine_label_heads): plan label's S (side 0) or P (side 1) head
+        array as built on the device -> (uint32 array or None, head words)"""
+        words, hw = C.c_uint64(), C.c_uint32()
+        L.check(self.L.ketogpu_engine_label_heads(self.h, side, None, 0, C.byref(words), C.byref(hw)))
+        if not words.value:
+            return None, 0
+        out = np.empty(words.value, dtype=np.uint32)
+        L.check(self.L.ketogpu_engine_label_heads(self.h, side, out.ctypes.data, words.value, C.byref(words),
+                                                  C.byref(hw)))
+        return out, hw.value
+
     def sync(self):
         """upload the device rows an in-place write patched (ketogpu_engine_sync; every
         check call does it first) -> (host ms, rows uploaded)"""

@@ -2532,11 +2532,12 @@ struct LabelRest {
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
 };
-// A request's S entries in LDS: HS words (the head's HS - 4 inline entries, then 4 pad
-// words) + 1, odd: the 16 lists start in different banks
-template <int HS>
+// A request's lists in LDS: the S head's inline entries (HS - 4, then 4 pad words) and the
+// P head's (HP - 4, then 4 pad words), each + 1 word: odd strides, so the 16 requests' lists
+// start in different banks
+template <int HS, int HP>
 struct LabelShared {
-    uint32_t S[16 * (HS + 1)];
+    uint32_t S[16 * (HS + 1)], P[16 * (HP + 1)];
 };
 
 // x among the W (a power of two) ascending entries of S (padded with 0xFFFFFFFF, which is
@@ -2584,11 +2585,20 @@ template <int W, int J>
 __device__ __forceinline__ uint32_t label_word(const uint32_t (&w)[W], uint32_t lane) {
     return (uint32_t)__shfl((int)w[J % W], (int)((lane & ~3u) + J / W), 64);
 }
+// a head's inline entries (words 4..H-1) to LDS positions 0..H-5, pad words at H-4..H-1
+template <int H>
+__device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[H / 4], uint32_t sub) {
+#pragma unroll
+    for (int k = 0; k < H / 4; k++) {
+        const uint32_t x = (H / 4) * sub + k;
+        L[(x + H - kHeadFixed) % H] = x < kHeadFixed ? 0xFFFFFFFFu : w[k];
+    }
+}
 
 template <int HS, int HP>
-__device__ __forceinline__ void label_unit(LabelShared<HS> &sh, const LabelGraph &L, uint32_t r_lane, uint32_t t_lane,
-                                           uint64_t *allowed, const uint64_t unit, const LabelRest &R,
-                                           unsigned long long *stats) {
+__device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelGraph &L, uint32_t r_lane,
+                                           uint32_t t_lane, uint64_t *allowed, const uint64_t unit,
+                                           const LabelRest &R, unsigned long long *stats) {
     static_assert((HS == 8 || HS == 16 || HS == 32) && (HP == 8 || HP == 16 || HP == 32), "heads of 8, 16 or 32 words");
     constexpr int SW = HS / 4, PW = HP / 4;  // head words per lane
     const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
@@ -2599,7 +2609,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS> &sh, const LabelGraph
 #pragma unroll
     for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
 #pragma unroll
-    for (int k = 0; k < PW; k++) pw[k] = 0u;
+    for (int k = 0; k < PW; k++) pw[k] = 0xFFFFFFFFu;
     if (valid) {  // both heads in flight at once: one dependent HBM read per request
         label_head_load<SW>(L.S + (uint64_t)t * HS, sub, sw);
         label_head_load<PW>(L.P + (uint64_t)r * HP, sub, pw);
@@ -2611,13 +2621,9 @@ __device__ __forceinline__ void label_unit(LabelShared<HS> &sh, const LabelGraph
     // (the overflow starts read here: no cross-lane reads inside the divergent search below)
     const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw, lane) * 16;
     const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw, lane) * 16;
-    // the head's inline entries (words 4..HS-1) to LDS positions 0..HS-5, pad at HS-4..HS-1
-    uint32_t *S = sh.S + q * (HS + 1);
-#pragma unroll
-    for (int k = 0; k < SW; k++) {
-        const uint32_t w = SW * sub + k;
-        S[(w + HS - kHeadFixed) % HS] = w < kHeadFixed ? 0xFFFFFFFFu : sw[k];
-    }
+    uint32_t *Sl = sh.S + q * (HS + 1), *Pl = sh.P + q * (HP + 1);
+    label_to_lds<HS>(Sl, sw, sub);
+    label_to_lds<HP>(Pl, pw, sub);
     // a request without labels (or with a wildcard root): listed for the second stage
     {
         const bool rest = sub == 0 && some && !labelled;
@@ -2629,27 +2635,29 @@ __device__ __forceinline__ void label_unit(LabelShared<HS> &sh, const LabelGraph
     bool hit = labelled && (smask & pmask) != 0;
     uint32_t looked = 0;
     if (labelled && !hit) {
-        const bool s_in = ns <= (uint32_t)(HS - kHeadFixed);
-        auto find = [&](uint32_t x) { return s_in ? label_find<HS>(S, x) : label_find_n(Sg, ns, x); };
-        if (np <= (uint32_t)(HP - kHeadFixed)) {
-#pragma unroll
-            for (int k = 0; k < PW; k++) {
-                const uint32_t w = PW * sub + k;  // word w holds entry w - 4
-                if (w >= kHeadFixed && w - kHeadFixed < np) {
-                    hit |= find(pw[k]);
-                    looked++;
-                }
-            }
-        } else {  // the whole P list in the overflow region
-            for (uint32_t k = sub; k < np && !hit; k += 4) {
-                hit |= find(Pg[k]);
-                looked++;
+        // the shorter list is walked (its entries round-robin over the request's four
+        // lanes), each entry looked up in the longer one by a binary search
+        const bool s_in = ns <= (uint32_t)(HS - kHeadFixed), p_in = np <= (uint32_t)(HP - kHeadFixed);
+        const bool walk_p = np <= ns;
+        if (s_in && p_in) {  // both lists in LDS (the common case: LDS addressing throughout)
+            if (walk_p)
+                for (uint32_t k = sub; k < np && !hit; k += 4, looked++) hit = label_find<HS>(Sl, Pl[k]);
+            else
+                for (uint32_t k = sub; k < ns && !hit; k += 4, looked++) hit = label_find<HP>(Pl, Sl[k]);
+        } else {  // a list in the overflow region
+            const uint32_t nw = walk_p ? np : ns, nl = walk_p ? ns : np;
+            const uint32_t *W = walk_p ? (p_in ? Pl : Pg) : (s_in ? Sl : Sg);
+            for (uint32_t k = sub; k < nw && !hit; k += 4, looked++) {
+                const uint32_t x = W[k];
+                hit = walk_p ? (s_in ? label_find<HS>(Sl, x) : label_find_n(Sg, nl, x))
+                             : (p_in ? label_find<HP>(Pl, x) : label_find_n(Pg, nl, x));
             }
         }
     }
     const uint64_t bits = __ballot(hit);
     uint64_t rows = labelled && sub == 0 ? 2 : 0;
-    uint64_t ent = looked + (labelled && sub == 0 ? ns + kHeadFixed : 0);  // + the two masks (4 words)
+    // entries read: the walked ones, the other list once, and the two masks (4 words)
+    uint64_t ent = looked + (labelled && sub == 0 ? (np <= ns ? ns : np) + kHeadFixed : 0);
 #pragma unroll
     for (int k = 32; k; k >>= 1) {
         rows += __shfl_down(rows, k, 64);
@@ -2674,7 +2682,7 @@ template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t *roots, const uint32_t *targets,
                                                    uint64_t n, uint64_t *allowed, LabelRest R,
                                                    unsigned long long *stats, uint64_t unit0) {
-    __shared__ LabelShared<HS> sh;
+    __shared__ LabelShared<HS, HP> sh;
     if (unit0 == 0) label_clear_next(R);
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
@@ -2689,7 +2697,7 @@ __global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L
                                                         const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
                                                         uint64_t *allowed, LabelRest R, unsigned long long *stats,
                                                         unsigned long long *first_bad) {
-    __shared__ LabelShared<HS> sh;
+    __shared__ LabelShared<HS, HP> sh;
     label_clear_next(R);
     uint32_t r[K], t[K];
     host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
@@ -2742,6 +2750,238 @@ __global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *
         lite_unit<SH, false>(S, g, frec, brec, bidi_load_rows(g, r, t), allowed, u, out, out_count, stats, nullptr,
                              idx, true);
         __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------- plan label: the heads' build
+// The head arrays are built on the device from the 2-hop labels (built once per snapshot on
+// the host, labels.cpp) and the graph already in HBM: one wave per node gathers the node's
+// entries (S: Lin of the interior entries of rev(x) + its other entries; P: Lout(x) for an
+// interior x, else x + Lout of every entry of fint(x)) into LDS, sorts them (bitonic over
+// the 64 lanes) and drops duplicates.  A node with more than 64 entries before deduplication
+// (or a row of more than 64) is left to the host (label_list), which writes its head after.
+// Pass 1 counts (and a histogram picks the head size), a scan places the overflow lists,
+// pass 2 writes.
+struct LabelDevLists {
+    const uint64_t *in_off, *out_off;
+    const uint32_t *in, *out;
+    const uint64_t *min, *mout;
+    uint32_t Ni;
+};
+constexpr uint32_t kLabelBig = 0xFFFFFFFEu;  // count of a node the host builds
+
+// one node's list on the wave: v (one value per lane, ascending, duplicates and padding
+// 0xFFFFFFFF not kept), keep (ballot of the kept lanes), mask; false: more than 64 entries
+template <bool PSIDE>
+__device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLists &D, uint32_t x, uint32_t *buf,
+                                             uint32_t &v, uint64_t &keep, uint64_t &mask) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t b = 0, m;
+    bool synth = false, self_raw = false;
+    if constexpr (!PSIDE) {
+        b = g.rev_off[x];
+        m = g.rev_off[(uint64_t)x + 1] - b;
+    } else if (x < D.Ni) {
+        synth = true;  // the row is x itself: Lout(x)
+        m = 1;
+    } else {
+        b = g.fint_off[x];
+        m = g.fint_off[(uint64_t)x + 1] - b;
+        self_raw = true;  // + the raw entry x
+    }
+    if (m > 64) return false;
+    uint32_t e = KETOGPU_NODE_NONE, c = 0;
+    uint64_t lo = 0, mk = 0;
+    if (lane < m) {
+        e = synth ? x : PSIDE ? g.fint_col[b + lane] : g.rev_col[b + lane];
+        if (e < D.Ni) {
+            const uint64_t *off = PSIDE ? D.out_off : D.in_off;
+            lo = off[e];
+            c = (uint32_t)(off[e + 1] - lo);
+            mk = PSIDE ? D.mout[e] : D.min[e];
+        } else {
+            c = 1;
+        }
+    }
+    const uint32_t incl = wave_incl_sum_u32(c);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63) + (self_raw ? 1u : 0u);
+    if (total > 64) return false;
+    wave_sync();  // (the previous node's reads of buf are done)
+    if (lane < m) {
+        uint32_t o = incl - c;
+        if (e < D.Ni) {
+            const uint32_t *lst = (PSIDE ? D.out : D.in) + lo;
+            for (uint32_t k = 0; k < c; k++) buf[o + k] = lst[k];
+        } else {
+            buf[o] = e;
+        }
+    }
+    if (self_raw && lane == 0) buf[total - 1] = x;
+    wave_sync();
+    v = lane < total ? buf[lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 32; k; k >>= 1) mk |= __shfl_xor(mk, k, 64);
+    mask = mk;
+    // bitonic sort, ascending over the 64 lanes
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j; j >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v, (int)j, 64);
+            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
+            v = take_min ? min(v, o) : max(v, o);
+        }
+    const uint32_t prev = (uint32_t)__shfl((int)v, (int)((lane + 63) & 63), 64);
+    keep = __ballot(v != 0xFFFFFFFFu && (lane == 0 || v != prev));
+    return true;
+}
+
+// pass 1: counts (kLabelBig for the host's nodes, listed in big), and per block the
+// histogram hist = {non-empty, <= 4, <= 12, <= 28 entries}
+template <bool PSIDE>
+__global__ __launch_bounds__(256) void label_count_kernel(DevGraph g, LabelDevLists D, uint32_t n, uint32_t *cnt,
+                                                          unsigned long long *hist, uint32_t *big,
+                                                          unsigned int *big_n, uint32_t big_cap) {
+    __shared__ uint32_t buf[4][64];
+    __shared__ unsigned long long h[4];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < 4) h[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long hw[4] = {0, 0, 0, 0};
+    for (uint32_t x = blockIdx.x * 4 + wave; x < n; x += gridDim.x * 4) {
+        uint32_t v;
+        uint64_t keep, mask;
+        if (!label_gather<PSIDE>(g, D, x, buf[wave], v, keep, mask)) {
+            if (lane == 0) {
+                cnt[x] = kLabelBig;
+                const uint32_t at = atomicAdd(big_n, 1u);
+                if (at < big_cap) big[at] = x;
+            }
+            continue;
+        }
+        const uint32_t c = (uint32_t)__popcll(keep);
+        if (lane == 0) {
+            cnt[x] = c;
+            hw[0] += c != 0;
+            hw[1] += c != 0 && c <= 4;
+            hw[2] += c != 0 && c <= 12;
+            hw[3] += c != 0 && c <= 28;
+        }
+    }
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) atomicAdd(&h[k], hw[k]);
+    __syncthreads();
+    if (threadIdx.x < 4) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// overflow lists, in 16-word units: a list of more than cap entries takes ceil(count / 16)
+__device__ __forceinline__ uint32_t label_ov16(uint32_t c, uint32_t cap) { return c > cap ? (c + 15) / 16 : 0u; }
+constexpr uint32_t kLabelScanPer = 16, kLabelScanBlock = 256;  // nodes per thread, threads per block
+// the scan's pass 1: each block's total of overflow units (its 4096 nodes)
+__global__ __launch_bounds__(256) void label_ov_sum_kernel(const uint32_t *cnt, uint32_t n, uint32_t cap,
+                                                           unsigned long long *block_sum) {
+    __shared__ unsigned long long part[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kLabelScanPer * kLabelScanBlock + threadIdx.x * kLabelScanPer;
+    unsigned long long t = 0;
+    for (uint32_t k = 0; k < kLabelScanPer; k++)
+        if (b0 + k < n) t += label_ov16(cnt[b0 + k], cap);
+#pragma unroll
+    for (int k = 32; k; k >>= 1) t += __shfl_xor(t, k, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) block_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+// pass 2: every node's overflow start (16-word units from base16) = the block's offset +
+// the exclusive prefix within the block
+__global__ __launch_bounds__(256) void label_ov_off_kernel(const uint32_t *cnt, uint32_t n, uint32_t cap,
+                                                           const unsigned long long *block_off, uint64_t base16,
+                                                           uint32_t *off16) {
+    __shared__ unsigned long long part[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t b0 = (uint64_t)blockIdx.x * kLabelScanPer * kLabelScanBlock + threadIdx.x * kLabelScanPer;
+    unsigned long long t = 0;
+    for (uint32_t k = 0; k < kLabelScanPer; k++)
+        if (b0 + k < n) t += label_ov16(cnt[b0 + k], cap);
+    unsigned long long incl = t;  // inclusive scan over the wave
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const unsigned long long o = __shfl_up(incl, k, 64);
+        if ((int)lane >= k) incl += o;
+    }
+    if (lane == 63) part[wave] = incl;
+    __syncthreads();
+    unsigned long long acc = base16 + block_off[blockIdx.x] + incl - t;
+    for (uint32_t w = 0; w < wave; w++) acc += part[w];
+    for (uint32_t k = 0; k < kLabelScanPer; k++)
+        if (b0 + k < n) {
+            const uint32_t c = cnt[b0 + k];
+            off16[b0 + k] = label_ov16(c, cap) ? (uint32_t)acc : 0u;
+            acc += label_ov16(c, cap);
+        }
+}
+
+// pass 2: heads (and overflow lists) of every node the device counted; A is pre-filled
+// with 0xFFFFFFFF
+template <bool PSIDE>
+__global__ __launch_bounds__(256) void label_write_kernel(DevGraph g, LabelDevLists D, uint32_t n, const uint32_t *cnt,
+                                                          const uint32_t *off16, uint32_t *A, uint32_t H,
+                                                          uint32_t permille, unsigned long long *tally) {
+    __shared__ uint32_t buf[4][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned long long ent = 0, nol = 0, ovf = 0;  // (lane 0) entries, heads marked kNoLabel, overflow lists
+    for (uint32_t x = blockIdx.x * 4 + wave; x < n; x += gridDim.x * 4) {
+        uint32_t v;
+        uint64_t keep, mask;
+        if (!label_gather<PSIDE>(g, D, x, buf[wave], v, keep, mask)) continue;  // the host's node (wave-uniform)
+        const uint32_t c = (uint32_t)__popcll(keep);
+        uint32_t *head = A + (uint64_t)x * H;
+        const bool inl = c <= H - kHeadFixed;
+        uint32_t *dst = inl ? head + kHeadFixed : A + (uint64_t)off16[x] * 16;
+        if ((keep >> lane) & 1) dst[lanes_below(keep)] = v;
+        if (lane == 0) {
+            // (the test knob's hash: labels.cpp label_nolabel)
+            uint64_t hx = (uint64_t)x * 0x9E3779B97F4A7C15ull + 17;
+            hx ^= hx >> 30, hx *= 0xbf58476d1ce4e5b9ull, hx ^= hx >> 27, hx *= 0x94d049bb133111ebull, hx ^= hx >> 31;
+            const bool nolabel = !PSIDE && permille && c && hx % 1000 < permille;
+            head[0] = nolabel ? kNoLabel : c;
+            head[1] = inl ? 0u : off16[x];
+            head[2] = (uint32_t)mask;
+            head[3] = (uint32_t)(mask >> 32);
+            ent += c;
+            nol += nolabel;
+            ovf += !inl;
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&tally[0], ent);
+        atomicAdd(&tally[1], nol);
+        atomicAdd(&tally[2], ovf);
+    }
+}
+
+// big[i]'s overflow start and (in) count to the host; (out) counts of the host's nodes in
+__global__ void label_big_io_kernel(const uint32_t *big, uint32_t nbig, uint32_t *cnt, const uint32_t *counts_in,
+                                    const uint32_t *off16, uint32_t *off_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nbig) return;
+    if (counts_in) cnt[big[i]] = counts_in[i];
+    if (off16) off_out[i] = off16[big[i]];
+}
+
+// the host's nodes: packed records {node, count, H head words, the list when it overflows}
+// (rec_off[i] = the i-th record's first word): heads to A + node * H, lists to the
+// overflow start in the head's word 1
+__global__ __launch_bounds__(64) void label_patch_kernel(const uint32_t *rec, const uint64_t *rec_off, uint32_t nrec,
+                                                         uint32_t *A, uint32_t H) {
+    for (uint32_t i = blockIdx.x; i < nrec; i += gridDim.x) {
+        const uint32_t *r = rec + rec_off[i];
+        const uint32_t x = r[0], c = r[1];
+        uint32_t *head = A + (uint64_t)x * H;
+        for (uint32_t k = threadIdx.x; k < H; k += 64) head[k] = r[2 + k];
+        if (c > H - kHeadFixed) {
+            uint32_t *dst = A + (uint64_t)r[3] * 16;
+            for (uint32_t k = threadIdx.x; k < c; k += 64) dst[k] = r[2 + H + k];
+        }
     }
 }
 
@@ -3744,6 +3984,7 @@ struct ketogpu_engine {
     uint32_t label_hs = 16, label_hp = 8;  // head words of S and P
     double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
     uint64_t label_bytes = 0, label_entries = 0;
+    uint64_t label_nwords[2] = {0, 0};  // words of the S and P arrays (heads + overflow)
     // a head-size pair (HS, HP) as template arguments
     template <class F>
     void label_dispatch(F &&f) {
@@ -4374,12 +4615,15 @@ struct ketogpu_engine {
                          candidates.end());
         if (bidi_cfg.lite == 2) bidi_cfg.lite = 1;
     }
-    // plan label's 2-hop labels and heads (labels.hpp), built on the host and uploaded; the
-    // arrays must fit half of the HBM left after the graph (and its edge records) and the
-    // host's memory (the size is known before anything is allocated).  On success the plan
-    // is label without trials, plan core and the hub index are skipped; on failure the
-    // engine goes on as if labels had not been asked for.
+    // plan label's 2-hop labels (labels.hpp, built once per snapshot on the host and shared
+    // by its engines) and the head arrays, built on the device from them and the graph in
+    // HBM (label_count_kernel / label_write_kernel; KETOGPU_LABEL_HOST=1: the host build,
+    // uploaded).  The arrays must fit half of the HBM left after the graph and its edge
+    // records (checked before they are allocated).  On success the plan is label without
+    // trials, and plan core and the hub index are skipped; on failure the engine goes on as
+    // if labels had not been asked for.
     void build_label(const Snapshot &s) {
+        const auto t0 = std::chrono::steady_clock::now();
         size_t free_b = 0, total_b = 0;
         HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
         const uint64_t records = 16ull * (s.fint_col.size() + s.rev_col.size());
@@ -4387,46 +4631,251 @@ struct ketogpu_engine {
         uint32_t hs = 0, hp = 0, permille = 0;
         if (const char *e = getenv("KETOGPU_LABEL_HEADS")) sscanf(e, "%u,%u", &hs, &hp);
         if (const char *e = getenv("KETOGPU_LABEL_REST_PERMILLE")) permille = (uint32_t)std::min(1000, std::max(0, atoi(e)));
-        LabelIndex li;
+        for (uint32_t h : {hs, hp})
+            if (h && h != 8 && h != 16 && h != 32) {
+                fprintf(stderr, "[ketogpu] plan label disabled: KETOGPU_LABEL_HEADS takes 8, 16 or 32 words\n");
+                drop_label();
+                return;
+            }
+        std::vector<void *> tmp;  // device temporaries of the build
+        auto free_tmp = [&] {
+            for (void *p : tmp) (void)hipFree(p);
+            tmp.clear();
+        };
+        uint32_t *A[2] = {nullptr, nullptr};  // S, P
+        uint32_t H[2] = {hs, hp};
+        uint64_t nolabel = 0, s_entries = 0, nonempty_s = 0;
         try {
-            build_labels(s, hs, hp, permille, budget, li);
+            if (getenv("KETOGPU_LABEL_HOST")) {  // the host build (A/B, and the test hook's path)
+                LabelIndex li;
+                build_labels(s, hs, hp, permille, budget, li);
+                A[0] = dupload(li.S);
+                owned.push_back(A[0]);
+                A[1] = dupload(li.P);
+                owned.push_back(A[1]);
+                H[0] = li.hs, H[1] = li.hp;
+                label_nwords[0] = li.S.size();
+                label_nwords[1] = li.P.size();
+                label_bytes = 4 * (li.S.size() + li.P.size());
+                label_entries = li.label_entries;
+                label_pll_ms = li.pll_ms;
+                nolabel = li.s_nolabel;
+                s_entries = li.s_entries;
+            } else {
+                const std::shared_ptr<const ReachLabels> R = reach_labels_of(s);
+                label_pll_ms = R->ms;
+                label_entries = R->in.size() + R->out.size();
+                auto up = [&](const auto &v) {
+                    using T = typename std::decay_t<decltype(v)>::value_type;
+                    T *p = dalloc<T>(std::max<size_t>(v.size(), 1));
+                    tmp.push_back(p);
+                    if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+                    return p;
+                };
+                LabelDevLists D{up(R->in_off), up(R->out_off), up(R->in), up(R->out), up(R->min), up(R->mout), s.Ni};
+                unsigned long long *ctr = dalloc<unsigned long long>(8);
+                tmp.push_back(ctr);
+                uint64_t used = 0;
+                label_bytes = 0;
+                for (int side = 0; side < 2; side++) {
+                    const uint32_t n = side == 0 ? s.N : s.Nx;
+                    uint32_t *cnt = dalloc<uint32_t>(std::max<uint32_t>(n, 1)), *off16 = dalloc<uint32_t>(std::max<uint32_t>(n, 1));
+                    tmp.push_back(cnt);
+                    tmp.push_back(off16);
+                    const uint32_t big_cap = std::max<uint32_t>(4096, n / 32);
+                    uint32_t *big = dalloc<uint32_t>(big_cap);
+                    tmp.push_back(big);
+                    HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
+                    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + 3) / 4, 1), 16384);
+                    if (n) {
+                        if (side == 0)
+                            KLAUNCH(label_count_kernel<false>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
+                                    (unsigned int *)(ctr + 4), big_cap);
+                        else
+                            KLAUNCH(label_count_kernel<true>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
+                                    (unsigned int *)(ctr + 4), big_cap);
+                    }
+                    unsigned long long hist[5];
+                    HIP_CHECK(hipMemcpyAsync(hist, ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+                    HIP_CHECK(hipStreamSynchronize(stream));
+                    const uint32_t nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
+                    if (nbig > big_cap) throw Error(KETOGPU_ENOMEM, "plan label: too many lists of more than 64 entries");
+                    // the host's nodes: their lists (label_list), their counts into cnt
+                    std::vector<uint32_t> hbig(nbig), hcnt(nbig);
+                    std::vector<std::vector<uint32_t>> blist(nbig);
+                    std::vector<uint64_t> bmask(nbig);
+                    if (nbig) {
+                        HIP_CHECK(hipMemcpy(hbig.data(), big, nbig * 4, hipMemcpyDeviceToHost));
+                        parallel_chunks(nbig, 64, [&](int, uint64_t b, uint64_t e) {
+                            for (uint64_t k = b; k < e; k++) {
+                                label_list(s, *R, side == 1, hbig[k], blist[k], bmask[k]);
+                                hcnt[k] = (uint32_t)blist[k].size();
+                            }
+                        });
+                        uint32_t *dc = dalloc<uint32_t>(nbig);
+                        tmp.push_back(dc);
+                        HIP_CHECK(hipMemcpy(dc, hcnt.data(), nbig * 4, hipMemcpyHostToDevice));
+                        KLAUNCH(label_big_io_kernel, dim3((nbig + 255) / 256), dim3(256), 0, stream, big, nbig, cnt, dc,
+                                nullptr, nullptr);
+                    }
+                    uint64_t ne = hist[0], fit[3] = {hist[1], hist[2], hist[3]};
+                    for (uint32_t c : hcnt) {  // (as the host build counts them)
+                        ne += c != 0;
+                        for (int k = 0; k < 3; k++) fit[k] += c != 0 && c <= (8u << k) - kHeadFixed;
+                    }
+                    if (!H[side]) H[side] = pick_head(ne, fit);
+                    if (side == 0) nonempty_s = ne;
+                    const uint32_t h = H[side], cap = h - kHeadFixed;
+                    // the overflow lists' starts: block totals, scanned on the host, then per node
+                    const uint64_t per = (uint64_t)kLabelScanPer * kLabelScanBlock;
+                    const uint32_t nb = (uint32_t)std::max<uint64_t>((n + per - 1) / per, 1);
+                    unsigned long long *bs = dalloc<unsigned long long>(nb);
+                    tmp.push_back(bs);
+                    KLAUNCH(label_ov_sum_kernel, dim3(nb), dim3(kLabelScanBlock), 0, stream, cnt, n, cap, bs);
+                    std::vector<unsigned long long> hb(nb);
+                    HIP_CHECK(hipMemcpyAsync(hb.data(), bs, nb * 8, hipMemcpyDeviceToHost, stream));
+                    HIP_CHECK(hipStreamSynchronize(stream));
+                    unsigned long long acc = 0;
+                    for (auto &x : hb) {
+                        const unsigned long long t = x;
+                        x = acc;
+                        acc += t;
+                    }
+                    const uint64_t base16 = ((uint64_t)n * h + 15) / 16, words = (base16 + acc) * 16;
+                    if (base16 + acc >= (1ull << 32)) throw Error(KETOGPU_EINVAL, "plan label: head arrays pass 2^36 words");
+                    used += 4 * words;
+                    if (used > budget)
+                        throw Error(KETOGPU_ENOMEM, "plan label: " + std::to_string(used) + "+ bytes of heads, budget " +
+                                                        std::to_string(budget));
+                    HIP_CHECK(hipMemcpy(bs, hb.data(), nb * 8, hipMemcpyHostToDevice));
+                    KLAUNCH(label_ov_off_kernel, dim3(nb), dim3(kLabelScanBlock), 0, stream, cnt, n, cap, bs, base16,
+                            off16);
+                    uint32_t *arr = dalloc<uint32_t>(words);
+                    owned.push_back(arr);
+                    A[side] = arr;
+                    label_nwords[side] = words;
+                    label_bytes += 4 * words;
+                    HIP_CHECK(hipMemsetAsync(arr, 0xFF, words * 4, stream));
+                    HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
+                    if (n) {
+                        if (side == 0)
+                            KLAUNCH(label_write_kernel<false>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, off16, arr,
+                                    h, permille, ctr);
+                        else
+                            KLAUNCH(label_write_kernel<true>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, off16, arr,
+                                    h, 0u, ctr);
+                    }
+                    if (nbig) {  // the host's nodes: overflow starts down, records up, one patch launch
+                        uint32_t *doff = dalloc<uint32_t>(nbig);
+                        tmp.push_back(doff);
+                        KLAUNCH(label_big_io_kernel, dim3((nbig + 255) / 256), dim3(256), 0, stream, big, nbig, cnt,
+                                nullptr, off16, doff);
+                        std::vector<uint32_t> hoff(nbig);
+                        HIP_CHECK(hipMemcpyAsync(hoff.data(), doff, nbig * 4, hipMemcpyDeviceToHost, stream));
+                        HIP_CHECK(hipStreamSynchronize(stream));
+                        std::vector<uint32_t> rec;
+                        std::vector<uint64_t> roff(nbig);
+                        for (uint32_t k = 0; k < nbig; k++) {
+                            roff[k] = rec.size();
+                            const uint32_t c = hcnt[k];
+                            const bool inl = c <= cap;
+                            const bool nl = side == 0 && c && label_nolabel(hbig[k], permille);
+                            rec.push_back(hbig[k]);
+                            rec.push_back(c);
+                            const size_t hd = rec.size();
+                            rec.resize(hd + h, 0xFFFFFFFFu);
+                            rec[hd] = nl ? kNoLabel : c;
+                            rec[hd + 1] = inl ? 0u : hoff[k];
+                            rec[hd + 2] = (uint32_t)bmask[k];
+                            rec[hd + 3] = (uint32_t)(bmask[k] >> 32);
+                            if (inl)
+                                std::copy(blist[k].begin(), blist[k].end(), rec.begin() + (ptrdiff_t)(hd + kHeadFixed));
+                            else
+                                rec.insert(rec.end(), blist[k].begin(), blist[k].end());
+                            nolabel += nl;
+                            if (side == 0) s_entries += c;
+                        }
+                        uint32_t *drec = dalloc<uint32_t>(rec.size());
+                        uint64_t *droff = dalloc<uint64_t>(nbig);
+                        tmp.push_back(drec);
+                        tmp.push_back(droff);
+                        HIP_CHECK(hipMemcpy(drec, rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
+                        HIP_CHECK(hipMemcpy(droff, roff.data(), nbig * 8, hipMemcpyHostToDevice));
+                        KLAUNCH(label_patch_kernel, dim3(std::min<uint32_t>(nbig, 4096)), dim3(64), 0, stream, drec, droff,
+                                nbig, arr, h);
+                    }
+                    unsigned long long tally[3];
+                    HIP_CHECK(hipMemcpyAsync(tally, ctr, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+                    HIP_CHECK(hipStreamSynchronize(stream));
+                    if (side == 0) {
+                        s_entries += tally[0];
+                        nolabel += tally[1];
+                    }
+                    if (cascade_log)
+                        fprintf(stderr, "[label] %s heads: %u nodes, %u words each, %llu lists in overflow, %u long lists "
+                                        "built on the host, %.2f GB\n",
+                                side == 0 ? "S" : "P", n, h, (unsigned long long)tally[2] + (unsigned long long)nbig,
+                                nbig, 4.0 * (double)words / 1e9);
+                    free_tmp_side(tmp, {cnt, off16, big});
+                }
+                free_tmp();
+            }
         } catch (const Error &e) {
             fprintf(stderr, "[ketogpu] plan label disabled: %s\n", e.what());
+            free_tmp();
+            release_label(A);
             drop_label();
             return;
         } catch (const std::bad_alloc &) {
             fprintf(stderr, "[ketogpu] plan label disabled: out of host memory\n");
+            free_tmp();
+            release_label(A);
             drop_label();
             return;
         }
-        uint32_t *P = dupload(li.P), *S = dupload(li.S);
-        owned.push_back(P);
-        owned.push_back(S);
         rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
         owned.push_back(rest_counts);
         HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
-        lgraph = LabelGraph{P, S};
-        label_hs = li.hs;
-        label_hp = li.hp;
-        label_bytes = 4 * (li.P.size() + li.S.size());
-        label_entries = li.label_entries;
-        label_pll_ms = li.pll_ms;
-        uint64_t nonempty = 0;
-        for (uint64_t x = 0; x < s.N; x++) nonempty += s.rev_off[x + 1] > s.rev_off[x];
-        label_coverage = nonempty ? 1.0 - (double)li.s_nolabel / (double)nonempty : 1.0;
+        lgraph = LabelGraph{A[1], A[0]};
+        label_hs = H[0];
+        label_hp = H[1];
+        label_coverage = nonempty_s ? 1.0 - (double)nolabel / (double)nonempty_s : 1.0;
+        if (getenv("KETOGPU_LABEL_HOST")) {
+            uint64_t ne = 0;
+            for (uint64_t x = 0; x < s.N; x++) ne += s.rev_off[x + 1] > s.rev_off[x];
+            label_coverage = ne ? 1.0 - (double)nolabel / (double)ne : 1.0;
+        }
         // the plan, without trials; neither plan core nor the hubs are built
         use_core = false;
         use_bidi = true;
         bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 3};
         trials_left = 0;
         candidates.clear();
-        label_build_ms = li.build_ms;
+        label_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (cascade_log)
-            fprintf(stderr, "[label] %u landmarks, %llu label entries (%.1f ms); S heads %u words (%llu entries, %llu "
-                            "lists in overflow), P heads %u words (%llu, %llu); %.2f GB; built in %.1f ms\n",
-                    s.Ni, (unsigned long long)li.label_entries, li.pll_ms, li.hs, (unsigned long long)li.s_entries,
-                    (unsigned long long)li.s_overflow, li.hp, (unsigned long long)li.p_entries,
-                    (unsigned long long)li.p_overflow, (double)label_bytes / 1e9, li.build_ms);
+            fprintf(stderr, "[label] %u landmarks, %llu label entries (%.1f ms); S heads %u words (%llu entries), P heads "
+                            "%u words; %.2f GB; built in %.1f ms\n",
+                    s.Ni, (unsigned long long)label_entries, label_pll_ms, label_hs, (unsigned long long)s_entries,
+                    label_hp, (double)label_bytes / 1e9, label_build_ms);
+    }
+    // a build's temporaries freed early (the side's counts and offsets)
+    static void free_tmp_side(std::vector<void *> &tmp, std::initializer_list<void *> ps) {
+        for (void *p : ps) {
+            auto it = std::find(tmp.begin(), tmp.end(), p);
+            if (it != tmp.end()) {
+                (void)hipFree(p);
+                tmp.erase(it);
+            }
+        }
+    }
+    // a failed build's head arrays
+    void release_label(uint32_t *(&A)[2]) {
+        for (uint32_t *&p : A)
+            if (p) {
+                owned.erase(std::remove(owned.begin(), owned.end(), (void *)p), owned.end());
+                (void)hipFree(p);
+                p = nullptr;
+            }
     }
 
     // Hub index.  Hubs are the interior nodes with the most interior successors; a search
@@ -5532,6 +5981,20 @@ int ketogpu_engine_sync(ketogpu_engine *e, double *ms, uint64_t *rows) {
     const uint64_t n = e->sync();
     if (rows) *rows = n;
     if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    API_END
+}
+
+int ketogpu_engine_label_heads(ketogpu_engine *e, int side, uint32_t *out, uint64_t capacity, uint64_t *words,
+                               uint32_t *head_words) {
+    API_BEGIN
+    if (!e || !words || !head_words || side < 0 || side > 1) throw Error(KETOGPU_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    *words = e->use_label ? e->label_nwords[side] : 0;
+    *head_words = e->use_label ? (side == 0 ? e->label_hs : e->label_hp) : 0;
+    if (out && *words && capacity >= *words) {
+        HIP_CHECK(hipSetDevice(e->device));
+        HIP_CHECK(hipMemcpy(out, side == 0 ? e->lgraph.S : e->lgraph.P, *words * 4, hipMemcpyDeviceToHost));
+    }
     API_END
 }
 

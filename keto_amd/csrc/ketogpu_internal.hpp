@@ -136,6 +136,8 @@ struct RowRef {
     int64_t first_bad = -1;  // index of first bad row in query order, -1 if none
 };
 
+struct ReachLabels;  // labels.hpp
+
 struct Snapshot {
     // ---- configuration
     std::vector<Namespace> namespaces;  // config order, unique names and ids
@@ -219,6 +221,10 @@ struct Snapshot {
         }
     }
     mutable std::shared_mutex mu;       // writes exclusive; engine, resolve and expand calls shared
+    // derived indexes built once per snapshot and shared by its engines (labels.cpp
+    // reach_labels_of); immutable snapshots only
+    mutable std::mutex derived_mu;
+    mutable std::shared_ptr<const ReachLabels> reach_cache;
     // An engine's way back to its snapshot at teardown: the snapshot's destructor clears it,
     // so an engine freed after its snapshot (a garbage collector's order) skips the
     // deregistration instead of touching freed memory.

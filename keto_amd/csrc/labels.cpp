@@ -45,10 +45,41 @@ void make_adj(const Snapshot &s, IAdj &a) {
     });
 }
 
-// M[v] bit i = landmark order[i] reaches v along direction d (reflexive): a frontier
-// propagation of 64-bit masks, level by level, on every build thread
-void reach_masks(const IAdj &a, const std::vector<uint32_t> &order, uint32_t bits, int d, std::vector<uint64_t> &M) {
+// a topological order of the interior graph (forward edges), or false when it has a cycle
+bool topo_order(const IAdj &a, std::vector<uint32_t> &topo) {
+    const uint32_t n = (uint32_t)a.deg[0].size();
+    std::vector<uint32_t> indeg(a.deg[1].begin(), a.deg[1].end());
+    topo.clear();
+    topo.reserve(n);
+    for (uint32_t v = 0; v < n; v++)
+        if (!indeg[v]) topo.push_back(v);
+    for (size_t h = 0; h < topo.size(); h++) {
+        const uint32_t y = topo[h];
+        const uint32_t *c = a.col[0] + a.beg[0][y];
+        for (uint32_t j = 0; j < a.deg[0][y]; j++)
+            if (--indeg[c[j]] == 0) topo.push_back(c[j]);
+    }
+    return topo.size() == n;
+}
+
+// M[v] bit i = landmark order[i] reaches v along direction d (reflexive).  An acyclic
+// interior graph (topo non-empty): one pass in topological order (reverse order backward);
+// else a frontier propagation of 64-bit masks, level by level, on every build thread
+void reach_masks(const IAdj &a, const std::vector<uint32_t> &order, const std::vector<uint32_t> &topo, uint32_t bits,
+                 int d, std::vector<uint64_t> &M) {
     const uint32_t n = (uint32_t)order.size();
+    if (!topo.empty()) {
+        M.assign(n, 0);
+        for (uint32_t i = 0; i < bits; i++) M[order[i]] |= 1ull << i;
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t y = topo[d == 0 ? k : n - 1 - k];
+            const uint64_t m = M[y];
+            if (!m) continue;
+            const uint32_t *c = a.col[d] + a.beg[d][y];
+            for (uint32_t j = 0; j < a.deg[d][y]; j++) M[c[j]] |= m;
+        }
+        return;
+    }
     std::vector<std::atomic<uint64_t>> A(n), P(n);
     std::vector<std::atomic<uint8_t>> inq(n);
     parallel_chunks(n, 1 << 16, [&](int, uint64_t b, uint64_t e) {
@@ -100,7 +131,8 @@ void reach_masks(const IAdj &a, const std::vector<uint32_t> &order, uint32_t bit
 // stamp 2r + 1 + d, never 0), the queue, and the entries found in a parallel batch
 struct Searcher {
     std::vector<uint32_t> vis, mark, q;
-    std::vector<std::pair<uint32_t, uint32_t>> add[2];  // (node, rank)
+    // (node, rank) per direction, bucketed by node % threads (the merge thread of the node)
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> add[2];
 };
 
 }  // namespace
@@ -116,16 +148,27 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
     // rank: most central first ((interior out-degree + 1) x (interior in-degree + 1))
     out.order.resize(n);
     std::iota(out.order.begin(), out.order.end(), 0u);
-    {
-        std::vector<uint64_t> key(n);
-        for (uint32_t v = 0; v < n; v++) key[v] = (uint64_t)(a.deg[0][v] + 1) * (a.deg[1][v] + 1);
-        std::sort(out.order.begin(), out.order.end(),
-                  [&](uint32_t x, uint32_t y) { return key[x] != key[y] ? key[x] > key[y] : x < y; });
+    {  // (key descending, node ascending) as one u64 per node: ~key << 32 | node
+        std::vector<uint64_t> kv(n);
+        for (uint32_t v = 0; v < n; v++) {
+            const uint64_t key = std::min<uint64_t>((uint64_t)(a.deg[0][v] + 1) * (a.deg[1][v] + 1), 0xFFFFFFFFull);
+            kv[v] = (0xFFFFFFFFull - key) << 32 | v;
+        }
+        std::sort(kv.begin(), kv.end());
+        for (uint32_t k = 0; k < n; k++) out.order[k] = (uint32_t)kv[k];
     }
+    static const bool plog = getenv("KETOGPU_LABEL_LOG") != nullptr;
+    auto phase = [&](const char *what) {
+        if (plog) fprintf(stderr, "[pll] %-12s %8.1f ms\n", what, ms_since(t0));
+    };
+    phase("order");
     const uint32_t bits = std::min<uint32_t>(n, kMaskBits);
     out.bits = bits;
-    reach_masks(a, out.order, bits, 0, out.min);
-    reach_masks(a, out.order, bits, 1, out.mout);
+    std::vector<uint32_t> topo;
+    if (!topo_order(a, topo)) topo.clear();
+    reach_masks(a, out.order, topo, bits, 0, out.min);
+    reach_masks(a, out.order, topo, bits, 1, out.mout);
+    phase("masks");
     // pruned searches of the other landmarks; L[0] = Lin, L[1] = Lout (ranks, unsorted
     // while building: the coverage test marks one side and scans the other)
     std::vector<std::vector<uint32_t>> L[2];
@@ -136,6 +179,8 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
     for (auto &x : sr) {
         x.vis.assign(n, 0);
         x.mark.assign(n, 0);
+        x.add[0].resize(T);
+        x.add[1].resize(T);
     }
     const std::vector<uint64_t> *mask[2] = {&out.min, &out.mout};
     // d = 0: forward from w, entries into Lin (w ->* y); d = 1: backward, into Lout.  The
@@ -162,7 +207,7 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
             if (direct)
                 L[d][y].push_back(r);
             else
-                S.add[d].push_back({y, r});
+                S.add[d][y % (uint32_t)T].push_back({y, r});
             const uint32_t *c = a.col[d] + a.beg[d][y];
             for (uint32_t j = 0; j < a.deg[d][y]; j++) {
                 const uint32_t z = c[j];
@@ -173,7 +218,7 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
             }
         }
     };
-    uint32_t seq = 1024, div = 8;
+    uint32_t seq = 0, div = 8;  // (seq 1024: 2% fewer entries, 1.7x the build time on config #4)
     if (const char *e = getenv("KETOGPU_LABEL_SEQ")) seq = (uint32_t)atoi(e);
     if (const char *e = getenv("KETOGPU_LABEL_BATCH_DIV")) div = std::max(1, atoi(e));
     uint32_t r = bits;
@@ -182,28 +227,36 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
         search(sr[0], r, 0, true);
         search(sr[0], r, 1, true);
     }
+    phase("sequential");
+    double t_search = 0, t_merge = 0;
     while (r < n) {
         const uint32_t bs = std::max<uint32_t>((uint32_t)T * 4, r / div);
         const uint32_t e = (uint32_t)std::min<uint64_t>(n, (uint64_t)r + bs);
+        const auto tb = Clock::now();
         parallel_chunks(e - r, 8, [&](int tid, uint64_t b, uint64_t f) {
             for (uint64_t k = b; k < f; k++) {
                 search(sr[tid], r + (uint32_t)k, 0, false);
                 search(sr[tid], r + (uint32_t)k, 1, false);
             }
         });
-        // merge: thread t appends the entries of nodes y with y % T == t
+        t_search += ms_since(tb);
+        const auto tm = Clock::now();
+        // merge: thread t appends the entries of nodes y with y % T == t (its buckets)
         parallel_chunks((uint64_t)T, 1, [&](int, uint64_t b, uint64_t f) {
             for (uint64_t t = b; t < f; t++)
                 for (int d = 0; d < 2; d++)
-                    for (auto &x : sr)
-                        for (auto &p : x.add[d])
-                            if (p.first % (uint32_t)T == t) L[d][p.first].push_back(p.second);
+                    for (auto &x : sr) {
+                        for (auto &p : x.add[d][t]) L[d][p.first].push_back(p.second);
+                        x.add[d][t].clear();
+                    }
         });
-        for (auto &x : sr)
-            for (int d = 0; d < 2; d++) x.add[d].clear();
+        t_merge += ms_since(tm);
         out.batches++;
         r = e;
     }
+    if (plog) fprintf(stderr, "[pll] batches: %llu, searches %.1f ms, merges %.1f ms\n",
+                      (unsigned long long)out.batches, t_search, t_merge);
+    phase("batched");
     for (auto &x : sr) std::vector<uint32_t>().swap(x.vis), std::vector<uint32_t>().swap(x.mark);
     // sorted CSR
     for (int d = 0; d < 2; d++) {
@@ -221,7 +274,18 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
             }
         });
     }
+    phase("csr");
     out.ms = ms_since(t0);
+}
+
+std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s) {
+    std::lock_guard<std::mutex> lk(s.derived_mu);
+    if (!s.reach_cache) {
+        auto R = std::make_shared<ReachLabels>();
+        build_reach_labels(s, *R);
+        s.reach_cache = std::move(R);
+    }
+    return s.reach_cache;
 }
 
 namespace {
@@ -266,20 +330,36 @@ struct Lists {
     }
 };
 
-// the smallest head (8, 16 or 32 words) whose inline entries hold >= 95% of the non-empty lists
-uint32_t pick_head(const std::vector<uint32_t> &cnt) {
+uint32_t pick_head_of(const std::vector<uint32_t> &cnt) {
     uint64_t ne = 0, fit[3] = {0, 0, 0};
     for (uint32_t c : cnt) {
         if (!c) continue;
         ne++;
         for (int k = 0; k < 3; k++) fit[k] += c <= (8u << k) - kHeadFixed;
     }
-    for (int k = 0; k < 3; k++)
-        if (fit[k] * 20 >= ne * 19) return 8u << k;
-    return 32;
+    return ketogpu::pick_head(ne, fit);
 }
 
 }  // namespace
+
+uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]) {
+    for (int k = 0; k < 3; k++)
+        if (fit[k] * 20 >= nonempty * 19) return 8u << k;
+    return 32;
+}
+
+bool label_nolabel(uint64_t x, uint32_t permille) {
+    return permille && mix64(x * 0x9E3779B97F4A7C15ull + 17) % 1000 < permille;
+}
+
+void label_list(const Snapshot &s, const ReachLabels &R, bool p_side, uint64_t x, std::vector<uint32_t> &out,
+                uint64_t &mask) {
+    const Lists l{s, R};
+    if (p_side)
+        l.p_list(x, out, mask);
+    else
+        l.s_list(x, out, mask);
+}
 
 void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_permille, uint64_t max_bytes,
                   LabelIndex &out) {
@@ -313,8 +393,8 @@ void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_per
             cp[x] = (uint32_t)tmp[tid].size();
         }
     });
-    out.hs = hs ? hs : pick_head(cs);
-    out.hp = hp ? hp : pick_head(cp);
+    out.hs = hs ? hs : pick_head_of(cs);
+    out.hp = hp ? hp : pick_head_of(cp);
     // overflow lists (whole, 16-word aligned) after the heads
     auto layout = [](const std::vector<uint32_t> &cnt, uint32_t h, std::vector<uint64_t> &ovf, uint64_t &lists) {
         ovf.resize(cnt.size());
@@ -356,7 +436,7 @@ void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_per
         uint64_t m, en = 0, nn = 0;
         for (uint64_t x = b; x < e; x++) {
             lists.s_list(x, tmp[tid], m);
-            const bool nolabel = rest_permille && cs[x] && mix64(x * 0x9E3779B97F4A7C15ull + 17) % 1000 < rest_permille;
+            const bool nolabel = cs[x] && label_nolabel(x, rest_permille);
             write(out.S, out.hs, os, x, tmp[tid], m, nolabel);
             en += tmp[tid].size();
             nn += nolabel;

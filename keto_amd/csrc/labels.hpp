@@ -36,6 +36,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "ketogpu_internal.hpp"
@@ -58,9 +59,22 @@ struct ReachLabels {
     double ms = 0;
 };
 
-// KETOGPU_LABEL_SEQ: landmarks searched one at a time after the masked ones (default 1024);
-// later ones run in parallel batches of rank / KETOGPU_LABEL_BATCH_DIV (default 8)
+// KETOGPU_LABEL_SEQ: landmarks searched one at a time after the masked ones (default 0);
+// the others run in parallel batches of max(4 x threads, rank / KETOGPU_LABEL_BATCH_DIV)
+// (default 8)
 void build_reach_labels(const Snapshot &s, ReachLabels &out);
+// the snapshot's labels, built once and shared by every engine over it (ketogpu_multi_new
+// builds one set for all devices); the snapshot must not be writable
+std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s);
+
+// one node's list and mask as its head holds them (p_side: P(x), else S(x))
+void label_list(const Snapshot &s, const ReachLabels &R, bool p_side, uint64_t x, std::vector<uint32_t> &out,
+                uint64_t &mask);
+// the smallest head (8, 16 or 32 words) whose inline entries (head - 4) hold >= 95% of the
+// non-empty lists; fit[k]: lists of at most (8 << k) - 4 entries
+uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]);
+// the KETOGPU_LABEL_REST_PERMILLE test knob: S head of x marked kNoLabel
+bool label_nolabel(uint64_t x, uint32_t permille);
 
 struct LabelIndex {
     uint32_t hs = 16, hp = 8;            // head words of S and P

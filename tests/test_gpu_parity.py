@@ -219,7 +219,7 @@ def test_hub_index_default_on_power_law(monkeypatch):
             assert st["hubs"] > 0
 
 
-def test_unit_spill_to_global_path():
+def test_unit_spill_to_global_path(monkeypatch):
     # both sides of the search are n nodes wide: top has n child groups g_i, the target
     # group T is a member of n groups p_i, and only g_7 -> p_7 connects them, so
     # no LDS table holds either side and requests fall through the whole cascade (bidi ->
@@ -234,12 +234,16 @@ def test_unit_spill_to_global_path():
     rows += [(1, "g00007", "m", None, 1, "p00007", "m")]
     rows += [(1, f"q{i:05d}", "m", None, 1, "T", "m") for i in range(3)]  # T also below q_i only
     snap = Snapshot.from_rows([("n", 1)], rows, sort=True)
+    label = check.Engine(snap)  # the default plan: labels answer without a search (nothing spills)
+    monkeypatch.setenv("KETOGPU_UNITS", "bidi")
     eng = check.Engine(snap)
     reqs = [rt.InternalRelationTuple("n", "top", "m", rt.SubjectSet("n", "T", "m")),
             rt.InternalRelationTuple("n", "top", "m", rt.SubjectID("u8")),
             rt.InternalRelationTuple("n", "g00009", "m", rt.SubjectSet("n", "T", "m")),  # g_9 -> u9 only
             rt.InternalRelationTuple("n", "q00001", "m", rt.SubjectSet("n", "T", "m")),
             rt.InternalRelationTuple("n", "p00003", "m", rt.SubjectSet("n", "T", "m"))] * 40
+    assert label.check_many(reqs) == [True, True, False, True, True] * 40
+    assert label.last_stats()["plan"] == 7 and label.last_stats()["spilled_units"] == 0
     got = eng.check_many(reqs)
     assert got == [True, True, False, True, True] * 40
     st = eng.last_stats()
@@ -394,3 +398,33 @@ def test_auto_plan_trials_then_keeps_one(kind, labels, monkeypatch):
     kept = eng.last_stats()["plan"]
     np.testing.assert_array_equal(eng.check_ids(roots[:5000], targets[:5000]), want[:5000])
     assert eng.last_stats()["plan"] == kept
+
+
+@pytest.mark.parametrize("graph,heads", [("random", "0,0"), ("random", "8,8"), ("family", "0,0"), ("family", "8,16"),
+                                         ("social", "0,0"), ("rbac", "0,0")])
+def test_label_device_build_equals_host(graph, heads, monkeypatch):
+    """the head arrays an engine builds on the device (label_count / write / patch kernels,
+    the host building only the lists of more than 64 entries) equal the host build
+    (labels.cpp build_labels, the test hook) word for word; a second engine over the same
+    snapshot reuses the snapshot's 2-hop labels (one build) and builds the same arrays"""
+    from keto_amd import synth
+    if graph == "random":
+        namespaces, rows = randgraph.make_graph(33, n_rows=900, n_obj=40, n_users=50, poison=True, collide=True)
+        snap = Snapshot.from_rows(namespaces, rows, page_size=3, sort=True)
+    elif graph == "family":
+        namespaces, rows, _ = randgraph.make_family_graph(92)
+        snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    else:
+        w = (synth.social(users=20000, groups=6000, tuples=150000, checks=10, seed=7) if graph == "social" else
+             synth.rbac(users=20000, groups=2000, docs=4000, tuples=120000, checks=10, seed=7))
+        snap = Snapshot.from_columns(w.namespaces, w.columns)
+    monkeypatch.setenv("KETOGPU_LABEL_HEADS", heads)
+    hs, hp = (int(x) for x in heads.split(","))
+    li = snap.label_index(hs, hp)
+    engines = [check.Engine(snap), check.Engine(snap)]
+    for eng in engines:
+        S, hs_dev = eng.label_heads(0)
+        P, hp_dev = eng.label_heads(1)
+        assert (hs_dev, hp_dev) == (li["s_head_words"], li["p_head_words"])
+        np.testing.assert_array_equal(S, li["S"])
+        np.testing.assert_array_equal(P, li["P"])
