@@ -453,6 +453,10 @@ typedef struct {
     uint64_t label_entries;     /* Lin + Lout entries                                   */
     uint64_t rest_requests;     /* requests of this run answered by the second stage    */
     double rest_ms;             /* second stage + statistics (events between kernels)   */
+    /* plan label on a writable snapshot (label_update: heads rewritten in place per write) */
+    uint64_t label_rewritten;   /* heads rewritten after writes                          */
+    uint64_t label_marked;      /* heads marked "no label" (second stage) since the build */
+    uint64_t label_relabels;    /* rebuilds from the current rows                        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
 /* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory) record a

@@ -2767,6 +2767,7 @@ struct LabelDevLists {
     const uint32_t *in, *out;
     const uint64_t *min, *mout;
     uint32_t Ni;
+    uint32_t ph[3];  // a writable snapshot's placeholders (free slots: Df, Dbi, Dbo; else NONE)
 };
 constexpr uint32_t kLabelBig = 0xFFFFFFFEu;  // count of a node the host builds
 
@@ -2794,7 +2795,9 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
     uint64_t lo = 0, mk = 0;
     if (lane < m) {
         e = synth ? x : PSIDE ? g.fint_col[b + lane] : g.rev_col[b + lane];
-        if (e < D.Ni) {
+        if (e == D.ph[0] || e == D.ph[1] || e == D.ph[2]) {
+            c = 0;  // a free slot
+        } else if (e < D.Ni) {
             const uint64_t *off = PSIDE ? D.out_off : D.in_off;
             lo = off[e];
             c = (uint32_t)(off[e + 1] - lo);
@@ -2807,7 +2810,7 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63) + (self_raw ? 1u : 0u);
     if (total > 64) return false;
     wave_sync();  // (the previous node's reads of buf are done)
-    if (lane < m) {
+    if (lane < m && c) {
         uint32_t o = incl - c;
         if (e < D.Ni) {
             const uint32_t *lst = (PSIDE ? D.out : D.in) + lo;
@@ -3985,6 +3988,13 @@ struct ketogpu_engine {
     double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
     uint64_t label_bytes = 0, label_entries = 0;
     uint64_t label_nwords[2] = {0, 0};  // words of the S and P arrays (heads + overflow)
+    // writable snapshots: what label_update needs to rewrite heads in place after a write
+    std::shared_ptr<const ReachLabels> lab_R;       // the 2-hop labels the heads were built from
+    std::vector<uint32_t> lab_cap[2], lab_ovf[2];   // per node: entries its storage holds, overflow start / 16
+    std::vector<uint64_t> lab_succ;                 // per interior node: hash of its real interior successors
+    std::vector<uint8_t> lab_pinv;                  // per expandable node: P marked kNoLabel (reaches a changed row)
+    uint64_t lab_invalid = 0, lab_rewritten = 0, lab_relabels = 0;
+    uint32_t lab_permille = 0;
     // a head-size pair (HS, HP) as template arguments
     template <class F>
     void label_dispatch(F &&f) {
@@ -4320,10 +4330,138 @@ struct ketogpu_engine {
             for (void *p : {(void *)d_seg, (void *)d_cols, (void *)d_recs}) (void)hipFree(p);
         }
         g.N = s.N;
+        if (use_label) label_update(fr, rr);
         patch_pos = s.patch_end();
         s.reader_at(this, patch_pos);
         synced_version = s.version;
         return nseg;
+    }
+
+    // hash of an interior node's real interior successors (writable rows: those below Dbi)
+    static uint64_t succ_hash(const Snapshot &s, uint32_t v) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (uint64_t k = s.fint_off[v]; k < s.fint_off[v + 1]; k++) {
+            const uint32_t u = s.fint_col[k];
+            if (u >= s.Dbi) break;  // the free slots (sorted last)
+            h = mix64(h ^ (u + 0x5851F42D4C957F2Dull));
+        }
+        return h;
+    }
+
+    // Plan label after an in-place write (writable snapshots), exact without a rebuild:
+    //  * a changed reverse row rev(t): S(t) recomputed from the current row and the labels'
+    //    Lin (the interior graph's labels are unchanged unless an interior row changed);
+    //  * a changed forward row of a non-interior node r: P(r) recomputed;
+    //  * an interior node v whose real interior successors changed (a nesting edge added or
+    //    removed): every expandable node that reaches v (backward over the current rows) gets
+    //    P = no label, so requests from those roots go to the second stage (plan lite over the
+    //    live device rows).  Exact: a request whose answer the change can alter has a root
+    //    that reaches a changed node; for any other root r, r's reachable region is unchanged
+    //    and so is every landmark w in it, so Lout(r) meets Lin(v) iff r ->* v as before.
+    //    Marks are kept (a later edge into a marked node marks its new predecessor too).
+    //  * a list that outgrows its node's storage: no label (second stage) until the relabel.
+    // When the marked heads pass KETOGPU_LABEL_RELABEL_PERMILLE of the P nodes (default 20),
+    // the labels are rebuilt from the current rows (relabel).
+    void label_update(const std::vector<uint32_t> &fr, const std::vector<uint32_t> &rr) {
+        const Snapshot &s = *snap;
+        if (!s.writable || !lab_R) return;
+        const ReachLabels &R = *lab_R;
+        std::vector<uint32_t> seeds;
+        for (uint32_t v : fr)
+            if (v < s.Ni && v != s.Df && v != s.Dbi) {
+                const uint64_t h = succ_hash(s, v);
+                if (h != lab_succ[v]) seeds.push_back(v), lab_succ[v] = h;
+            }
+        std::vector<uint32_t> marked;  // P heads newly marked no label
+        for (size_t h = 0; h < seeds.size(); h++) {  // seeds grows: a backward search
+            const uint32_t y = seeds[h];
+            if (lab_pinv[y]) continue;
+            lab_pinv[y] = 1;
+            marked.push_back(y);
+            for (uint64_t k = s.rev_off[y]; k < s.rev_off[y + 1]; k++) {
+                const uint32_t p = s.rev_col[k];
+                if (p != s.Dbi && p != s.Dbo && p < s.Nx && !lab_pinv[p]) seeds.push_back(p);
+            }
+        }
+        std::vector<uint32_t> rec[2];
+        std::vector<uint64_t> roff[2];
+        std::vector<uint32_t> l;
+        auto emit = [&](int side, uint32_t x, bool nolabel, uint64_t mask) {
+            const uint32_t h = side == 0 ? label_hs : label_hp, c = (uint32_t)l.size();
+            const bool fits = !nolabel && c <= lab_cap[side][x];
+            std::vector<uint32_t> &r = rec[side];
+            roff[side].push_back(r.size());
+            r.push_back(x);
+            r.push_back(fits ? c : 0u);  // entries the patch copies to the overflow region
+            const size_t hd = r.size();
+            r.resize(hd + h, 0xFFFFFFFFu);
+            if (!fits) {
+                r[hd] = kNoLabel, r[hd + 1] = r[hd + 2] = r[hd + 3] = 0;
+                lab_invalid += !nolabel || side == 1;
+                return;
+            }
+            const bool inl = c <= h - kHeadFixed;
+            r[hd] = c;
+            r[hd + 1] = inl ? 0u : lab_ovf[side][x];
+            r[hd + 2] = (uint32_t)mask;
+            r[hd + 3] = (uint32_t)(mask >> 32);
+            if (inl)
+                std::copy(l.begin(), l.end(), r.begin() + (ptrdiff_t)(hd + kHeadFixed));
+            else
+                r.insert(r.end(), l.begin(), l.end());
+            lab_rewritten++;
+        };
+        uint64_t mask = 0;
+        for (uint32_t t : rr) {
+            if (t >= lab_cap[0].size()) continue;
+            label_list(s, R, false, t, l, mask);
+            emit(0, t, !l.empty() && label_nolabel(t, lab_permille), mask);
+        }
+        for (uint32_t x : marked) {
+            l.clear();
+            emit(1, x, true, 0);
+        }
+        for (uint32_t r : fr) {
+            if (r < s.Ni || r >= s.Nx || lab_pinv[r]) continue;
+            bool stale = false;  // an entry that reaches a changed node: its Lout may be stale
+            for (uint64_t k = s.fint_off[r]; k < s.fint_off[r + 1] && !stale; k++) {
+                const uint32_t c = s.fint_col[k];
+                stale = c != s.Df && lab_pinv[c];
+            }
+            if (stale) {
+                lab_pinv[r] = 1;
+                l.clear();
+                emit(1, r, true, 0);
+                continue;
+            }
+            label_list(s, R, true, r, l, mask);
+            emit(1, r, false, mask);
+        }
+        for (int side = 0; side < 2; side++) {
+            if (roff[side].empty()) continue;
+            uint32_t *drec = dupload(rec[side]);
+            uint64_t *droff = dupload(roff[side]);
+            KLAUNCH(label_patch_kernel, dim3((unsigned)std::min<size_t>(roff[side].size(), 4096)), dim3(64), 0, stream,
+                    drec, droff, (uint32_t)roff[side].size(), const_cast<uint32_t *>(side == 0 ? lgraph.S : lgraph.P),
+                    side == 0 ? label_hs : label_hp);
+            HIP_CHECK(hipStreamSynchronize(stream));
+            (void)hipFree(drec);
+            (void)hipFree(droff);
+        }
+        uint64_t limit = 20;
+        if (const char *e = getenv("KETOGPU_LABEL_RELABEL_PERMILLE")) limit = strtoull(e, nullptr, 10);
+        if (lab_invalid * 1000 > limit * std::max<uint64_t>(s.Nx, 1)) relabel();
+    }
+
+    // the labels rebuilt from the current rows (the old arrays freed first)
+    void relabel() {
+        uint32_t *A[2] = {const_cast<uint32_t *>(lgraph.S), const_cast<uint32_t *>(lgraph.P)};
+        release_label(A);
+        lgraph = LabelGraph{nullptr, nullptr};
+        lab_R.reset();
+        use_label = true;
+        build_label(*snap);
+        lab_relabels++;
     }
 
     ~ketogpu_engine() {
@@ -4392,10 +4530,10 @@ struct ketogpu_engine {
         };
         // bidi / lite: R4 flags come from forward rows, so snapshots with ambiguous keys stay on v2
         use_lite = lite_req && use_v2 && !s.has_ambiguous && lite_ok;
-        // plan core and plan label: not on writable snapshots (an in-place write would change
-        // closures and labels)
+        // plan core: not on writable snapshots (an in-place write would change closures)
         use_core = (p == "core" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_CORE") == nullptr;
-        use_label = (p == "label" || p == "auto") && use_lite && !s.writable && getenv("KETOGPU_NO_LABEL") == nullptr;
+        // (labels on a writable snapshot are kept exact in place by label_update)
+        use_label = (p == "label" || p == "auto") && use_lite && getenv("KETOGPU_NO_LABEL") == nullptr;
         if (const char *e = getenv("KETOGPU_CLOSURE")) sscanf(e, "%u,%u", &closure_cap[0], &closure_cap[1]);
         if (const char *e = getenv("KETOGPU_CORE_SHAPE")) core_shape = atoi(e);
         if (const char *e = getenv("KETOGPU_CORE_BLOCKS")) sscanf(e, "%u,%u", &core_block[0], &core_block[1]);
@@ -4672,13 +4810,14 @@ struct ketogpu_engine {
                     if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
                     return p;
                 };
-                LabelDevLists D{up(R->in_off), up(R->out_off), up(R->in), up(R->out), up(R->min), up(R->mout), s.Ni};
+                LabelDevLists D{up(R->in_off), up(R->out_off), up(R->in), up(R->out), up(R->min), up(R->mout), s.Ni,
+                                {s.writable ? s.Df : NONE, s.writable ? s.Dbi : NONE, s.writable ? s.Dbo : NONE}};
                 unsigned long long *ctr = dalloc<unsigned long long>(8);
                 tmp.push_back(ctr);
                 uint64_t used = 0;
                 label_bytes = 0;
                 for (int side = 0; side < 2; side++) {
-                    const uint32_t n = side == 0 ? s.N : s.Nx;
+                    const uint32_t n = side == 0 ? (uint32_t)label_s_nodes(s) : s.Nx;
                     uint32_t *cnt = dalloc<uint32_t>(std::max<uint32_t>(n, 1)), *off16 = dalloc<uint32_t>(std::max<uint32_t>(n, 1));
                     tmp.push_back(cnt);
                     tmp.push_back(off16);
@@ -4807,6 +4946,16 @@ struct ketogpu_engine {
                     unsigned long long tally[3];
                     HIP_CHECK(hipMemcpyAsync(tally, ctr, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
                     HIP_CHECK(hipStreamSynchronize(stream));
+                    if (s.writable) {  // what label_update needs: every node's storage (counts, overflow starts)
+                        std::vector<uint32_t> &cap_v = lab_cap[side], &ovf_v = lab_ovf[side];
+                        cap_v.resize(n);
+                        ovf_v.resize(n);
+                        if (n) {
+                            HIP_CHECK(hipMemcpy(cap_v.data(), cnt, (size_t)n * 4, hipMemcpyDeviceToHost));
+                            HIP_CHECK(hipMemcpy(ovf_v.data(), off16, (size_t)n * 4, hipMemcpyDeviceToHost));
+                        }
+                        for (uint32_t x = 0; x < n; x++) cap_v[x] = cap_v[x] <= cap ? cap : (cap_v[x] + 15) / 16 * 16;
+                    }
                     if (side == 0) {
                         s_entries += tally[0];
                         nolabel += tally[1];
@@ -4819,6 +4968,7 @@ struct ketogpu_engine {
                     free_tmp_side(tmp, {cnt, off16, big});
                 }
                 free_tmp();
+                if (s.writable) lab_R = R;
             }
         } catch (const Error &e) {
             fprintf(stderr, "[ketogpu] plan label disabled: %s\n", e.what());
@@ -4833,10 +4983,34 @@ struct ketogpu_engine {
             drop_label();
             return;
         }
-        rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
-        owned.push_back(rest_counts);
-        HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
+        if (!rest_counts) {
+            rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
+            owned.push_back(rest_counts);
+            HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
+        }
         lgraph = LabelGraph{A[1], A[0]};
+        if (s.writable) {
+            if (!lab_R) {  // (the host build path: labels and storage from the snapshot again)
+                lab_R = reach_labels_of(s);
+                for (int side = 0; side < 2; side++) {
+                    const uint64_t n = side == 0 ? label_s_nodes(s) : s.Nx;
+                    std::vector<uint32_t> hd((size_t)n * H[side]);
+                    if (n) HIP_CHECK(hipMemcpy(hd.data(), A[side], hd.size() * 4, hipMemcpyDeviceToHost));
+                    lab_cap[side].resize(n);
+                    lab_ovf[side].resize(n);
+                    for (uint64_t x = 0; x < n; x++) {
+                        const uint32_t c = hd[x * H[side]], o = hd[x * H[side] + 1];
+                        lab_ovf[side][x] = o;
+                        lab_cap[side][x] = o && c != kNoLabel ? (c + 15) / 16 * 16 : H[side] - kHeadFixed;
+                    }
+                }
+            }
+            lab_succ.resize(s.Ni);
+            for (uint32_t v = 0; v < s.Ni; v++) lab_succ[v] = succ_hash(s, v);
+            lab_pinv.assign(s.Nx, 0);
+            lab_invalid = 0;
+            lab_permille = permille;
+        }
         label_hs = H[0];
         label_hp = H[1];
         label_coverage = nonempty_s ? 1.0 - (double)nolabel / (double)nonempty_s : 1.0;
@@ -5541,6 +5715,9 @@ struct ketogpu_engine {
         rs.label_pll_ms = label_pll_ms;
         rs.label_bytes = label_bytes;
         rs.label_entries = label_entries;
+        rs.label_rewritten = lab_rewritten;
+        rs.label_marked = lab_invalid;
+        rs.label_relabels = lab_relabels;
         ev_used = 0;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> push_ev, pull_ev;
         hipEvent_t t_begin = ev(), t_end = ev();

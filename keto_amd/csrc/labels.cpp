@@ -19,7 +19,9 @@ using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
 
 // the interior graph in both directions: forward fint(v), backward the interior prefix of
-// the sorted rev(v) (the nodes of a path between interior nodes are all interior)
+// the sorted rev(v) (the nodes of a path between interior nodes are all interior).  On a
+// writable snapshot rows end in placeholder slots (Df / Dbi, the two largest interior ids,
+// snapshot_write.cpp make_writable): the real interior entries are those below Dbi.
 struct IAdj {
     const uint32_t *col[2] = {nullptr, nullptr};
     std::vector<uint64_t> beg[2];
@@ -27,7 +29,7 @@ struct IAdj {
 };
 
 void make_adj(const Snapshot &s, IAdj &a) {
-    const uint32_t n = s.Ni;
+    const uint32_t n = s.Ni, bound = s.writable ? s.Dbi : n;
     a.col[0] = s.fint_col.data();
     a.col[1] = s.rev_col.data();
     for (int d = 0; d < 2; d++) {
@@ -36,11 +38,12 @@ void make_adj(const Snapshot &s, IAdj &a) {
     }
     parallel_chunks(n, 1 << 16, [&](int, uint64_t b, uint64_t e) {
         for (uint64_t v = b; v < e; v++) {
+            const uint32_t *fb = s.fint_col.data() + s.fint_off[v], *fe = s.fint_col.data() + s.fint_off[v + 1];
             a.beg[0][v] = s.fint_off[v];
-            a.deg[0][v] = (uint32_t)(s.fint_off[v + 1] - s.fint_off[v]);
+            a.deg[0][v] = s.writable ? (uint32_t)(std::lower_bound(fb, fe, bound) - fb) : (uint32_t)(fe - fb);
             const uint32_t *rb = s.rev_col.data() + s.rev_off[v], *re = s.rev_col.data() + s.rev_off[v + 1];
             a.beg[1][v] = s.rev_off[v];
-            a.deg[1][v] = (uint32_t)(std::lower_bound(rb, re, n) - rb);
+            a.deg[1][v] = (uint32_t)(std::lower_bound(rb, re, bound) - rb);
         }
     });
 }
@@ -280,9 +283,10 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
 
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s) {
     std::lock_guard<std::mutex> lk(s.derived_mu);
-    if (!s.reach_cache) {
+    if (!s.reach_cache || s.reach_cache->version != s.version) {  // (a writable snapshot's writes bump it)
         auto R = std::make_shared<ReachLabels>();
         build_reach_labels(s, *R);
+        R->version = s.version;
         s.reach_cache = std::move(R);
     }
     return s.reach_cache;
@@ -300,6 +304,7 @@ struct Lists {
         const uint32_t *b = s.rev_col.data() + s.rev_off[x], *e = s.rev_col.data() + s.rev_off[x + 1];
         for (const uint32_t *p = b; p < e; p++) {
             const uint32_t v = *p;
+            if (s.writable && (v == s.Dbi || v == s.Dbo)) continue;  // a free slot
             if (v < R.n) {
                 mask |= R.min[v];
                 out.insert(out.end(), R.in.begin() + (ptrdiff_t)R.in_off[v], R.in.begin() + (ptrdiff_t)R.in_off[v + 1]);
@@ -322,6 +327,7 @@ struct Lists {
         out.push_back((uint32_t)r);
         const uint32_t *b = s.fint_col.data() + s.fint_off[r], *e = s.fint_col.data() + s.fint_off[r + 1];
         for (const uint32_t *p = b; p < e; p++) {
+            if (s.writable && *p == s.Df) continue;  // a free slot
             mask |= R.mout[*p];
             out.insert(out.end(), R.out.begin() + (ptrdiff_t)R.out_off[*p], R.out.begin() + (ptrdiff_t)R.out_off[*p + 1]);
         }
@@ -348,6 +354,8 @@ uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]) {
     return 32;
 }
 
+uint64_t label_s_nodes(const Snapshot &s) { return s.writable ? s.n_cap : s.N; }
+
 bool label_nolabel(uint64_t x, uint32_t permille) {
     return permille && mix64(x * 0x9E3779B97F4A7C15ull + 17) % 1000 < permille;
 }
@@ -372,7 +380,7 @@ void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_per
     out.pll_ms = R.ms;
     out.label_entries = R.in.size() + R.out.size();
     const Lists lists{s, R};
-    const uint64_t ns = s.N, np = s.Nx;
+    const uint64_t ns = label_s_nodes(s), np = s.Nx;
     out.s_nodes = ns;
     out.p_nodes = np;
     // pass 1: list lengths
@@ -475,7 +483,6 @@ int ketogpu_label_index_build(const ketogpu_snapshot *s, uint32_t s_head_words, 
         *out = nullptr;
         const auto *snap = reinterpret_cast<const ketogpu::Snapshot *>(s);
         std::shared_lock<std::shared_mutex> lk(snap->mu);
-        if (snap->writable) throw ketogpu::Error(KETOGPU_EINVAL, "plan label: a writable snapshot");
         auto l = std::make_unique<ketogpu_label_index>();
         ketogpu::build_labels(*snap, s_head_words, p_head_words, 0, 0, l->li);
         *out = l.release();

@@ -56,6 +56,7 @@ struct ReachLabels {
     std::vector<uint64_t> in_off, out_off;
     std::vector<uint32_t> in, out;       // ranks >= bits, ascending per node
     uint64_t batches = 0;                // parallel batches of the pruned searches
+    uint64_t version = 0;                // the snapshot version they were built at
     double ms = 0;
 };
 
@@ -63,8 +64,8 @@ struct ReachLabels {
 // the others run in parallel batches of max(4 x threads, rank / KETOGPU_LABEL_BATCH_DIV)
 // (default 8)
 void build_reach_labels(const Snapshot &s, ReachLabels &out);
-// the snapshot's labels, built once and shared by every engine over it (ketogpu_multi_new
-// builds one set for all devices); the snapshot must not be writable
+// the snapshot's labels, built once per snapshot version and shared by every engine over
+// it (ketogpu_multi_new builds one set for all devices)
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s);
 
 // one node's list and mask as its head holds them (p_side: P(x), else S(x))
@@ -73,6 +74,8 @@ void label_list(const Snapshot &s, const ReachLabels &R, bool p_side, uint64_t x
 // the smallest head (8, 16 or 32 words) whose inline entries (head - 4) hold >= 95% of the
 // non-empty lists; fit[k]: lists of at most (8 << k) - 4 entries
 uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]);
+// S heads: every node, and on a writable snapshot every reserved id too (n_cap)
+uint64_t label_s_nodes(const Snapshot &s);
 // the KETOGPU_LABEL_REST_PERMILLE test knob: S head of x marked kNoLabel
 bool label_nolabel(uint64_t x, uint32_t permille);
 

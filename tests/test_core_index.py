@@ -251,3 +251,19 @@ def test_long_lists():
     assert any(want) and not all(want)
     li = check_labels(snap, reqs, want, (8, 8))
     assert li["s_overflow"] > 0 and li["label_entries"] > 0
+
+
+def test_labels_on_a_written_writable_snapshot():
+    """a writable snapshot's rows end in free slots (placeholder nodes): the labels are
+    built from the real entries only, and answer every request exactly after writes"""
+    from tests.test_writes import _graph, _writes, _expected, _sqlite_key
+    namespaces, rows = _graph(341, n_rows=700, n_obj=25, n_users=30)
+    w = Snapshot.from_rows(namespaces, rows, sort=True, writable=True)
+    cur = sorted(rows, key=_sqlite_key)
+    for step in range(3):
+        ins, dele = _writes(600 + step, namespaces, cur)
+        assert w.write(ins, dele)["applied"]
+        cur = _expected(cur, ins, dele)
+        reqs = randgraph.make_requests(700 + step, namespaces, cur, n=800, wildcard=False)
+        want = randgraph.oracle_store(namespaces, cur).check_batch(reqs)
+        check_labels(w, reqs, want)

@@ -409,7 +409,7 @@ def test_label_device_build_equals_host(graph, heads, monkeypatch):
     snapshot reuses the snapshot's 2-hop labels (one build) and builds the same arrays"""
     from keto_amd import synth
     if graph == "random":
-        namespaces, rows = randgraph.make_graph(33, n_rows=900, n_obj=40, n_users=50, poison=True, collide=True)
+        namespaces, rows = randgraph.make_graph(33, n_rows=900, n_obj=40, n_users=50, poison=True)  # (no R4 keys)
         snap = Snapshot.from_rows(namespaces, rows, page_size=3, sort=True)
     elif graph == "family":
         namespaces, rows, _ = randgraph.make_family_graph(92)

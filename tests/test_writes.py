@@ -217,17 +217,28 @@ def _tuple(r, id2name):
 
 
 @pytest.mark.gpu
-def test_versioned_engine_writes_in_place_and_reads_them():
+@pytest.mark.parametrize("plan", ["label", "label-marks", "label-relabel", "lite"])
+def test_versioned_engine_writes_in_place_and_reads_them(plan, monkeypatch):
     """read-your-writes against the oracle after every batch; most batches in place, a
-    batch with a new group through the rebuild"""
+    batch with a new group through the rebuild.  Plan label keeps its labels exact in place
+    (label_update: changed rows' heads rewritten, roots above a changed nesting edge sent to
+    the second stage), relabelling past the default share of marked heads, never
+    (label-marks) or at every marked head (label-relabel); plan lite for comparison"""
     from keto_amd.freshness import VersionedEngine
     if L.lib().ketogpu_device_count() < 1:
         pytest.fail("no HIP device visible")
+    if plan == "lite":
+        monkeypatch.setenv("KETOGPU_NO_LABEL", "1")
+    elif plan == "label-marks":
+        monkeypatch.setenv("KETOGPU_LABEL_RELABEL_PERMILLE", "1000")
+    elif plan == "label-relabel":
+        monkeypatch.setenv("KETOGPU_LABEL_RELABEL_PERMILLE", "0")
     namespaces, rows = _graph(331, n_rows=700, n_obj=25, n_users=30)
     ve = VersionedEngine(Snapshot.from_rows(namespaces, rows, sort=True, writable=True))
     id2name = {i: n for n, i in namespaces}
     cur = sorted(rows, key=_sqlite_key)
     paths = []
+    marks = relabels = 0
     for step in range(8):
         ins, dele = _writes(400 + step, namespaces, cur, new_groups=(step == 5))
         ve.transact(insert=[_tuple(r, id2name) for r in ins], delete=[_tuple(d, id2name) for d in dele])
@@ -248,6 +259,11 @@ def test_versioned_engine_writes_in_place_and_reads_them():
                         f"fresh writable engine {sum(a != bool(b) for a, b in zip(fresh_w, want))}, "
                         f"fresh compact engine {sum(a != bool(b) for a, b in zip(fresh_c, want))}")
         assert list(ve._state[1].check_batch(tuples)) == [bool(x) for x in want], step  # the id path
+        st = eng.last_stats()
+        assert (st["plan"] == 7) == (plan != "lite"), (step, st["plan"])
+        if plan != "lite" and ve.last_write["path"] == "in_place":
+            marks += st["label_marked"] > 0
+            relabels = max(relabels, st["label_relabels"])
         orc = randgraph.oracle_store(namespaces, cur)
         known = {n for n, _ in namespaces}
         for ns, o, r, _ in [q for q in reqs if q[0] in known][:40]:
@@ -255,6 +271,10 @@ def test_versioned_engine_writes_in_place_and_reads_them():
             want_tree = orc.expand({"subject_set": {"namespace": ns, "object": o, "relation": r}}, 3)
             assert got == want_tree, (step, ns, o, r)
     assert paths.count("in_place") >= 5 and "rebuild" in paths, paths
+    if plan == "label-marks":
+        assert marks > 0 and relabels == 0  # nesting edges changed: roots marked, never relabelled
+    if plan == "label-relabel":
+        assert relabels > 0
 
 
 def test_hub_fanout_is_refused_past_the_budget(monkeypatch):
