@@ -2532,25 +2532,18 @@ struct LabelRest {
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
 };
-// A request's lists in LDS: the S head's inline entries (HS - 4, then 4 pad words) and the
-// P head's (HP - 4, then 4 pad words), each + 1 word: odd strides, so the 16 requests' lists
+// A request's two heads in LDS, as read (word k of the head at position k; the entries
+// from word 4), rows of HS + 4 / HP + 4 words: 16-byte aligned, and the 16 requests' rows
 // start in different banks
+// + a scratch row where the wave stages one overflow list at a time (kLabelScratch words)
+constexpr uint32_t kLabelScratch = 512;
 template <int HS, int HP>
-struct LabelShared {
-    uint32_t S[16 * (HS + 1)], P[16 * (HP + 1)];
+struct alignas(16) LabelShared {
+    uint32_t S[16 * (HS + 4)], P[16 * (HP + 4)];
+    uint32_t X[kLabelScratch];
 };
 
-// x among the W (a power of two) ascending entries of S (padded with 0xFFFFFFFF, which is
-// no entry)
-template <int W>
-__device__ __forceinline__ bool label_find(const uint32_t *S, uint32_t x) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t step = W / 2; step; step >>= 1)
-        if (S[pos + step - 1] < x) pos += step;
-    return S[pos] == x;
-}
-// x among the n ascending entries of an overflow list (global memory)
+// x among the n ascending entries of a list (LDS or global memory)
 __device__ __forceinline__ bool label_find_n(const uint32_t *S, uint32_t n, uint32_t x) {
     const uint32_t n0 = n;
     uint32_t lo = 0;
@@ -2580,20 +2573,63 @@ __device__ __forceinline__ void label_head_load(const uint32_t *head, uint32_t s
         }
     }
 }
-// word j (< 4: count, overflow start, mask lo, mask hi) of the request's head, on every lane
+// word J (< 4: count, overflow start, mask lo, mask hi) of the request's head on all four of
+// its lanes: a DPP quad broadcast (the four lanes of a request are one DPP quad)
 template <int W, int J>
-__device__ __forceinline__ uint32_t label_word(const uint32_t (&w)[W], uint32_t lane) {
-    return (uint32_t)__shfl((int)w[J % W], (int)((lane & ~3u) + J / W), 64);
+__device__ __forceinline__ uint32_t label_word(const uint32_t (&w)[W]) {
+    constexpr int src = J / W;
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[J % W], src * 0x55, 0xf, 0xf, false);  // quad_perm [src x 4]
 }
-// a head's inline entries (words 4..H-1) to LDS positions 0..H-5, pad words at H-4..H-1
-template <int H>
-__device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[H / 4], uint32_t sub) {
+// the head image to LDS (aligned rows)
+template <int W>
+__device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[W], uint32_t sub) {
+    if constexpr (W == 2) {
+        reinterpret_cast<uint2 *>(L)[sub] = make_uint2(w[0], w[1]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < H / 4; k++) {
-        const uint32_t x = (H / 4) * sub + k;
-        L[(x + H - kHeadFixed) % H] = x < kHeadFixed ? 0xFFFFFFFFu : w[k];
+        for (int k = 0; k < W / 4; k++)
+            reinterpret_cast<uint4 *>(L)[(W / 4) * sub + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
 }
+// the lane's head words as entries to compare: the four header words and the padding
+// become 0xFFFFFFFE, which equals neither an entry (< 2^31) nor the other list's padding
+template <int W>
+__device__ __forceinline__ void label_cmp_words(const uint32_t (&w)[W], uint32_t sub, uint32_t (&c)[W]) {
+#pragma unroll
+    for (int k = 0; k < W; k++) c[k] = (uint32_t)(W * sub + k) < kHeadFixed || w[k] == 0xFFFFFFFFu ? 0xFFFFFFFEu : w[k];
+}
+// does one of the n entries at L (LDS, 16-byte aligned, padded with 0xFFFFFFFF to a
+// multiple of 4) equal one of the lane's words c?  Every lane of the request reads the
+// same entries (LDS broadcast) and compares them with its quarter of the other head
+template <int W>
+__device__ __forceinline__ bool label_meet(const uint32_t *L, uint32_t n, const uint32_t (&c)[W]) {
+    bool hit = false;
+    for (uint32_t j = 0; j < n && !hit; j += 4) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(L + j);
+#pragma unroll
+        for (int k = 0; k < W; k++) hit |= c[k] == x.x || c[k] == x.y || c[k] == x.z || c[k] == x.w;
+    }
+    return hit;
+}
+
+// x among the E ascending entries at L (LDS; E = head - 4, not a power of two): a branchless
+// binary search, positions past E read as above every entry
+template <int E>
+__device__ __forceinline__ bool label_find_e(const uint32_t *L, uint32_t x) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t step = 16; step; step >>= 1)
+        if (step <= (uint32_t)E && pos + step <= (uint32_t)E && L[pos + step - 1] < x) pos += step;
+    return pos < (uint32_t)E && L[pos] == x;
+}
+
+// KETO_LABEL_MEET: how the shorter of two inline lists meets the other (0: each entry,
+// round-robin over the request's four lanes, binary-searched in the other list in LDS;
+// 1: all four lanes read every entry and compare it with their quarter of the other head
+// in registers)
+#ifndef KETO_LABEL_MEET
+#define KETO_LABEL_MEET 0
+#endif
 
 template <int HS, int HP>
 __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelGraph &L, uint32_t r_lane,
@@ -2614,16 +2650,15 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
         label_head_load<SW>(L.S + (uint64_t)t * HS, sub, sw);
         label_head_load<PW>(L.P + (uint64_t)r * HP, sub, pw);
     }
-    const uint32_t ns = label_word<SW, 0>(sw, lane), np = label_word<PW, 0>(pw, lane);
+    const uint32_t ns = label_word<SW, 0>(sw), np = label_word<PW, 0>(pw);
     const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
-    const uint64_t smask = (uint64_t)label_word<SW, 2>(sw, lane) | (uint64_t)label_word<SW, 3>(sw, lane) << 32;
-    const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw, lane) | (uint64_t)label_word<PW, 3>(pw, lane) << 32;
-    // (the overflow starts read here: no cross-lane reads inside the divergent search below)
-    const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw, lane) * 16;
-    const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw, lane) * 16;
-    uint32_t *Sl = sh.S + q * (HS + 1), *Pl = sh.P + q * (HP + 1);
-    label_to_lds<HS>(Sl, sw, sub);
-    label_to_lds<HP>(Pl, pw, sub);
+    const uint64_t smask = (uint64_t)label_word<SW, 2>(sw) | (uint64_t)label_word<SW, 3>(sw) << 32;
+    const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw) | (uint64_t)label_word<PW, 3>(pw) << 32;
+    const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw) * 16;  // overflow lists
+    const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw) * 16;
+    uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
+    label_to_lds<SW>(Sl, sw, sub);
+    label_to_lds<PW>(Pl, pw, sub);
     // a request without labels (or with a wildcard root): listed for the second stage
     {
         const bool rest = sub == 0 && some && !labelled;
@@ -2633,41 +2668,83 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     }
     __syncthreads();
     bool hit = labelled && (smask & pmask) != 0;
-    uint32_t looked = 0;
+    // 1. the heads' inline entries: whole lists, or the first entries of an overflowing one
+    //    (most hits are found there): the shorter walked, round-robin over the request's
+    //    four lanes, each entry searched in the other (KETO_LABEL_MEET 1: compared with the
+    //    other head's words in registers)
+    const uint32_t es = min(ns, (uint32_t)(HS - kHeadFixed)), ep = min(np, (uint32_t)(HP - kHeadFixed));
     if (labelled && !hit) {
-        // the shorter list is walked (its entries round-robin over the request's four
-        // lanes), each entry looked up in the longer one by a binary search
-        const bool s_in = ns <= (uint32_t)(HS - kHeadFixed), p_in = np <= (uint32_t)(HP - kHeadFixed);
-        const bool walk_p = np <= ns;
-        if (s_in && p_in) {  // both lists in LDS (the common case: LDS addressing throughout)
-            if (walk_p)
-                for (uint32_t k = sub; k < np && !hit; k += 4, looked++) hit = label_find<HS>(Sl, Pl[k]);
+        if (!KETO_LABEL_MEET) {
+            if (es <= ep)
+                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_find_e<HP - kHeadFixed>(Pl + kHeadFixed, Sl[kHeadFixed + k]);
             else
-                for (uint32_t k = sub; k < ns && !hit; k += 4, looked++) hit = label_find<HP>(Pl, Sl[k]);
-        } else {  // a list in the overflow region
-            const uint32_t nw = walk_p ? np : ns, nl = walk_p ? ns : np;
-            const uint32_t *W = walk_p ? (p_in ? Pl : Pg) : (s_in ? Sl : Sg);
-            for (uint32_t k = sub; k < nw && !hit; k += 4, looked++) {
-                const uint32_t x = W[k];
-                hit = walk_p ? (s_in ? label_find<HS>(Sl, x) : label_find_n(Sg, nl, x))
-                             : (p_in ? label_find<HP>(Pl, x) : label_find_n(Pg, nl, x));
-            }
+                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_find_e<HS - kHeadFixed>(Sl + kHeadFixed, Pl[kHeadFixed + k]);
+        } else if (es <= ep) {
+            uint32_t c[PW];
+            label_cmp_words<PW>(pw, sub, c);
+            hit = label_meet<PW>(Sl + kHeadFixed, es, c);
+        } else {
+            uint32_t c[SW];
+            label_cmp_words<SW>(sw, sub, c);
+            hit = label_meet<SW>(Pl + kHeadFixed, ep, c);
         }
     }
-    const uint64_t bits = __ballot(hit);
-    uint64_t rows = labelled && sub == 0 ? 2 : 0;
-    // entries read: the walked ones, the other list once, and the two masks (4 words)
-    uint64_t ent = looked + (labelled && sub == 0 ? (np <= ns ? ns : np) + kHeadFixed : 0);
-#pragma unroll
-    for (int k = 32; k; k >>= 1) {
-        rows += __shfl_down(rows, k, 64);
-        ent += __shfl_down(ent, k, 64);
+    // 2. a request with an overflowing list and no hit yet: the whole lists, one request at
+    //    a time per wave — the longer list staged in LDS by the whole wave (one dependent
+    //    read, not a chain of them), the shorter walked by the request's lanes
+    {
+        uint64_t need = __ballot(labelled && !hit && sub == 0 && (ns > (uint32_t)(HS - kHeadFixed) || np > (uint32_t)(HP - kHeadFixed)));
+        while (need) {  // (wave-uniform)
+            const uint32_t j = (uint32_t)__builtin_ctzll(need) & ~3u;
+            need &= need - 1;
+            const uint32_t nsj = (uint32_t)__builtin_amdgcn_readlane((int)ns, (int)j);
+            const uint32_t npj = (uint32_t)__builtin_amdgcn_readlane((int)np, (int)j);
+            const bool walk_p = npj <= nsj;
+            const uint32_t nw = walk_p ? npj : nsj, nl = walk_p ? nsj : npj;
+            const bool l_over = walk_p ? nsj > (uint32_t)(HS - kHeadFixed) : npj > (uint32_t)(HP - kHeadFixed);
+            const bool w_over = walk_p ? npj > (uint32_t)(HP - kHeadFixed) : nsj > (uint32_t)(HS - kHeadFixed);
+            const uint64_t lg = (uint64_t)(walk_p ? Sg : Pg), wg = (uint64_t)(walk_p ? Pg : Sg);
+            const uint32_t *Lg = (const uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lg >> 32), (int)j) << 32) |
+                                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lg, (int)j));
+            const uint32_t *Wg = (const uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(wg >> 32), (int)j) << 32) |
+                                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wg, (int)j));
+            const uint32_t q0 = j >> 2;
+            const uint32_t *Ll = walk_p ? sh.S + q0 * (HS + 4) + kHeadFixed : sh.P + q0 * (HP + 4) + kHeadFixed;
+            const uint32_t *Wl = walk_p ? sh.P + q0 * (HP + 4) + kHeadFixed : sh.S + q0 * (HS + 4) + kHeadFixed;
+            const uint32_t *O = Ll;  // where the longer list is searched
+            if (l_over) {
+                if (nl <= kLabelScratch) {  // overflow lists are whole 16-word units: uint4 reads stay inside
+                    for (uint32_t i = lane; i * 4 < nl; i += 64)
+                        reinterpret_cast<uint4 *>(sh.X)[i] = reinterpret_cast<const uint4 *>(Lg)[i];
+                    __syncthreads();
+                    O = sh.X;
+                } else {
+                    O = Lg;
+                }
+            }
+            if (q == q0) {
+                const uint32_t *W = w_over ? Wg : Wl;
+                for (uint32_t k = sub; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
+            }
+            __syncthreads();
+        }
     }
+    uint32_t looked = 0;
+    const uint64_t bits = __ballot(hit);
+    // statistics: 2 rows (heads) and the entries read (both lists and the masks) per request
+    const uint32_t rows = wave_sum_all(labelled && sub == 0 ? 2u : 0u);
+    const uint32_t ent = wave_sum_all(labelled && sub == 0 ? ns + np + kHeadFixed : 0u);
+    (void)looked;
+    // bit j of the unit's result = any of the request's four lanes (scalar bit compression)
+    uint64_t x = bits | bits >> 1;
+    x = (x | x >> 2) & 0x1111111111111111ull;
+    x = (x | x >> 3) & 0x0303030303030303ull;
+    x = (x | x >> 6) & 0x000F000F000F000Full;
+    x = (x | x >> 12) & 0x000000FF000000FFull;
+    x = (x | x >> 24) & 0xFFFFull;
     if (lane == 0) {
-        uint32_t res = 0;
-        for (int j = 0; j < 16; j++) res |= ((bits >> (4 * j)) & 0xFull) ? 1u << j : 0u;
         const uint64_t c0 = unit * 16;
-        if (res) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)res << (c0 & 63));
+        if (x) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)x << (c0 & 63));
         atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
         atomicAdd(&stat_slot(stats)[2], (unsigned long long)ent);  // u32 entries: 4 B each
     }
@@ -2939,8 +3016,11 @@ __global__ __launch_bounds__(256) void label_write_kernel(DevGraph g, LabelDevLi
         const uint32_t c = (uint32_t)__popcll(keep);
         uint32_t *head = A + (uint64_t)x * H;
         const bool inl = c <= H - kHeadFixed;
-        uint32_t *dst = inl ? head + kHeadFixed : A + (uint64_t)off16[x] * 16;
-        if ((keep >> lane) & 1) dst[lanes_below(keep)] = v;
+        if ((keep >> lane) & 1) {  // (an overflowing list: whole in the overflow region, its prefix in the head)
+            const uint32_t pos = lanes_below(keep);
+            if (pos < H - kHeadFixed) head[kHeadFixed + pos] = v;
+            if (!inl) A[(uint64_t)off16[x] * 16 + pos] = v;
+        }
         if (lane == 0) {
             // (the test knob's hash: labels.cpp label_nolabel)
             uint64_t hx = (uint64_t)x * 0x9E3779B97F4A7C15ull + 17;
@@ -4405,10 +4485,8 @@ struct ketogpu_engine {
             r[hd + 1] = inl ? 0u : lab_ovf[side][x];
             r[hd + 2] = (uint32_t)mask;
             r[hd + 3] = (uint32_t)(mask >> 32);
-            if (inl)
-                std::copy(l.begin(), l.end(), r.begin() + (ptrdiff_t)(hd + kHeadFixed));
-            else
-                r.insert(r.end(), l.begin(), l.end());
+            std::copy(l.begin(), l.begin() + std::min<size_t>(c, h - kHeadFixed), r.begin() + (ptrdiff_t)(hd + kHeadFixed));
+            if (!inl) r.insert(r.end(), l.begin(), l.end());
             lab_rewritten++;
         };
         uint64_t mask = 0;
@@ -4927,10 +5005,9 @@ struct ketogpu_engine {
                             rec[hd + 1] = inl ? 0u : hoff[k];
                             rec[hd + 2] = (uint32_t)bmask[k];
                             rec[hd + 3] = (uint32_t)(bmask[k] >> 32);
-                            if (inl)
-                                std::copy(blist[k].begin(), blist[k].end(), rec.begin() + (ptrdiff_t)(hd + kHeadFixed));
-                            else
-                                rec.insert(rec.end(), blist[k].begin(), blist[k].end());
+                            std::copy(blist[k].begin(), blist[k].begin() + std::min<size_t>(c, cap),
+                                      rec.begin() + (ptrdiff_t)(hd + kHeadFixed));
+                            if (!inl) rec.insert(rec.end(), blist[k].begin(), blist[k].end());
                             nolabel += nl;
                             if (side == 0) s_entries += c;
                         }

@@ -436,8 +436,11 @@ void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_per
         hd[1] = (uint32_t)(ovf[x] / 16);
         hd[2] = (uint32_t)mask;
         hd[3] = (uint32_t)(mask >> 32);
-        uint32_t *dst = l.size() > h - kHeadFixed ? A.data() + ovf[x] : hd + kHeadFixed;
-        std::copy(l.begin(), l.end(), dst);
+        // an overflowing list lies whole in the overflow region, its first h - 4 entries also
+        // in the head (most hits are found there without the second read)
+        const size_t inl = std::min<size_t>(l.size(), h - kHeadFixed);
+        std::copy(l.begin(), l.begin() + (ptrdiff_t)inl, hd + kHeadFixed);
+        if (l.size() > h - kHeadFixed) std::copy(l.begin(), l.end(), A.data() + ovf[x]);
     };
     std::atomic<uint64_t> es{0}, ep{0}, nl{0};
     parallel_chunks(ns, 1 << 14, [&](int tid, uint64_t b, uint64_t e) {

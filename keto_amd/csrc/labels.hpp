@@ -32,7 +32,8 @@
 // the non-empty lists):
 //   [count | overflow start / 16 | mask lo | mask hi | entries ascending ... | 0xFFFFFFFF pad]
 // a list of more than head - 4 entries is kept whole at words 16 x (overflow start) (after
-// the heads, in the same array); count = kNoLabel: the request goes to the second stage.
+// the heads, in the same array), its first head - 4 entries also in the head; count =
+// kNoLabel: the request goes to the second stage.
 #pragma once
 
 #include <cstdint>

@@ -177,7 +177,7 @@ def label_list(A, h, x):
     else:
         assert ov * 16 + c <= len(A)
         lst = A[ov * 16: ov * 16 + c]
-        assert np.all(A[base + 4: base + h] == NONE_)
+        np.testing.assert_array_equal(A[base + 4: base + h], lst[: h - 4])  # the prefix, also in the head
     assert np.all(np.diff(lst.astype(np.int64)) > 0)
     return lst, mask
 
