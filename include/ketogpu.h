@@ -452,6 +452,7 @@ typedef struct {
     uint64_t label_bytes;       /* S + P arrays in HBM                                  */
     uint64_t label_entries;     /* Lin + Lout entries                                   */
     uint64_t rest_requests;     /* requests of this run answered by the second stage    */
+    uint64_t full_requests;     /* requests whose overflowing list the dense pass searched */
     double rest_ms;             /* second stage + statistics (events between kernels)   */
     /* plan label on a writable snapshot (label_update: heads rewritten in place per write) */
     uint64_t label_rewritten;   /* heads rewritten after writes                          */

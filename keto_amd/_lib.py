@@ -105,7 +105,8 @@ class RunStats(C.Structure):
         ("closure_entries_b", C.c_uint64), ("core_build_ms", C.c_double), ("label_on", C.c_int32),
         ("label_coverage", C.c_double), ("label_build_ms", C.c_double), ("label_s_head", C.c_uint32),
         ("label_p_head", C.c_uint32), ("label_pll_ms", C.c_double), ("label_bytes", C.c_uint64),
-        ("label_entries", C.c_uint64), ("rest_requests", C.c_uint64), ("rest_ms", C.c_double),
+        ("label_entries", C.c_uint64), ("rest_requests", C.c_uint64), ("full_requests", C.c_uint64),
+        ("rest_ms", C.c_double),
         ("label_rewritten", C.c_uint64), ("label_marked", C.c_uint64), ("label_relabels", C.c_uint64)]
 
     PLANS = {0: "global", 1: "bidi", 2: "v2", 3: "wave", 4: "unit", 5: "lite", 6: "core", 7: "label"}

@@ -2528,19 +2528,17 @@ struct LabelGraph {
 // stage (workgroup 0) clears the other set for the next call.
 constexpr int kRestShards = 64, kRestStride = 32;
 struct LabelRest {
-    uint32_t *list;
+    uint32_t *list;                    // request indices (the rest list)
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
+    uint4 *rec = nullptr;              // the full list: {request, root, target, 0} records
 };
 // A request's two heads in LDS, as read (word k of the head at position k; the entries
 // from word 4), rows of HS + 4 / HP + 4 words: 16-byte aligned, and the 16 requests' rows
 // start in different banks
-// + a scratch row where the wave stages one overflow list at a time (kLabelScratch words)
-constexpr uint32_t kLabelScratch = 512;
 template <int HS, int HP>
 struct alignas(16) LabelShared {
     uint32_t S[16 * (HS + 4)], P[16 * (HP + 4)];
-    uint32_t X[kLabelScratch];
 };
 
 // x among the n ascending entries of a list (LDS or global memory)
@@ -2631,10 +2629,13 @@ __device__ __forceinline__ bool label_find_e(const uint32_t *L, uint32_t x) {
 #define KETO_LABEL_MEET 0
 #endif
 
+// A unit of 16 requests by one wave (four lanes per request), the heads' inline entries
+// only: a request left open with an overflowing list is listed in F for the dense second
+// pass (label_full_kernel), so no wave waits on one request's second read.
 template <int HS, int HP>
 __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelGraph &L, uint32_t r_lane,
                                            uint32_t t_lane, uint64_t *allowed, const uint64_t unit,
-                                           const LabelRest &R, unsigned long long *stats) {
+                                           const LabelRest &R, const LabelRest &F, unsigned long long *stats) {
     static_assert((HS == 8 || HS == 16 || HS == 32) && (HP == 8 || HP == 16 || HP == 32), "heads of 8, 16 or 32 words");
     constexpr int SW = HS / 4, PW = HP / 4;  // head words per lane
     const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
@@ -2659,14 +2660,14 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
     label_to_lds<SW>(Sl, sw, sub);
     label_to_lds<PW>(Pl, pw, sub);
+    const uint32_t shard = (uint32_t)(unit % kRestShards);
     // a request without labels (or with a wildcard root): listed for the second stage
     {
         const bool rest = sub == 0 && some && !labelled;
-        const uint32_t shard = (uint32_t)(unit % kRestShards);
         const uint32_t at = lds_append(rest, R.count + shard * kRestStride);
         if (rest) R.list[shard * R.cap + at] = (uint32_t)(unit * 16 + q);
     }
-    __syncthreads();
+    wave_sync();  // (the images: this wave's own rows)
     bool hit = labelled && (smask & pmask) != 0;
     // 1. the heads' inline entries: whole lists, or the first entries of an overflowing one
     //    (most hits are found there): the shorter walked, round-robin over the request's
@@ -2689,45 +2690,13 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
             hit = label_meet<SW>(Pl + kHeadFixed, ep, c);
         }
     }
-    // 2. a request with an overflowing list and no hit yet: the whole lists, one request at
-    //    a time per wave — the longer list staged in LDS by the whole wave (one dependent
-    //    read, not a chain of them), the shorter walked by the request's lanes
+    // 2. a request with an overflowing list and no hit yet: listed for label_full_kernel
     {
-        uint64_t need = __ballot(labelled && !hit && sub == 0 && (ns > (uint32_t)(HS - kHeadFixed) || np > (uint32_t)(HP - kHeadFixed)));
-        while (need) {  // (wave-uniform)
-            const uint32_t j = (uint32_t)__builtin_ctzll(need) & ~3u;
-            need &= need - 1;
-            const uint32_t nsj = (uint32_t)__builtin_amdgcn_readlane((int)ns, (int)j);
-            const uint32_t npj = (uint32_t)__builtin_amdgcn_readlane((int)np, (int)j);
-            const bool walk_p = npj <= nsj;
-            const uint32_t nw = walk_p ? npj : nsj, nl = walk_p ? nsj : npj;
-            const bool l_over = walk_p ? nsj > (uint32_t)(HS - kHeadFixed) : npj > (uint32_t)(HP - kHeadFixed);
-            const bool w_over = walk_p ? npj > (uint32_t)(HP - kHeadFixed) : nsj > (uint32_t)(HS - kHeadFixed);
-            const uint64_t lg = (uint64_t)(walk_p ? Sg : Pg), wg = (uint64_t)(walk_p ? Pg : Sg);
-            const uint32_t *Lg = (const uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(lg >> 32), (int)j) << 32) |
-                                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lg, (int)j));
-            const uint32_t *Wg = (const uint32_t *)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(wg >> 32), (int)j) << 32) |
-                                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wg, (int)j));
-            const uint32_t q0 = j >> 2;
-            const uint32_t *Ll = walk_p ? sh.S + q0 * (HS + 4) + kHeadFixed : sh.P + q0 * (HP + 4) + kHeadFixed;
-            const uint32_t *Wl = walk_p ? sh.P + q0 * (HP + 4) + kHeadFixed : sh.S + q0 * (HS + 4) + kHeadFixed;
-            const uint32_t *O = Ll;  // where the longer list is searched
-            if (l_over) {
-                if (nl <= kLabelScratch) {  // overflow lists are whole 16-word units: uint4 reads stay inside
-                    for (uint32_t i = lane; i * 4 < nl; i += 64)
-                        reinterpret_cast<uint4 *>(sh.X)[i] = reinterpret_cast<const uint4 *>(Lg)[i];
-                    __syncthreads();
-                    O = sh.X;
-                } else {
-                    O = Lg;
-                }
-            }
-            if (q == q0) {
-                const uint32_t *W = w_over ? Wg : Wl;
-                for (uint32_t k = sub; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
-            }
-            __syncthreads();
-        }
+        const uint64_t hb = __ballot(hit);
+        const bool full = sub == 0 && labelled && !((hb >> (lane & ~3u)) & 0xF) &&
+                          (ns > (uint32_t)(HS - kHeadFixed) || np > (uint32_t)(HP - kHeadFixed));
+        const uint32_t at = lds_append(full, F.count + shard * kRestStride);
+        if (full) F.rec[shard * F.cap + at] = make_uint4((uint32_t)(unit * 16 + q), r, t, 0u);
     }
     uint32_t looked = 0;
     const uint64_t bits = __ballot(hit);
@@ -2750,46 +2719,130 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     }
 }
 
-// the next call's rest counters, cleared by workgroup 0 of the first stage
-__device__ __forceinline__ void label_clear_next(const LabelRest &R) {
-    if (blockIdx.x == 0) R.next_count[threadIdx.x * kRestStride] = 0u;  // 64 lanes: every shard
+// the next call's list counters (rest and full), cleared by wave 0 of workgroup 0
+__device__ __forceinline__ void label_clear_next(const LabelRest &R, const LabelRest &F) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // 64 lanes: every shard
+        R.next_count[threadIdx.x * kRestStride] = 0u;
+        F.next_count[threadIdx.x * kRestStride] = 0u;
+    }
 }
 
 template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t *roots, const uint32_t *targets,
-                                                   uint64_t n, uint64_t *allowed, LabelRest R,
+                                                   uint64_t n, uint64_t *allowed, LabelRest R, LabelRest F,
                                                    unsigned long long *stats, uint64_t unit0) {
     __shared__ LabelShared<HS, HP> sh;
-    if (unit0 == 0) label_clear_next(R);
+    if (unit0 == 0) label_clear_next(R, F);
     const uint64_t units = (n + 15) / 16;
     const uint64_t unit = unit0 + blockIdx.x;
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
-    label_unit<HS, HP>(sh, L, r, t, allowed, unit, R, stats);
+    label_unit<HS, HP>(sh, L, r, t, allowed, unit, R, F, stats);
 }
 
-// pinned host requests read in place (host_unit_requests)
-template <int K, int HS, int HP>
-__global__ __launch_bounds__(64) void label_host_kernel(DevGraph g, LabelGraph L, const uint32_t *hr,
-                                                        const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
-                                                        uint64_t *allowed, LabelRest R, unsigned long long *stats,
-                                                        unsigned long long *first_bad) {
-    __shared__ LabelShared<HS, HP> sh;
-    label_clear_next(R);
-    uint32_t r[K], t[K];
-    host_unit_requests<K>(g, hr, ht, dr, dt, n, first_bad, r, t);
-    const uint64_t units = (n + 15) / 16;
-#pragma unroll 1
-    for (int k = 0; k < K; k++) {
-        const uint64_t unit = (uint64_t)blockIdx.x * K + k;
-        if (unit >= units) break;
-        uint32_t rk = r[0], tk = t[0];
+// pinned host requests read in place: four waves per workgroup, one unit each; wave 0 reads
+// the four units' requests (host_unit_requests: two 256-byte PCIe reads) and hands them over
+// in LDS, so the units' head reads and searches run side by side
+template <int HS, int HP>
+__global__ __launch_bounds__(256) void label_host_kernel(DevGraph g, LabelGraph L, const uint32_t *hr,
+                                                         const uint32_t *ht, uint32_t *dr, uint32_t *dt, uint64_t n,
+                                                         uint64_t *allowed, LabelRest R, LabelRest F,
+                                                         unsigned long long *stats, unsigned long long *first_bad) {
+    __shared__ LabelShared<HS, HP> sh[4];
+    __shared__ uint32_t rq[2][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    label_clear_next(R, F);
+    if (wave == 0) {
+        uint32_t r[4], t[4];
+        host_unit_requests<4>(g, hr, ht, dr, dt, n, first_bad, r, t);
+        if (lane < 16)
 #pragma unroll
-        for (int j = 1; j < K; j++)
-            if (j == k) rk = r[j], tk = t[j];
-        label_unit<HS, HP>(sh, L, rk, tk, allowed, unit, R, stats);
-        __syncthreads();
+            for (int k = 0; k < 4; k++) rq[0][16 * k + lane] = r[k], rq[1][16 * k + lane] = t[k];
     }
+    __syncthreads();
+    const uint64_t units = (n + 15) / 16;
+    const uint64_t unit = (uint64_t)blockIdx.x * 4 + wave;
+    if (unit >= units) return;  // (a whole wave: no barrier follows)
+    const uint32_t rk = lane < 16 ? rq[0][16 * wave + lane] : KETOGPU_NODE_NONE;
+    const uint32_t tk = lane < 16 ? rq[1][16 * wave + lane] : KETOGPU_NODE_NONE;
+    label_unit<HS, HP>(sh[wave], L, rk, tk, allowed, unit, R, F, stats);
+}
+
+// The dense second pass over the requests the first stage left open with an overflowing
+// list (F, request indices): gathered 16 to a wave, four lanes per request, persistent.
+// Each request's heads are read again, its longer list is staged in LDS (up to
+// kFullStage words; one dependent read: the four lanes' loads are independent) and the
+// shorter one walked and binary-searched in it.
+constexpr uint32_t kFullStage = 256;
+// Workgroup 0 also totals both lists' shard counts for the host (totals[0]: the rest list,
+// totals[1]: this list), so the rest stage can be launched only when it has requests.
+template <int HS, int HP>
+__global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *allowed, LabelRest R, LabelRest F,
+                                                        unsigned int *total_rest, unsigned int *total_full,
+                                                        unsigned long long *stats) {
+    __shared__ LabelShared<HS, HP> sh;
+    __shared__ alignas(16) uint32_t stage[16][kFullStage];
+    const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
+    constexpr int SW = HS / 4, PW = HP / 4;
+    const uint32_t c = F.count[lane * kRestStride];
+    const uint32_t nu = (c + 15) / 16;
+    const uint32_t incl = wave_incl_sum_u32(nu);
+    const uint64_t units = (uint64_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (blockIdx.x == 0) {
+        const uint32_t tr = wave_sum_all(R.count[lane * kRestStride]), tf = wave_sum_all(c);
+        if (lane == 0) *total_rest = tr, *total_full = tf;
+    }
+    uint64_t ent = 0;
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint32_t shard = (uint32_t)__builtin_ctzll(__ballot(incl > u));
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)(incl - nu), (int)shard);
+        const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)shard);
+        const uint64_t j = (u - first) * 16 + (lane & 15);
+        uint4 rec = make_uint4(KETOGPU_NODE_NONE, 0, 0, 0);
+        if (lane < 16 && j < cs) rec = F.rec[shard * F.cap + j];
+        const uint32_t idx = (uint32_t)__shfl((int)rec.x, (int)q, 64);
+        const uint32_t rr = (uint32_t)__shfl((int)rec.y, (int)q, 64), tt = (uint32_t)__shfl((int)rec.z, (int)q, 64);
+        const bool valid = idx != KETOGPU_NODE_NONE;
+        uint32_t sw[SW], pw[PW];
+#pragma unroll
+        for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < PW; k++) pw[k] = 0xFFFFFFFFu;
+        if (valid) {
+            label_head_load<SW>(L.S + (uint64_t)tt * HS, sub, sw);
+            label_head_load<PW>(L.P + (uint64_t)rr * HP, sub, pw);
+        }
+        const uint32_t ns = label_word<SW, 0>(sw), np = label_word<PW, 0>(pw);
+        const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw) * 16;
+        const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw) * 16;
+        uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
+        label_to_lds<SW>(Sl, sw, sub);
+        label_to_lds<PW>(Pl, pw, sub);
+        const bool walk_p = np <= ns;
+        const uint32_t nw = walk_p ? np : ns, nl = walk_p ? ns : np;
+        const bool l_over = walk_p ? ns > (uint32_t)(HS - kHeadFixed) : np > (uint32_t)(HP - kHeadFixed);
+        const bool w_over = walk_p ? np > (uint32_t)(HP - kHeadFixed) : ns > (uint32_t)(HS - kHeadFixed);
+        const uint32_t *Lg = walk_p ? Sg : Pg, *Wg = walk_p ? Pg : Sg;
+        // the longer list: staged from its overflow region (whole 16-word units: the uint4
+        // reads stay inside), else its head image
+        if (valid && l_over && nl <= kFullStage)
+            for (uint32_t i = sub; i * 4 < nl; i += 4)
+                reinterpret_cast<uint4 *>(stage[q])[i] = reinterpret_cast<const uint4 *>(Lg)[i];
+        wave_sync();
+        const uint32_t *O = !l_over ? (walk_p ? Sl : Pl) + kHeadFixed : nl <= kFullStage ? stage[q] : Lg;
+        const uint32_t *W = w_over ? Wg : (walk_p ? Pl : Sl) + kHeadFixed;
+        bool hit = false;
+        if (valid)
+            for (uint32_t k = sub; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
+        const uint64_t bits = __ballot(hit);
+        if (valid && sub == 0) {
+            if ((bits >> lane) & 0xF) atomicOr((unsigned long long *)&allowed[idx >> 6], 1ull << (idx & 63));
+            ent += nl;  // the longer list read once more (u32 entries)
+        }
+        wave_sync();  // (the LDS rows are rewritten by the next unit)
+    }
+    const uint32_t e = wave_sum_all((uint32_t)ent);
+    if (lane == 0 && e) atomicAdd(&stat_slot(stats)[2], (unsigned long long)e);
 }
 
 // the second stage: plan lite's traversal over the requests the labels did not answer
@@ -4056,7 +4109,7 @@ struct ketogpu_engine {
     // them: every request but wildcard roots is one intersection)
     bool use_label = false;
     LabelGraph lgraph{};
-    unsigned int *rest_counts = nullptr;  // two sets of kRestShards counters, one cache line each
+    unsigned int *rest_counts = nullptr;  // rest and full lists: two sets each of kRestShards counters, one cache line each
     uint64_t label_calls = 0;             // selects the set
     LabelRest label_rest(uint64_t n) {    // this call's rest list over requests [0, n)
         const uint64_t units = (n + 15) / 16;
@@ -4064,6 +4117,15 @@ struct ketogpu_engine {
         return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
                          rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
     }
+    LabelRest label_full(uint64_t n) {  // this call's list for label_full_kernel (records)
+        const uint64_t units = (n + 15) / 16;
+        const unsigned set = 2 + (unsigned)(label_calls & 1);
+        return LabelRest{nullptr, rest_counts + set * kRestShards * kRestStride,
+                         rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards),
+                         full_rec};
+    }
+    uint4 *full_rec = nullptr;  // plan label's full list: {request, root, target, 0} per request (spill_cap)
+    uint64_t full_prev = 1024 * 16;  // the previous call's full-list requests (the pass's grid)
     uint32_t label_hs = 16, label_hp = 8;  // head words of S and P
     double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
     uint64_t label_bytes = 0, label_entries = 0;
@@ -4090,9 +4152,9 @@ struct ketogpu_engine {
     // plan label, host batches (4 units per workgroup)
     void launch_label_host(const Batch &q, const HostSrc *src, uint64_t bunits) {
         label_dispatch([&](auto hs, auto hp) {
-            KLAUNCH((label_host_kernel<4, decltype(hs)::value, decltype(hp)::value>), dim3((unsigned)((bunits + 3) / 4)),
-                    dim3(64), 0, stream, g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n,
-                    q.allowed, label_rest(q.n), st.stats, d_bad);
+            KLAUNCH((label_host_kernel<decltype(hs)::value, decltype(hp)::value>), dim3((unsigned)((bunits + 3) / 4)),
+                    dim3(256), 0, stream, g, lgraph, src->roots, src->targets, io->d_roots, io->d_targets, q.n,
+                    q.allowed, label_rest(q.n), label_full(q.n), st.stats, d_bad);
         });
     }
     int core_shape = 2;  // KETOGPU_CORE_SHAPE: 0 = LiteShape, 1 = CoreShapeS, 2 = CoreShapeM (default: 0.195 vs 0.221 ms per 10^6 config #2 requests, profiles/r04/ab_shape)
@@ -4144,7 +4206,7 @@ struct ketogpu_engine {
         if (c.lite == 3) {  // plan label: 2-hop labels, plan lite for requests without
             label_dispatch([&](auto hs, auto hp) {
                 KLAUNCH((label_kernel<decltype(hs)::value, decltype(hp)::value>), dim3(grid), dim3(64), pad, stream,
-                        lgraph, q.roots, q.targets, q.n, q.allowed, label_rest(q.n), stats, unit0);
+                        lgraph, q.roots, q.targets, q.n, q.allowed, label_rest(q.n), label_full(q.n), stats, unit0);
             });
             return;
         }
@@ -4556,7 +4618,7 @@ struct ketogpu_engine {
         if (wait_ev) (void)hipEventDestroy(wait_ev);
         for (void *p : owned) (void)hipFree(p);
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
-                        (void *)spill_flags})
+                        (void *)spill_flags, (void *)full_rec})
             if (p) (void)hipFree(p);
         if (h_ctr) (void)hipHostFree(h_ctr);
         if (h_res) (void)hipHostFree(h_res);
@@ -5061,9 +5123,9 @@ struct ketogpu_engine {
             return;
         }
         if (!rest_counts) {
-            rest_counts = dalloc<unsigned int>(2 * kRestShards * kRestStride);
+            rest_counts = dalloc<unsigned int>(4 * kRestShards * kRestStride);
             owned.push_back(rest_counts);
-            HIP_CHECK(hipMemset(rest_counts, 0, 2 * kRestShards * kRestStride * sizeof(unsigned int)));
+            HIP_CHECK(hipMemset(rest_counts, 0, 4 * kRestShards * kRestStride * sizeof(unsigned int)));
         }
         lgraph = LabelGraph{A[1], A[0]};
         if (s.writable) {
@@ -5231,7 +5293,9 @@ struct ketogpu_engine {
             if (p) (void)hipFree(p);
         // (+ 2048: plan label's sharded rest list rounds every shard's region up to whole units)
         spill_cap = std::max<uint64_t>(n + 2048, 1024);
-        spill_units = dalloc<uint32_t>(2 * spill_cap);
+        spill_units = dalloc<uint32_t>(2 * spill_cap);  // two ping-pong lists
+        if (full_rec) (void)hipFree(full_rec);
+        full_rec = dalloc<uint4>(spill_cap);
         spill_roots = dalloc<uint32_t>(spill_cap);
         spill_targets = dalloc<uint32_t>(spill_cap);
         spill_allowed = dalloc<uint64_t>(spill_cap / 64 + 1);
@@ -5283,6 +5347,16 @@ struct ketogpu_engine {
             u_prev = 1;
         }
         const int cur = (int)(stages.size() & 1);  // the list the last stage writes
+        // plan label: the dense pass over the requests with an overflowing list, always (it
+        // also totals the rest list for the lazy decision below: spill_count[0]); persistent,
+        // its grid from the previous call's count
+        if (bidi_cfg.lite == 3)
+            label_dispatch([&](auto hs, auto hp) {
+                const unsigned fg = (unsigned)std::min<uint64_t>(std::max<uint64_t>(full_prev / 16 + 64, 64), 16384);
+                KLAUNCH((label_full_kernel<decltype(hs)::value, decltype(hp)::value>), dim3(fg), dim3(64), 0, stream,
+                        lgraph, q.allowed, label_rest(q.n), label_full(q.n), &spill_count[0], &spill_count[7],
+                        st.stats + 4 * kStatSlots);
+            });
         auto launch_stages = [&](uint64_t prev0) {
             for (size_t k = 0, c = 0; k < stages.size(); k++, c ^= 1)
                 launch_stage(stages[k], q, list[c], &spill_count[k], fans[k], list[c ^ 1], &spill_count[k + 1],
@@ -5294,8 +5368,8 @@ struct ketogpu_engine {
         // shows spills, followed by a second statistics pass, the result copies again and a
         // second synchronization.  KETOGPU_CASCADE_EAGER=1: always up front (A/B).
         static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
-        // (plan label: its second stage always runs — it totals the sharded rest counts)
-        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0 && bidi_cfg.lite != 3;
+        // (plan label: the rest stage as lazily — label_full_kernel totals the rest list)
+        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0;
         if (!lazy) launch_stages(stage_prev[0]);
         // b == nullptr (host batches): no event between the call's kernels (each costs ~6 us of
         // GPU idle between the launches it separates); one event after the last launch
@@ -5342,7 +5416,11 @@ struct ketogpu_engine {
             fprintf(stderr, "\n");
         }
         for (size_t k = 0; k < ns; k++) rs.spilled_units += cnt[k];
-        if (bidi_cfg.lite == 3) rs.rest_requests = cnt[0];
+        if (bidi_cfg.lite == 3) {
+            rs.rest_requests = cnt[0];
+            rs.full_requests = cnt[7];
+            full_prev = cnt[7];
+        }
         for (size_t k = 0; k < stages.size() && k < 8; k++) stage_prev[k] = (uint64_t)cnt[k] * fans[k];
         rs.push_launches += launched;
         rs.unit_launches += launched;

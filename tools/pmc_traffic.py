@@ -27,6 +27,7 @@ FAMILIES = [
     # plan label: closure labels (one intersection per request)
     ("label_host_kernel (host batches)", r"label_host_kernel"),
     ("label_rest_kernel (second stage)", r"label_rest_kernel"),
+    ("label_full_kernel (overflow lists)", r"label_full_kernel"),
     ("label_kernel", r"\blabel_kernel"),
     # plan core: lite over the core arrays with closure rows (template argument CL = true)
     ("core lite_host_kernel (host batches)", r"lite_host_kernel<.*, true>"),
