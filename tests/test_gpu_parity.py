@@ -428,3 +428,8 @@ def test_label_device_build_equals_host(graph, heads, monkeypatch):
         assert (hs_dev, hp_dev) == (li["s_head_words"], li["p_head_words"])
         np.testing.assert_array_equal(S, li["S"])
         np.testing.assert_array_equal(P, li["P"])
+    # one 2-hop label build per snapshot (labels.cpp reach_labels_of): the engines report the
+    # same build (its time), which the host hook's own build does not share
+    pll = [e.check_ids(np.zeros(1, np.uint32), np.zeros(1, np.uint32)) is not None and e.last_stats()["label_pll_ms"]
+           for e in engines]
+    assert pll[0] == pll[1] > 0
