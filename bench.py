@@ -214,13 +214,19 @@ def main():
     q = eng0.upload(roots[b0:e0], targets[b0:e0])
     for _ in range(a.warmup + 1):
         q.run()
-    runs = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         q.run()
-        runs.append(eng0.last_stats())
     dt_res = time.perf_counter() - t0
     assert np.array_equal(q.download(), allowed[b0:e0])
+    # the kernels' own times: the same runs again with a timing event between the call's
+    # kernels (each event idles the GPU a few microseconds: not the rate above)
+    eng0.set_events(True)
+    runs = []
+    for _ in range(a.steps):
+        q.run()
+        runs.append(eng0.last_stats())
+    eng0.set_events(False)
     st = runs[-1]
 
     out_line = None

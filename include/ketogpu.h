@@ -460,10 +460,11 @@ typedef struct {
     uint64_t label_relabels;    /* rebuilds from the current rows                        */
 } ketogpu_run_stats;
 int ketogpu_engine_last_stats(const ketogpu_engine *e, ketogpu_run_stats *out);
-/* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory) record a
- * timing event between the call's kernels, so last_stats' main_ms is the first stage's own
- * device time (each event pair costs a few microseconds of idle GPU between the launches);
- * 0 (default): one event pair around the whole call (KETOGPU_EVENTS=all sets 1 at creation) */
+/* every_kernel = 1: host-to-host batches (ketogpu_check_ids from pinned memory), and plan
+ * label's device-resident batches, record a timing event between the call's kernels, so
+ * last_stats' main_ms is the first stage's own device time (each event pair costs a few
+ * microseconds of idle GPU between the launches); 0 (default): one event pair around the
+ * whole call (KETOGPU_EVENTS=all sets 1 at creation) */
 int ketogpu_engine_set_events(ketogpu_engine *e, int every_kernel);
 
 /* Upload the device rows patched by ketogpu_snapshot_write since the engine's last sync

@@ -4390,7 +4390,7 @@ struct ketogpu_engine {
     // plan's: 4 for plan label — its units are short, so its PCIe reads bound the launch and
     // wider ones pay (0.172 vs 0.204 ms per 10^6 requests, profiles/r04/ab_label2..5) — else 2)
     int host_units = 0;
-    bool light_events = true;           // host batches: timing events only around the whole call
+    bool light_events = true;           // timing events only around the whole call (host and device batches)
     hipEvent_t light_begin = nullptr;   // that call's begin event (run_once -> run_units)
     uint64_t *h_res = nullptr;            // pinned: a run's result words, flag words, verdict
     EmitReq emit_req;                     // host batch: emit launched with the statistics reduction
@@ -5515,7 +5515,7 @@ struct ketogpu_engine {
                 const bool direct = src && src->mapped && pipe_direct &&
                                     (bidi_cfg == BidiCfg{9, 64, KETO_F1, 7, 16, 1} || bidi_cfg.lite);
                 // (the chunk pipeline's other streams wait for an event after the clear)
-                const bool light = direct && light_begin;
+                const bool light = light_begin && (direct || !src);
                 hipEvent_t a = light ? light_begin : ev(), b = light ? nullptr : ev();
                 if (!light) HIP_CHECK(hipEventRecord(a, stream));
                 const uint64_t bunits = (q.n + bidi_cfg.u - 1) / bidi_cfg.u;
@@ -5880,7 +5880,7 @@ struct ketogpu_engine {
         // host batches: the run's begin event ahead of the clear launch (no event between
         // the call's kernels, KETOGPU_EVENTS=all restores them)
         light_begin = nullptr;
-        if (src && light_events) {
+        if (light_events && (src || (use_units && !wave_u && use_bidi && q.n && bidi_cfg.lite == 3))) {
             HIP_CHECK(hipEventRecord(t_begin, stream));
             light_begin = t_begin;
         }

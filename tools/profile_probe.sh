@@ -19,6 +19,7 @@ echo "[probe] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 tools/label_probe.py --load "$SNAP" --host > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
 python3 tools/timeline.py "$OUT/trace" --calls 2 > "$OUT/timeline.txt" 2>&1 || true
+python3 tools/timeline.py "$OUT/trace" --calls 2 --match "label_kernel<" > "$OUT/timeline_resident.txt" 2>&1 || true
 for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
          "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD" \
          "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES"; do

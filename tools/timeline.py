@@ -1,6 +1,6 @@
 """Timeline of host-to-host check calls from a rocprofv3 trace (kernel + memory copy).
 
-    python tools/timeline.py gpurun_out/<dir>/trace [--calls 2]
+    python tools/timeline.py gpurun_out/<dir>/trace [--calls 2] [--match label_kernel]
 
 Reads *kernel_trace.csv and *memory_copy_trace.csv, groups activity into calls (idle gaps
 of more than 200 us separate them) and prints, for the last --calls host-to-host calls (a
@@ -60,7 +60,11 @@ def main():
         last_end = max(last_end or 0, e[1])
     if cur:
         calls.append(cur)
-    piped = [c for c in calls if any(", 1>" in e[3] or "_host_kernel" in e[3] for e in c)]
+    if "--match" in sys.argv:  # calls with a kernel whose name contains this (e.g. label_kernel: HBM-resident runs)
+        m = sys.argv[sys.argv.index("--match") + 1]
+        piped = [c for c in calls if any(m in e[3] for e in c)]
+    else:
+        piped = [c for c in calls if any(", 1>" in e[3] or "_host_kernel" in e[3] for e in c)]
     if "--first" in sys.argv:  # the earliest host-to-host calls (the bench's timed steps)
         piped = piped[:ncalls + 2]
     for c in piped[-ncalls:]:
