@@ -73,6 +73,7 @@ def main():
     p.add_argument("--tuples", type=int, default=50_000_000)
     p.add_argument("--sizes", default="1,10,100,1000,10000")
     p.add_argument("--sample", type=int, default=100_000)
+    p.add_argument("--nest", type=int, default=20, help="nesting rows written last (the interior graph changes)")
     a = p.parse_args()
     f = a.tuples / 50e6
     w = synth.rbac(users=int(10e6 * f), groups=int(100e3 * f), docs=int(2e6 * f), tuples=a.tuples, checks=1_000_000,
@@ -134,6 +135,39 @@ def main():
         written += ins + dele
         out.setdefault("writes", []).append(entry)
         log(f"write {entry}")
+
+    # checks after the writes: the writable engine keeps its plan (label: heads rewritten in place)
+    st = ew.last_stats()
+    out["after_writes"] = {"rows_written": len(written), "plan": st["plan"],
+                           "writable_host": round(timed_host(ew, wroots, wtargets)),
+                           "writable_hbm": round(timed_hbm(ew, wroots, wtargets)),
+                           "label_rewritten": st["label_rewritten"], "label_marked": st["label_marked"],
+                           "label_relabels": st["label_relabels"]}
+    log(f"after the writes: {out['after_writes']}")
+    if a.nest:  # nesting edges between existing groups: changes the interior graph
+        gcols = w.columns
+        kind, ns = gcols["subject_kind"], gcols["namespace_id"]
+        sets = np.flatnonzero((ns == 1) & (kind == 1))
+        pick = sets[rng.integers(0, len(sets), size=2 * a.nest)]
+        sv = lambda c, i: bytes(gcols[c + "_data"][gcols[c + "_off"][i]:gcols[c + "_off"][i + 1]]).decode()
+        # a parent that already nests a group gets another existing nested group (both interior)
+        ins = [(1, sv("object", pick[2 * k]), "member", None, 1, sv("ss_object", pick[2 * k + 1]), "member")
+               for k in range(a.nest)]
+        res = wsnap.write(ins, [])
+        t1 = time.perf_counter()
+        sync_ms, rows = ew.sync() if res["applied"] else (0.0, 0)
+        entry = {"nest_rows": a.nest, "applied": res["applied"], "reason": res["reason"],
+                 "write_ms": round(res["seconds"] * 1e3, 3), "sync_ms": round(sync_ms, 3),
+                 "total_ms": round(res["seconds"] * 1e3 + (time.perf_counter() - t1) * 1e3, 3)}
+        if res["applied"]:
+            batches.append((ins, []))
+            written += ins
+            h = timed_host(ew, wroots, wtargets)
+            st = ew.last_stats()
+            entry.update(writable_host_after=round(h), plan=st["plan"], label_marked=st["label_marked"],
+                         label_relabels=st["label_relabels"], rest_requests=st["rest_requests"])
+        out["nest_write"] = entry
+        log(f"nesting write {entry}")
 
     # the rebuild path on the compact snapshot, and the cross-check
     t0 = time.time()
