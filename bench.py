@@ -424,11 +424,14 @@ def main_partitioned(a, rank, world, local):
         log(f"core gathered: {core_info}")
         eng = TieredEngine(sh, device=local, core=core, comm=ncomm)
         mine = slice(rank * per_gpu, (rank + 1) * per_gpu)  # this rank's own requests
-        pinned = (check.pinned(roots[mine]), check.pinned(targets[mine]))
+        # resident in HBM when the timed region starts (read in place by every pass)
+        dev_req = [torch.from_numpy(np.ascontiguousarray(x[mine]).view(np.int32)).to(f"cuda:{local}")
+                   for x in (roots, targets)]
+        torch.cuda.synchronize()
         bits = np.zeros((per_gpu + 63) // 64, dtype=np.uint64)
 
         def step():
-            eng.check_ids_raw(pinned[0].array, pinned[1].array, bits)
+            eng.check_ids_ptr(dev_req[0].data_ptr(), dev_req[1].data_ptr(), per_gpu, bits)
     else:
         # requests in pinned host memory, as for the replicated line (ketogpu_part_begin
         # copies them to HBM by DMA); every rank passes the whole batch
@@ -451,7 +454,12 @@ def main_partitioned(a, rank, world, local):
         st1 = eng.stats()
         d = {k: st1[k] - st0[k] for k in ("rows_opened", "records_read", "eval_kernel_ms", "eval_kernel_launches")}
         launches = max(d["eval_kernel_launches"], 1)
-        bytes_launch = (16 * d["rows_opened"] + 16 * d["records_read"]) / launches + 8 * per_gpu + per_gpu / 8
+        tier_label = bool(st1["label"])
+        if tier_label:  # list words (4 B; masks included), request ids, answer bits, list bounds
+            per_req = 16 if ncomm is not None else 32  # received-list bounds, or the own lists' offsets
+            bytes_launch = 4 * d["records_read"] / launches + (8 + per_req) * per_gpu + per_gpu / 8
+        else:
+            bytes_launch = (16 * d["rows_opened"] + 16 * d["records_read"]) / launches + 8 * per_gpu + per_gpu / 8
         ms_launch = d["eval_kernel_ms"] / launches
         achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
         fam = None
@@ -482,7 +490,8 @@ def main_partitioned(a, rank, world, local):
     if rank == 0:
         if tier:
             traffic, traffic_note = None, "no PMC summary for this workload"
-            tpath = os.path.join(ROOT, "profiles", "r04", f"traffic_config5_x{f:g}.json")
+            kname = "tier_label_kernel" if tier_label else "tier_eval_kernel"
+            tpath = os.path.join(ROOT, "profiles", "r05", f"traffic_config5_x{f:g}.json")
             if os.path.exists(tpath):  # tools/profile.sh with WORKLOAD=config5_partitioned_x<scale>
                 try:
                     tr = json.load(open(tpath))
@@ -492,16 +501,19 @@ def main_partitioned(a, rank, world, local):
                         traffic_note = (f"stale: {os.path.relpath(tpath, ROOT)} was profiled at kernel sources "
                                         f"{tr.get('source_hash')}, HEAD is {kernel_source_hash()}")
                     else:
-                        traffic = tr.get("kernels", {}).get("tier_eval_kernel", {}).get("hbm_bytes_per_launch")
+                        traffic = tr.get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch")
                         traffic_note = f"{os.path.relpath(tpath, ROOT)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
                 except (OSError, ValueError):
                     traffic_note = "unreadable PMC summary"
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "traffic_source": traffic_note, "kernel": "tier_eval_kernel",
+                    "traffic_source": traffic_note, "kernel": kname,
                     "bytes_per_launch": int(bytes_launch), "ms_per_launch": round(ms_launch, 4),
                     "measured": "hipEvents around the first evaluation stage on the engine's stream, every timed step",
-                    "bytes_formula": "16*rows_opened + 16*records_read + 8*requests + requests/8 (as the replicated "
+                    "bytes_formula": ("4*list words read (masks included) + 8*requests + requests/8 + 16*requests "
+                                      "(received-list bounds; 32 at world 1 without exchange: the own lists' offsets)")
+                                     if tier_label else
+                                     "16*rows_opened + 16*records_read + 8*requests + requests/8 (as the replicated "
                                      "line's lite kernel)"}
         else:
             dominant = max(fam, key=lambda k: fam[k]["ms"])
@@ -529,7 +541,8 @@ def main_partitioned(a, rank, world, local):
                "data": "synthetic: config #5 RBAC-shape stream generator (keto_amd/csrc/synth.cpp ks_c5), seed 0x4B45544F",
                "config": {"workload": f"config5_partitioned_x{f:g}", **sizes, "checks": n_req,
                           "mode": ("hash-partitioned graph (partition-aware loader), two-tier: core on every rank, "
-                                   "seed rows exchanged, each rank its own requests") if tier else
+                                   + ("2-hop label lists of the seed nodes exchanged (plan label)" if tier_label else
+                                      "seed rows exchanged") + ", each rank its own requests, HBM-resident") if tier else
                                   "hash-partitioned graph (partition-aware loader), native per-level exchange",
                           "parallelism": f"partition x{world}"},
                "roofline": roof, "cpu_baseline": cpu, "parity": parity,

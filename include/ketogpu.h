@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define KETOGPU_ABI_VERSION 8 /* 8: 2-hop reachability labels (plan label), run stats
+#define KETOGPU_ABI_VERSION 9 /* 9: plan label in the two-tier mode (tier stats label_*);
+                                 8: 2-hop reachability labels (plan label), run stats
                                     label_* / rest_*;
                                  7: two-tier partitioned mode (ketogpu_core_*, ketogpu_tier_*);
                                  6: partitioned rounds behind the C ABI (comm, part_engine);
@@ -770,6 +771,8 @@ int ketogpu_part_engine_new_steps(const ketogpu_part_steps *steps, ketogpu_comm 
  *   queries  request i asks owner(r) for fint(r) and owner(t) for rev(t)  [all-to-all]
  *   replies  the owners send those rows                                     [all-to-all]
  *   evaluate the bidirectional LDS unit of the single-GPU engine over the local core
+ * (plan label, the default: the owners reply with their nodes' 2-hop label lists instead
+ * and the evaluation is one list intersection per request)
  * A world of one rank reads its own rows in place (no exchange at all).  Unlike
  * ketogpu_part_check_ids, every rank passes ITS OWN requests (any number, 0 included)
  * and gets the answers to them; the call is collective (every rank calls it for each of
@@ -819,12 +822,20 @@ typedef struct {
     uint64_t core_records, seed_records; /* device records: core (both directions), own rows */
     double eval_kernel_ms;               /* hipEvent time of the first evaluation stage      */
     uint64_t eval_kernel_launches;
+    /* plan label (KETOGPU_TIER_LABEL=0 at ketogpu_tier_new: off): owners answer a query with
+     * the node's label list (masks + entries) instead of its row, and the evaluation is one
+     * intersection per request (no later stage, no per-level fallback).  rows_opened: 2 per
+     * request, records_read: list words read */
+    uint64_t label;                      /* 1: plan label                                    */
+    uint64_t label_words;                /* this rank's S and P list words (masks included)  */
+    double label_build_ms;               /* labels of the core + the owned lists             */
 } ketogpu_tier_stats;
 /* the shard and core stay owned by the caller; the tier borrows s, core and comm */
 int ketogpu_tier_new(const ketogpu_shard *s, const ketogpu_core *core, ketogpu_comm *comm,
                      const ketogpu_tier_opts *opts, ketogpu_tier **out);
-/* this rank's n requests (host memory; pinned buffers are read in place at world 1) ->
- * ceil(n/64) words of answer bits.  An id outside the layout fails the call with
+/* this rank's n requests (host memory — pinned buffers are read in place — or the tier
+ * device's memory, read in place by every pass) -> ceil(n/64) words of answer bits (host
+ * memory).  An id outside the layout fails the call with
  * KETOGPU_EINVAL on that rank (its peers fail with the same code). */
 int ketogpu_tier_check_ids(ketogpu_tier *t, const uint32_t *roots, const uint32_t *targets, size_t n,
                            uint64_t *allowed_bits);

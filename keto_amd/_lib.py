@@ -278,7 +278,8 @@ class TierStats(C.Structure):
         "calls", "batches", "requests", "overflow_requests", "fallback_calls", "queries_sent", "records_sent",
         "records_received", "collectives", "rows_opened", "records_read")] + [
         ("exchange_ms", C.c_double), ("evaluate_ms", C.c_double), ("core_records", C.c_uint64),
-        ("seed_records", C.c_uint64), ("eval_kernel_ms", C.c_double), ("eval_kernel_launches", C.c_uint64)]
+        ("seed_records", C.c_uint64), ("eval_kernel_ms", C.c_double), ("eval_kernel_launches", C.c_uint64),
+        ("label", C.c_uint64), ("label_words", C.c_uint64), ("label_build_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -2655,8 +2655,6 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
     const uint64_t smask = (uint64_t)label_word<SW, 2>(sw) | (uint64_t)label_word<SW, 3>(sw) << 32;
     const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw) | (uint64_t)label_word<PW, 3>(pw) << 32;
-    const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw) * 16;  // overflow lists
-    const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw) * 16;
     uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
     label_to_lds<SW>(Sl, sw, sub);
     label_to_lds<PW>(Pl, pw, sub);
@@ -3305,6 +3303,11 @@ __device__ __forceinline__ void tier_row(const tier::Graph &G, const tier::Query
         bad = true;
         return;
     }
+    if (G.label) {  // label mode: the node's S / P list (masks, then entries)
+        const uint64_t *o = (q.tag & 1u) ? G.ls_off : l < G.Nxl ? G.lp_off : nullptr;
+        if (o) b = o[l], e = o[l + 1];
+        return;
+    }
     if (q.tag & 1u) {
         b = G.lr_off[l];
         e = G.lr_off[l + 1];
@@ -3469,6 +3472,169 @@ __global__ __launch_bounds__(kTB) void tier_seed_kernel(tier::Graph G, const tie
             uint32_t *b = reinterpret_cast<uint32_t *>(&bnd[i]) + 2 * (tag & 1u);
             if (prev != tag) b[0] = (uint32_t)k;
             if (next != tag) b[1] = (uint32_t)(k + 1);
+        }
+    }
+}
+
+// Label mode replies (tier.hpp "label replies"): a destination's segment is the lengths of
+// the lists it asked for, in its query order, then the lists themselves, 4-byte words.
+// seg(k): the segment of query k, given the segments' first queries (world + 1 entries)
+__device__ __forceinline__ uint32_t tier_seg(const uint64_t *first, uint32_t world, uint64_t k) {
+    uint32_t lo = 0, hi = world;  // the last p with first[p] <= k
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (first[mid] <= k)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// The owner's side: query j of segment p (qs: the received segments' first queries, off:
+// the lists' lengths scanned over all received queries) writes its length at
+// j + off[qs[p]] and its list at qs[p + 1] + off[j] — the segment layout above, with no
+// per-segment pass.  One wave per 64 queries, lanes over consecutive words (like
+// tier_reply_copy_kernel).
+__global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
+                                                               const uint64_t *off, const uint64_t *qs, uint32_t world,
+                                                               uint32_t *out, uint64_t cap) {
+    __shared__ uint64_t s_pre[kTB / 64][65];
+    __shared__ uint64_t s_src[kTB / 64][64];
+    __shared__ uint64_t s_dst[kTB / 64][64];
+    __shared__ uint32_t s_side[kTB / 64][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t j0 = ((uint64_t)blockIdx.x * (kTB / 64) + wv) * 64; j0 < n; j0 += (uint64_t)gridDim.x * kTB) {
+        const uint64_t j = j0 + lane;
+        uint64_t b = 0, e = 0, dst = 0;
+        uint32_t side = 0;
+        if (j < n) {
+            bool miss;
+            const tier::Query qq = q[j];
+            tier_row(G, qq, b, e, miss);
+            side = qq.tag & 1u;
+            const uint32_t p = tier_seg(qs, world, j);
+            const uint64_t h = j + off[qs[p]];
+            if (h < cap) out[h] = (uint32_t)(e - b);
+            dst = qs[p + 1] + off[j];
+        }
+        const uint64_t o0 = off[j0];
+        s_pre[wv][lane] = (j < n ? off[j] : off[n]) - o0;
+        s_src[wv][lane] = b;
+        s_dst[wv][lane] = dst;
+        s_side[wv][lane] = side;
+        const uint64_t total = (j0 + 64 < n ? off[j0 + 64] : off[n]) - o0;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (uint64_t o = lane; o < total; o += 64) {
+            int lo = 0, hi = 64;  // the last query whose offset is <= o owns it (empty lists never win)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_pre[wv][mid] <= o)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const uint64_t w = o - s_pre[wv][lo];
+            const uint32_t *src = s_side[wv][lo] ? G.ls_col : G.lp_col;
+            const uint64_t d = s_dst[wv][lo] + w;
+            if (d < cap) out[d] = src[s_src[wv][lo] + w];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// The asker's side: the length of the list its k-th sent query got back (sq: its sent
+// segments' first queries, rp: the received segments' first words)
+__global__ __launch_bounds__(kTB) void tier_label_lens_kernel(const uint32_t *recv, uint64_t nsent, const uint64_t *sq,
+                                                              const uint64_t *rp, uint32_t world, uint64_t *lens) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kTB + threadIdx.x; k < nsent; k += (uint64_t)gridDim.x * kTB) {
+        const uint32_t p = tier_seg(sq, world, k);
+        lens[k] = recv[rp[p] + (k - sq[p])];
+    }
+}
+
+// ... and with the lengths scanned (g), each list's bounds: it starts at sq[p + 1] + g[k]
+// (the same layout seen from the asker), for request tag >> 1, side tag & 1
+__global__ __launch_bounds__(kTB) void tier_label_bounds_kernel(const tier::Query *sent, uint64_t nsent,
+                                                                const uint64_t *sq, const uint64_t *g, uint32_t world,
+                                                                uint4 *bnd, uint64_t nreq) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kTB + threadIdx.x; k < nsent; k += (uint64_t)gridDim.x * kTB) {
+        const uint32_t p = tier_seg(sq, world, k);
+        const uint32_t tag = sent[k].tag;
+        const uint64_t i = tag >> 1;
+        if (i >= nreq) continue;
+        const uint64_t b = sq[p + 1] + g[k];
+        reinterpret_cast<uint2 *>(&bnd[i])[tag & 1u] = make_uint2((uint32_t)b, (uint32_t)(b + (g[k + 1] - g[k])));
+    }
+}
+
+// Label mode evaluation: one wave per 16 requests, four lanes per request.  Both lists'
+// first kTierLab words go to LDS; the masks decide first, then the shorter list's entries
+// (round-robin over the four lanes) are binary-searched in the longer one (LDS when it fits,
+// else where it lies).  DIRECT: world 1, the lists read in place.
+constexpr uint32_t kTierLab = 64;
+template <bool DIRECT>
+__global__ __launch_bounds__(64) void tier_label_kernel(tier::Graph G, tier::Eval E, const uint32_t *recv) {
+    __shared__ uint32_t L[16][2][kTierLab];
+    const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
+    const uint64_t c = (uint64_t)blockIdx.x * 16 + q;
+    uint32_t r, t;
+    tier_request(G, E, c, r, t);
+    const uint32_t *lp = nullptr, *ls = nullptr;
+    uint32_t np = 0, ns = 0;
+    if (r != KETOGPU_NODE_NONE) {
+        if constexpr (DIRECT) {
+            const uint32_t lr = tier_local(G, r), lt = tier_local(G, t);
+            if (lr != KETOGPU_NODE_NONE && lr < G.Nxl) {
+                const uint64_t b = G.lp_off[lr];
+                lp = G.lp_col + b;
+                np = (uint32_t)(G.lp_off[lr + 1] - b);
+            }
+            if (lt != KETOGPU_NODE_NONE) {
+                const uint64_t b = G.ls_off[lt];
+                ls = G.ls_col + b;
+                ns = (uint32_t)(G.ls_off[lt + 1] - b);
+            }
+        } else {
+            const uint4 b = E.bnd[c];
+            lp = recv + b.x;
+            np = b.y - b.x;
+            ls = recv + b.z;
+            ns = b.w - b.z;
+        }
+    }
+    for (uint32_t j = sub; j < min(np, kTierLab); j += 4) L[q][0][j] = lp[j];
+    for (uint32_t j = sub; j < min(ns, kTierLab); j += 4) L[q][1][j] = ls[j];
+    __syncthreads();
+    bool hit = false;
+    const bool valid = np >= 2 && ns >= 2;
+    if (valid) {
+        const uint64_t pm = L[q][0][0] | (uint64_t)L[q][0][1] << 32, sm = L[q][1][0] | (uint64_t)L[q][1][1] << 32;
+        hit = (pm & sm) != 0;
+        // walk A (the shorter), search B
+        const bool a_p = np <= ns;
+        const uint32_t na = (a_p ? np : ns) - 2, nb = (a_p ? ns : np) - 2;
+        const uint32_t *A = a_p ? &L[q][0][0] : &L[q][1][0], *B = a_p ? &L[q][1][0] : &L[q][0][0];
+        const uint32_t *Ag = a_p ? lp : ls, *Bg = a_p ? ls : lp;
+        for (uint32_t k = sub; k < na && !hit; k += 4) {
+            const uint32_t x = k + 2 < kTierLab ? A[k + 2] : Ag[k + 2];
+            hit = label_find_n(nb + 2 <= kTierLab ? B + 2 : Bg + 2, nb, x);
+        }
+    }
+    const uint64_t hb = __ballot(hit);
+    uint64_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) bits |= ((hb >> (4 * k)) & 0xFull) ? (1ull << k) : 0ull;
+    const uint64_t vb = __ballot(valid && sub == 0);
+    uint32_t ent = sub == 0 ? np + ns : 0;
+    for (int o = 32; o; o >>= 1) ent += (uint32_t)__shfl_xor((int)ent, o, 64);
+    if (lane == 0) {
+        const uint64_t u0 = (uint64_t)blockIdx.x * 16;
+        if (bits) atomicOr((unsigned long long *)&E.allowed[u0 >> 6], (unsigned long long)(bits << (u0 & 63)));
+        if (vb) {
+            atomicAdd(&stat_slot(E.stats)[0], 2ull * (unsigned long long)__popcll(vb));
+            atomicAdd(&stat_slot(E.stats)[1], (unsigned long long)ent);
         }
     }
 }
@@ -3960,6 +4126,31 @@ void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_
 void launch_seed_records(const Graph &g, const Reply *recv, uint64_t n, Rec *seed, uint4 *bnd, uint64_t nreq,
                          hipStream_t s) {
     if (n) KLAUNCH(tier_seed_kernel, dim3(tier_grid(n, kTB * kSeedPer)), dim3(kTB), 0, s, g, recv, n, seed, bnd, nreq);
+}
+
+void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
+                        uint32_t world, uint32_t *out, uint64_t cap, hipStream_t s) {
+    if (n) KLAUNCH(tier_label_reply_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, qs, world, out, cap);
+}
+
+void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
+                       uint64_t *lens, hipStream_t s) {
+    if (nsent) KLAUNCH(tier_label_lens_kernel, dim3(tier_grid(nsent, kTB)), dim3(kTB), 0, s, recv, nsent, sq, rp, world, lens);
+}
+
+void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
+                         uint4 *bnd, uint64_t nreq, hipStream_t s) {
+    if (nsent)
+        KLAUNCH(tier_label_bounds_kernel, dim3(tier_grid(nsent, kTB)), dim3(kTB), 0, s, sent, nsent, sq, g, world, bnd, nreq);
+}
+
+void launch_label_eval(const Graph &g, const Eval &e, const uint32_t *recv_label, hipStream_t s) {
+    if (!e.n) return;
+    const unsigned units = (unsigned)((e.n + 15) / 16);
+    if (recv_label)
+        KLAUNCH(tier_label_kernel<false>, dim3(units), dim3(64), 0, s, g, e, recv_label);
+    else
+        KLAUNCH(tier_label_kernel<true>, dim3(units), dim3(64), 0, s, g, e, recv_label);
 }
 
 }  // namespace tier

@@ -140,14 +140,37 @@ struct Searcher {
 
 }  // namespace
 
+namespace {
+void build_reach(IAdj &a, uint32_t n, ReachLabels &out);
+}
+
 void build_reach_labels(const Snapshot &s, ReachLabels &out) {
-    const auto t0 = Clock::now();
     out = ReachLabels{};
-    const uint32_t n = s.Ni;
-    out.n = n;
-    if (!n) return;
     IAdj a;
     make_adj(s, a);
+    build_reach(a, s.Ni, out);
+}
+
+void build_reach_labels_csr(uint32_t n, const uint64_t *f_off, const uint32_t *f_col, const uint64_t *b_off,
+                            const uint32_t *b_col, ReachLabels &out) {
+    out = ReachLabels{};
+    IAdj a;
+    a.col[0] = f_col;
+    a.col[1] = b_col;
+    for (int d = 0; d < 2; d++) {
+        const uint64_t *off = d == 0 ? f_off : b_off;
+        a.beg[d].assign(off, off + n);
+        a.deg[d].resize(n);
+        for (uint32_t v = 0; v < n; v++) a.deg[d][v] = (uint32_t)(off[v + 1] - off[v]);
+    }
+    build_reach(a, n, out);
+}
+
+namespace {
+void build_reach(IAdj &a, uint32_t n, ReachLabels &out) {
+    const auto t0 = Clock::now();
+    out.n = n;
+    if (!n) return;
     // rank: most central first ((interior out-degree + 1) x (interior in-degree + 1))
     out.order.resize(n);
     std::iota(out.order.begin(), out.order.end(), 0u);
@@ -280,6 +303,7 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
     phase("csr");
     out.ms = ms_since(t0);
 }
+}  // namespace
 
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s) {
     std::lock_guard<std::mutex> lk(s.derived_mu);

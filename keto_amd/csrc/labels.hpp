@@ -65,6 +65,10 @@ struct ReachLabels {
 // the others run in parallel batches of max(4 x threads, rank / KETOGPU_LABEL_BATCH_DIV)
 // (default 8)
 void build_reach_labels(const Snapshot &s, ReachLabels &out);
+// the same over a graph given as CSR rows (n nodes; forward and backward rows, every entry
+// below n): the two-tier partitioned mode's replicated core (tier.cpp)
+void build_reach_labels_csr(uint32_t n, const uint64_t *f_off, const uint32_t *f_col, const uint64_t *b_off,
+                            const uint32_t *b_col, ReachLabels &out);
 // the snapshot's labels, built once per snapshot version and shared by every engine over
 // it (ketogpu_multi_new builds one set for all devices)
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s);

@@ -31,6 +31,8 @@
 #include <string>
 #include <vector>
 
+#include "core_index.hpp"  // parallel_chunks
+#include "labels.hpp"
 #include "part_round.hpp"
 #include "tier.hpp"
 
@@ -192,6 +194,15 @@ std::unique_ptr<ketogpu_core> gather_core(const ketogpu_shard_graph &v, Comm *co
     return c;
 }
 
+bool device_memory(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice;
+}
+
 // --------------------------------------------------------------- steps
 // One rank's steps of a two-tier batch (device: TierDevice below; tests: the caller's
 // vtable over host memory).  Codes are KETOGPU_*.
@@ -209,6 +220,10 @@ struct TierSteps {
                          uint64_t nrecv, uint64_t *bits, std::vector<uint32_t> &overflow) = 0;
     virtual void stats(ketogpu_tier_stats &) {}
     virtual std::string error() = 0;
+    // bytes per reply item (tier::Reply; plan label: 4-byte words, tier.hpp "label replies")
+    virtual uint64_t reply_unit() const { return sizeof(tier::Reply); }
+    // the reply items received from each source this step (before evaluate)
+    virtual void replies_from(const uint64_t *, int) {}
 };
 
 struct VtableTier : TierSteps {
@@ -252,21 +267,32 @@ struct TierDevice : TierSteps {
     // per-step scratch (grown on demand)
     Buf d_req, d_lens, d_scan, d_bnd, d_seed, d_bits, d_list[3];
     unsigned long long *d_small = nullptr;  // [0..63] counts, [64..127] cursors, [128] first_bad, [129] bad query,
-                                            // [130..132] list counts, [136..] stats
+                                            // [130..132] list counts, [136..] stats, [kSeg..] label segments
     uint64_t *h_small = nullptr;            // pinned mirror
     // the current step's requests (device-readable) and replies in flight
     const uint32_t *cur_r = nullptr, *cur_t = nullptr, *src_r = nullptr, *src_t = nullptr;
     uint64_t cur_n = 0;
-    bool in_place = false;  // cur_r / cur_t are the caller's buffers (a pinned view)
+    bool in_place = false;  // cur_r / cur_t are the caller's buffers (a pinned view, or HBM)
+    bool req_hbm = false;   // ... in this device's memory: read in place by every pass
     const tier::Query *rq = nullptr;
     uint64_t rq_n = 0;
     // the first evaluation stage bracketed by events (the roofline's kernel time)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double eval_ms = 0;
     uint64_t eval_launches = 0;
+    // plan label (KETOGPU_TIER_LABEL, default 1): the owned nodes' label lists answer the
+    // queries and the evaluation is one intersection per request (labels.hpp)
+    uint64_t label_words = 0;
+    double label_ms = 0;
 
     static constexpr size_t kCounts = 0, kCursor = 64, kFirstBad = 128, kBadQuery = 129, kLists = 130, kStats = 136;
-    static constexpr size_t kSmall = kStats + kEvalStatsLen;
+    // label replies: segments' first items, 65 words each: received queries (owner side),
+    // sent queries and received words (asker side)
+    static constexpr size_t kSeg = kStats + kEvalStatsLen, kQs = kSeg, kSq = kSeg + 72, kRp = kSeg + 144;
+    static constexpr size_t kSmall = kSeg + 216;
+    // the step's sent queries (label replies are matched to them by position)
+    const tier::Query *sent = nullptr;
+    std::vector<uint64_t> sent_counts, recv_from;
 
     ~TierDevice() override {
         if (stream) {
@@ -378,7 +404,88 @@ struct TierDevice : TierSteps {
         G.lr_base = (int64_t)((intptr_t)G.lr_rec - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
         core_records = core->f_col.size() + core->b_col.size();
         seed_records = v.lf_off[v.owned_expandable] + v.lr_off[v.owned_nodes];
+        const char *lab = getenv("KETOGPU_TIER_LABEL");
+        if (!lab || atoi(lab) != 0) build_label_lists(v, core);
         THIP(hipDeviceSynchronize());
+    }
+
+    // The 2-hop labels of the replicated core (the same on every rank: it is the same core)
+    // and, per owned node, its S list (labels.hpp: Lin of the interior entries of rev(x) +
+    // the other entries) and per owned expandable node its P list (Lout(x) for an interior
+    // x, else {x} + Lout of fint(x)), each stored as [mask lo, mask hi, entries ascending].
+    void build_label_lists(const ketogpu_shard_graph &v, const ketogpu_core *core) {
+        const auto t0 = Clock::now();
+        ReachLabels R;
+        build_reach_labels_csr((uint32_t)core->Ni, core->f_off.data(), core->f_col.data(), core->b_off.data(),
+                               core->b_col.data(), R);
+        const uint32_t W = v.world, rank = v.rank;
+        const uint64_t Nil = v.owned_interior, Nxl = v.owned_expandable, Nl = v.owned_nodes;
+        auto global = [&](uint64_t l) -> uint64_t {
+            if (l < Nil) return l * W + rank;
+            if (l < Nxl) return v.num_interior + (l - Nil) * W + rank;
+            return v.num_expandable + (l - Nxl) * W + rank;
+        };
+        auto add_out = [&](uint32_t x, std::vector<uint32_t> &o, uint64_t &m) {
+            m |= R.mout[x];
+            o.insert(o.end(), R.out.begin() + (ptrdiff_t)R.out_off[x], R.out.begin() + (ptrdiff_t)R.out_off[x + 1]);
+        };
+        // one node's list (p: P side) into o, mask into m
+        auto list = [&](bool p, uint64_t l, std::vector<uint32_t> &o, uint64_t &m) {
+            o.clear();
+            m = 0;
+            if (p) {
+                const uint64_t g = global(l);
+                if (g < R.n) {
+                    add_out((uint32_t)g, o, m);
+                    return;  // Lout is ascending already
+                }
+                o.push_back((uint32_t)g);
+                for (uint64_t k = v.lf_off[l]; k < v.lf_off[l + 1]; k++) add_out(v.lf_col[k], o, m);
+            } else {
+                for (uint64_t k = v.lr_off[l]; k < v.lr_off[l + 1]; k++) {
+                    const uint32_t x = v.lr_col[k];
+                    if (x < R.n) {
+                        m |= R.min[x];
+                        o.insert(o.end(), R.in.begin() + (ptrdiff_t)R.in_off[x], R.in.begin() + (ptrdiff_t)R.in_off[x + 1]);
+                    } else {
+                        o.push_back(x);
+                    }
+                }
+            }
+            std::sort(o.begin(), o.end());
+            o.erase(std::unique(o.begin(), o.end()), o.end());
+        };
+        auto build = [&](bool p, uint64_t nodes, const uint64_t *&d_off, const uint32_t *&d_col) {
+            std::vector<uint64_t> off(nodes + 1, 0);
+            parallel_chunks(nodes, 1 << 14, [&](int, uint64_t b, uint64_t e) {
+                std::vector<uint32_t> o;
+                uint64_t m;
+                for (uint64_t l = b; l < e; l++) {
+                    list(p, l, o, m);
+                    off[l + 1] = 2 + o.size();
+                }
+            });
+            for (uint64_t l = 0; l < nodes; l++) off[l + 1] += off[l];
+            std::vector<uint32_t> col(off[nodes]);
+            parallel_chunks(nodes, 1 << 14, [&](int, uint64_t b, uint64_t e) {
+                std::vector<uint32_t> o;
+                uint64_t m;
+                for (uint64_t l = b; l < e; l++) {
+                    list(p, l, o, m);
+                    uint32_t *w = col.data() + off[l];
+                    w[0] = (uint32_t)m;
+                    w[1] = (uint32_t)(m >> 32);
+                    std::copy(o.begin(), o.end(), w + 2);
+                }
+            });
+            label_words += col.size();
+            d_off = upload(off.data(), off.size());
+            d_col = upload(col.data(), col.size());
+        };
+        build(false, Nl, G.ls_off, G.ls_col);
+        build(true, Nxl, G.lp_off, G.lp_col);
+        G.label = 1;
+        label_ms = ms_since(t0);
     }
 
     // the step's requests as the device reads them: pinned memory in place, else copied.
@@ -391,6 +498,7 @@ struct TierDevice : TierSteps {
         cur_r = (const uint32_t *)host_view(r, dev, true);
         cur_t = cur_r ? (const uint32_t *)host_view(t, dev, true) : nullptr;
         in_place = cur_r && cur_t;
+        req_hbm = in_place && device_memory(r) && device_memory(t);
         if (!in_place) {
             uint32_t *d = (uint32_t *)d_req.ensure(8 * std::max<uint64_t>(n, 1));
             if (n) {
@@ -425,7 +533,7 @@ struct TierDevice : TierSteps {
             THIP(hipMemsetAsync(d_small, 0, 128 * 8, stream));
             THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 8, stream));
             // requests read in place from pinned memory are staged into HBM by the count pass
-            uint32_t *stage = n && in_place ? (uint32_t *)d_req.ensure(8 * n) : nullptr;
+            uint32_t *stage = n && in_place && !req_hbm ? (uint32_t *)d_req.ensure(8 * n) : nullptr;
             tier::launch_query_count(G, cur_r, cur_t, n, d_small + kCounts, d_small + kFirstBad, stage, stream);
             if (stage) {
                 cur_r = stage;
@@ -442,6 +550,8 @@ struct TierDevice : TierSteps {
             THIP(hipMemcpyAsync(d_small + kCursor, h_small + kCursor, 64 * 8, hipMemcpyHostToDevice, stream));
             // no wait: the exchange reads `send` on this stream (or copies it to the host here first)
             tier::launch_query_scatter(G, cur_r, cur_t, n, d_small + kCursor, send, stream);
+            sent = send;
+            sent_counts.assign(counts, counts + G.world);
         });
     }
 
@@ -462,18 +572,41 @@ struct TierDevice : TierSteps {
                 if (p < G.world) at += from[p];
             }
             THIP(hipMemcpyAsync(h_small + kBadQuery, d_small + kBadQuery, 8, hipMemcpyDeviceToHost, stream));
+            if (G.label) {  // the received segments' first queries, for launch_label_reply
+                seg_firsts(from, kQs);
+                THIP(hipMemcpyAsync(d_small + kQs, h_small + kQs, 8 * (G.world + 1), hipMemcpyHostToDevice, stream));
+            }
             THIP(hipStreamSynchronize(stream));
             if (h_small[kBadQuery] != ~0ull)
                 throw Error(KETOGPU_EINVAL, "a query for a node this rank does not own (query " +
                                                 std::to_string(h_small[kBadQuery]) + ")");
-            for (uint32_t p = 0; p < G.world; p++) counts[p] = h_small[kCursor + p + 1] - h_small[kCursor + p];
+            // label replies: the segment also carries one length per query
+            for (uint32_t p = 0; p < G.world; p++)
+                counts[p] = h_small[kCursor + p + 1] - h_small[kCursor + p] + (G.label ? from[p] : 0);
         });
     }
+
+    // h_small[at + p] = items before segment p (p = 0..world)
+    void seg_firsts(const uint64_t *cnt, size_t at) {
+        uint64_t acc = 0;
+        for (uint32_t p = 0; p < G.world; p++) {
+            h_small[at + p] = acc;
+            acc += cnt[p];
+        }
+        h_small[at + G.world] = acc;
+    }
+
+    uint64_t reply_unit() const override { return G.label ? 4 : sizeof(tier::Reply); }
+    void replies_from(const uint64_t *from, int world) override { recv_from.assign(from, from + world); }
 
     int reply_emit(tier::Reply *send, uint64_t cap) override {
         return guarded("two-tier replies", [&] {
             THIP(hipSetDevice(dev));
-            tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
+            if (G.label)
+                tier::launch_label_reply(G, rq, rq_n, (const uint64_t *)d_lens.p, (const uint64_t *)(d_small + kQs), G.world,
+                                         (uint32_t *)send, cap, stream);
+            else
+                tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
         });
     }
 
@@ -497,7 +630,7 @@ struct TierDevice : TierSteps {
             E.allowed = allowed;
             E.stats = d_small + kStats;
             E.first_bad = d_small + kFirstBad;
-            if (recv) {
+            if (recv && !G.label) {
                 // seed bounds are u32 offsets into the received entries (tier_seed_kernel): a
                 // step past 2^32 entries fails on this rank (the code travels in the next
                 // status gather); a smaller ketogpu_tier_opts.max_batch splits it
@@ -512,6 +645,50 @@ struct TierDevice : TierSteps {
                 E.recv = seed;
                 E.recv_base_f = (int64_t)((intptr_t)seed - (intptr_t)G.core_f) / (int64_t)sizeof(tier::Rec);
                 E.recv_base_b = (int64_t)((intptr_t)seed - (intptr_t)G.core_b) / (int64_t)sizeof(tier::Rec);
+            }
+            if (G.label) {  // one intersection per request, nothing left for a later stage
+                const uint32_t *rwords = (const uint32_t *)recv;
+                if (recv) {
+                    if (nrecv >= (1ull << 32))
+                        throw Error(KETOGPU_ENOMEM, "two-tier: a step received 2^32 or more reply words (" +
+                                                        std::to_string(nrecv) + "); lower max_batch");
+                    if (sent_counts.size() != G.world || recv_from.size() != G.world)
+                        throw Error(KETOGPU_EINVAL, "two-tier: label replies without this step's queries");
+                    uint64_t nsent = 0;
+                    for (uint64_t c : sent_counts) nsent += c;
+                    seg_firsts(sent_counts.data(), kSq);
+                    seg_firsts(recv_from.data(), kRp);
+                    THIP(hipMemcpyAsync(d_small + kSq, h_small + kSq, 8 * 144, hipMemcpyHostToDevice, stream));
+                    uint64_t *lens = (uint64_t *)d_lens.ensure(8 * (nsent + 1));
+                    uint64_t *scr = (uint64_t *)d_scan.ensure(8 * (nsent / 1024 + 2));
+                    const uint64_t *sq = (const uint64_t *)(d_small + kSq), *rp = (const uint64_t *)(d_small + kRp);
+                    tier::launch_label_lens(rwords, nsent, sq, rp, G.world, lens, stream);
+                    tier::launch_scan(lens, nsent, scr, stream);
+                    uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
+                    THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
+                    tier::launch_label_bounds(sent, nsent, sq, lens, G.world, bnd, n, stream);
+                    E.bnd = bnd;
+                }
+                THIP(hipEventRecord(ev0, stream));
+                tier::launch_label_eval(G, E, rwords, stream);
+                THIP(hipEventRecord(ev1, stream));
+                if (words) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
+                THIP(hipMemcpyAsync(h_small + kFirstBad, d_small + kFirstBad, 8, hipMemcpyDeviceToHost, stream));
+                THIP(hipStreamSynchronize(stream));
+                if (n) {
+                    float ms = 0;
+                    THIP(hipEventElapsedTime(&ms, ev0, ev1));
+                    eval_ms += ms;
+                    eval_launches++;
+                }
+                if (h_small[kFirstBad] != ~0ull)
+                    throw Error(KETOGPU_EINVAL, "request " + std::to_string(h_small[kFirstBad]) +
+                                                    " has an id outside the partitioned layout");
+                if (force_overflow) {
+                    std::fill(bits, bits + words, 0);
+                    for (uint64_t c = 0; c < n; c++) overflow.push_back((uint32_t)c);
+                }
+                return;
             }
             unsigned *lc = (unsigned *)(d_small + kLists);  // three u32 list counts (+ padding)
             THIP(hipEventRecord(ev0, stream));
@@ -564,6 +741,9 @@ struct TierDevice : TierSteps {
         st.seed_records = seed_records;
         st.eval_kernel_ms = eval_ms;
         st.eval_kernel_launches = eval_launches;
+        st.label = G.label;
+        st.label_words = label_words;
+        st.label_build_ms = label_ms;
     }
 
     std::string error() override { return err; }
@@ -658,8 +838,17 @@ struct ketogpu_tier {
             ns += sb[p];
             nr += rb[p];
         }
-        recv.ensure(nr);
         const auto t0 = Clock::now();
+        if (world == 1 && !comm->loop_self && !stage) {
+            // one rank: what it sends is what it receives, the buffers trade places (no copy)
+            std::swap(send.p, recv.p);
+            std::swap(send.cap, recv.cap);
+            st.collectives++;
+            st.exchange_ms += ms_since(t0);
+            *n_in = nr / unit;
+            return KETOGPU_OK;
+        }
+        recv.ensure(nr);
         if (stage) {  // device steps, host transport
             h_send.ensure(ns);
             h_recv.ensure(nr);
@@ -704,18 +893,20 @@ struct ketogpu_tier {
             if (code) fail(code, local, steps->error());
             local = steps->reply_sizes(q_recv.as<tier::Query>(), nq, from.data(), counts.data());
             uint64_t out = 0;
+            const uint64_t unit = steps->reply_unit();
             if (!local) {
                 for (uint64_t c : counts) out += c;
                 try {
-                    r_send.ensure(sizeof(tier::Reply) * out);
+                    r_send.ensure(unit * out);
                 } catch (const Error &e) {
                     local = e.code;
                 }
             }
             if (!local) local = steps->reply_emit(r_send.as<tier::Reply>(), out);
             if (!local) st.records_sent += out;
-            code = exchange(local, counts.data(), sizeof(tier::Reply), r_send, r_recv, &nr, from);
+            code = exchange(local, counts.data(), unit, r_send, r_recv, &nr, from);
             if (code) fail(code, local, steps->error());
+            steps->replies_from(from.data(), world);
             st.records_received += nr;
             local = steps->evaluate(roots, targets, n, r_recv.as<tier::Reply>(), nr, bits, overflow);
         }
@@ -757,6 +948,16 @@ struct ketogpu_tier {
         st.fallback_calls++;
         st.overflow_requests += mine.size();
         std::vector<uint32_t> pairs(2 * mine.size());
+        std::vector<uint32_t> hr, ht;  // requests in device memory: a host copy for this rare path
+        if (steps->device && !mine.empty() && device_memory(roots)) {
+            const uint64_t n = (uint64_t)mine.back() + 1;
+            hr.resize(n);
+            ht.resize(n);
+            THIP(hipMemcpy(hr.data(), roots, 4 * n, hipMemcpyDefault));
+            THIP(hipMemcpy(ht.data(), targets, 4 * n, hipMemcpyDefault));
+            roots = hr.data();
+            targets = ht.data();
+        }
         for (size_t k = 0; k < mine.size(); k++) {
             pairs[2 * k] = roots[mine[k]];
             pairs[2 * k + 1] = targets[mine[k]];

@@ -55,6 +55,13 @@ struct Graph {
     const uint32_t *lf_node, *lr_node;  // the same rows' entries as plain node ids (the replies)
     int64_t lf_base, lr_base;         // lf_rec - core_f and lr_rec - core_b in records
     uint32_t both_max, seed_max;
+    // label mode (plan label, labels.hpp): every rank builds the same 2-hop labels of the
+    // replicated core; an owner's S list of every owned node and P list of every owned
+    // expandable node, each [mask lo, mask hi, entries ascending]: a query is answered with
+    // the list instead of the row, and the evaluation is one intersection per request
+    uint32_t label;
+    const uint64_t *ls_off, *lp_off;
+    const uint32_t *ls_col, *lp_col;
 };
 
 // evaluation stages: 0 = one 16-request unit per workgroup over every unit of the batch,
@@ -74,6 +81,23 @@ struct Eval {
 };
 void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_list, const unsigned *in_count,
                  uint32_t *out_list, unsigned *out_count, unsigned grid, hipStream_t s);
+// Label replies (plan label): 4-byte words; the segment for one destination is the lengths
+// of the lists it asked for (its query order), then the lists.  With qs[p] the first query
+// of segment p (p = 0..world, qs[world] = total) and off the lengths' exclusive scan over
+// all queries, query j of segment p has its length at j + off[qs[p]] and its list at
+// qs[p + 1] + off[j] — the same formula on the asking side over ITS sent queries.
+//   owner:  reply_lengths -> scan -> launch_label_reply (lengths and lists in one pass)
+//   asker:  launch_label_lens (the lengths out of the received segments, rp[p] = segment
+//           p's first word) -> scan -> launch_label_bounds (per request the bounds of its P
+//           list (x, y) and S list (z, w); bnd cleared by the caller) -> launch_label_eval
+// launch_label_eval: recv_label null: the rank owns every node and reads its own lists
+void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
+                        uint32_t world, uint32_t *out, uint64_t cap, hipStream_t s);
+void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
+                       uint64_t *lens, hipStream_t s);
+void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
+                         uint4 *bnd, uint64_t nreq, hipStream_t s);
+void launch_label_eval(const Graph &g, const Eval &e, const uint32_t *recv_label, hipStream_t s);
 int stage_units_per_cu(int stage);
 
 // queries of the batch grouped by owner: count (per destination) then scatter at cursors

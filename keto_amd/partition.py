@@ -520,6 +520,11 @@ class TieredEngine:
         L.check(self.L.ketogpu_tier_check_ids(self.h, roots.ctypes.data, targets.ctypes.data, n, bits.ctypes.data))
         return np.unpackbits(bits.view(np.uint8), bitorder="little")[:n].astype(bool)
 
+    def check_ids_ptr(self, roots_ptr, targets_ptr, n, bits):
+        """the batch call on raw request pointers (host memory, or this device's HBM: read in
+        place by every pass) -> bits (host uint64 array)"""
+        L.check(self.L.ketogpu_tier_check_ids(self.h, roots_ptr, targets_ptr, n, bits.ctypes.data))
+
     def check_ids_raw(self, roots, targets, bits):
         """the batch call on caller arrays (pinned buffers are read in place at world 1)"""
         L.check(self.L.ketogpu_tier_check_ids(self.h, roots.ctypes.data, targets.ctypes.data, len(roots),

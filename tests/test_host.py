@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in L.SIGNATURES, f"{s} lacks a ctypes signature"
-    assert lib.ketogpu_abi_version() == 8
+    assert lib.ketogpu_abi_version() == 9
 
 
 def test_builder_rejects_unsorted_rows_and_duplicate_namespaces():

@@ -220,14 +220,31 @@ def _need_gpu():
         pytest.fail("no HIP device visible")
 
 
+# plan label (the default: owners reply with label lists, one intersection per request)
+# and the row exchange + LDS units (KETOGPU_TIER_LABEL=0)
+LABEL = pytest.mark.parametrize("label", ["1", "0"], ids=["label", "rows"])
+
+
+def _mode(monkeypatch, label):
+    monkeypatch.setenv("KETOGPU_TIER_LABEL", label)
+
+
+def _check_mode(st, label):
+    assert st["label"] == int(label)
+    if label == "1":
+        assert st["label_words"] > 0 and st["overflow_requests"] == 0
+
+
 @pytest.mark.gpu
+@LABEL
 @pytest.mark.parametrize("seed", [91, 92])
-def test_tier_device_single_rank(seed):
-    """world 1: rows read in place, the lite unit over the core; random networks with
-    poisoned pages, several steps, pinned and pageable requests"""
+def test_tier_device_single_rank(seed, label, monkeypatch):
+    """world 1: rows (or label lists) read in place; random networks with poisoned pages,
+    several steps, pinned and pageable requests"""
     from keto_amd import check
     from keto_amd.partition import TieredEngine
     _need_gpu()
+    _mode(monkeypatch, label)
     namespaces, rows, reqs = _case(seed, n_rows=1500, n_req=3000)
     sh = _load(namespaces, rows)
     want = _want(namespaces, rows, reqs)
@@ -238,6 +255,7 @@ def test_tier_device_single_rank(seed):
     np.testing.assert_array_equal(eng.check_ids(pr.array, pt.array), want)
     st = eng.stats()
     assert st["batches"] == 2 * 3 and st["rows_opened"] > 0 and st["overflow_requests"] == 0
+    _check_mode(st, label)
     # an id outside the layout fails the call; the engine answers the next batch
     r = roots.copy()
     r[5] = 1 << 30
@@ -248,12 +266,14 @@ def test_tier_device_single_rank(seed):
 
 
 @pytest.mark.gpu
-def test_tier_device_config5_matches_oracle():
+@LABEL
+def test_tier_device_config5_matches_oracle(label, monkeypatch):
     """config #5's shape through the partition-aware loader, the core and the HIP steps,
     every request against the oracle (and the per-level engine agrees)"""
     from keto_amd import synth
     from keto_amd.partition import PartitionedEngine, Shard, TieredEngine
     _need_gpu()
+    _mode(monkeypatch, label)
     w = synth.config5(users=100000, groups=10000, docs=40000, tuples=1_000_000, checks=20000, seed=23)
     from oracle import oracle as O
     st = O.Store(w.namespaces, 100)
@@ -264,24 +284,29 @@ def test_tier_device_config5_matches_oracle():
     roots, targets, status = sh.resolve_batch(w.request_batch())
     eng = TieredEngine(sh, device=0)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    _check_mode(eng.stats(), label)
     np.testing.assert_array_equal(PartitionedEngine(sh, device=0, direction="backward").check_ids(roots, targets),
                                   want)
     assert want[w.chk_pos.astype(bool)].all()
 
 
 @pytest.mark.gpu
-def test_tier_device_power_law_cascade():
+@LABEL
+def test_tier_device_power_law_cascade(label, monkeypatch):
     """power-law nesting (config #4's shape, small): large closures take the larger-table
-    stages and, past them, the per-level engine; every answer against the oracle"""
+    stages and, past them, the per-level engine (rows mode), or long label lists read past
+    their LDS copies (label mode); every answer against the oracle"""
     from keto_amd import synth
     from keto_amd.partition import Shard, TieredEngine
     _need_gpu()
+    _mode(monkeypatch, label)
     w = synth.social(users=20000, groups=4000, tuples=200_000, checks=20000, seed=31)
     want = randgraph_want(w)
     sh = Shard.load(w.namespaces, lambda: iter([w.columns]))
     roots, targets, status = sh.resolve_batch(w.request_batch())
     eng = TieredEngine(sh, device=0)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    _check_mode(eng.stats(), label)
 
 
 def randgraph_want(w):
@@ -291,8 +316,9 @@ def randgraph_want(w):
 
 
 @pytest.mark.gpu
+@LABEL
 @pytest.mark.parametrize("loop_self", [False, True])
-def test_tier_device_rccl_world1_matches_oracle(loop_self, monkeypatch):
+def test_tier_device_rccl_world1_matches_oracle(loop_self, label, monkeypatch):
     """a real RCCL communicator of one rank: the exchange path (queries, replies, seed
     records from the received rows) against the oracle.  By default the own segment of each
     all-to-all is a copy-engine DMA and the world-1 count gathers are skipped, so only the
@@ -301,6 +327,7 @@ def test_tier_device_rccl_world1_matches_oracle(loop_self, monkeypatch):
     the data path of a multi-GPU run, executed on one GPU (counted by the communicator)"""
     if loop_self:
         monkeypatch.setenv("KETOGPU_TEST_RCCL_SELF", "1")
+    _mode(monkeypatch, label)
     from keto_amd import synth
     from keto_amd.partition import NativeComm, Shard, TieredEngine
     _need_gpu()
@@ -317,20 +344,24 @@ def test_tier_device_rccl_world1_matches_oracle(loop_self, monkeypatch):
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
     s = eng.stats()
     assert s["queries_sent"] > 0 and s["records_sent"] == s["records_received"] > 0
+    _check_mode(s, label)
     cs = comm.stats()
     assert cs["rccl"] == 1 and cs["loop_self"] == int(loop_self) and cs["allgathers"] > 0
     if loop_self:  # two all-to-alls (queries, replies) and their count gathers per step
         steps = (len(roots) + 4095) // 4096
         assert cs["sends"] >= 2 * steps and cs["recvs"] == cs["sends"] and cs["allgathers"] >= 2 * steps
-        assert cs["bytes_sent"] >= 8 * (s["queries_sent"] + s["records_sent"])
+        unit = 4 if label == "1" else 8  # label replies are 4-byte words, row replies 8-byte records
+        assert cs["bytes_sent"] >= 8 * s["queries_sent"] + unit * s["records_sent"]
     else:
         assert cs["sends"] == 0 and cs["recvs"] == 0
 
 
 @pytest.mark.gpu
-def test_tier_device_two_ranks_share_gpu():
+@LABEL
+def test_tier_device_two_ranks_share_gpu(label, monkeypatch):
     """two ranks on the box's GPU over gloo: device steps, host transport (staged)"""
     _need_gpu()
+    _mode(monkeypatch, label)
     namespaces, rows, reqs = _case(85)
     want = _want(namespaces, rows, reqs)
     got, stats, _ = _run_tier(2, 85, 29790, device_steps=True)
