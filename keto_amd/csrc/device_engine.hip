@@ -3292,12 +3292,33 @@ __global__ __launch_bounds__(kTB) void tier_query_scatter_kernel(tier::Graph G, 
     }
 }
 
+// world 1 (one owner): request i's queries sit at slots 2i and 2i + 1, no counting pass;
+// a request without an answer (an id NONE or outside the layout) gets two NONE slots
+__global__ __launch_bounds__(kTB) void tier_pair_kernel(tier::Graph G, const uint32_t *roots, const uint32_t *targets,
+                                                        uint64_t n, tier::Query *out, unsigned long long *first_bad,
+                                                        uint32_t *stage) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kTB) {
+        uint32_t r = roots[i], t = targets[i];
+        if (stage) {
+            stage[i] = r;
+            stage[n + i] = t;
+        }
+        if ((r != KETOGPU_NODE_NONE && r >= G.Nx) || (t != KETOGPU_NODE_NONE && t >= G.N)) {
+            atomicMin(first_bad, (unsigned long long)i);
+            r = t = KETOGPU_NODE_NONE;
+        }
+        if (r == KETOGPU_NODE_NONE || t == KETOGPU_NODE_NONE) r = t = KETOGPU_NODE_NONE;
+        reinterpret_cast<uint4 *>(out)[i] = make_uint4((uint32_t)(i << 1), r, (uint32_t)(i << 1 | 1), t);
+    }
+}
+
 // the owner's side: the length of the row each received query asks for (lens[j]); a
 // query for a node this rank does not own (a misrouted record) raises *bad
 __device__ __forceinline__ void tier_row(const tier::Graph &G, const tier::Query &q, uint64_t &b, uint64_t &e,
                                          bool &bad) {
     b = e = 0;
     bad = false;
+    if (q.node == KETOGPU_NODE_NONE) return;  // a world-1 pair slot of an unanswerable request
     const uint32_t l = tier_local(G, q.node);
     if (l == KETOGPU_NODE_NONE) {
         bad = true;
@@ -3555,17 +3576,19 @@ __global__ __launch_bounds__(kTB) void tier_label_lens_kernel(const uint32_t *re
 }
 
 // ... and with the lengths scanned (g), each list's bounds: it starts at sq[p + 1] + g[k]
-// (the same layout seen from the asker), for request tag >> 1, side tag & 1
+// (the same layout seen from the asker), for request tag >> 1, side tag & 1.  A list that
+// would end past the received words (cap) is left empty, so the evaluation never reads
+// past them (the world-1 step evaluates a batch whose replies outgrew the buffer again)
 __global__ __launch_bounds__(kTB) void tier_label_bounds_kernel(const tier::Query *sent, uint64_t nsent,
                                                                 const uint64_t *sq, const uint64_t *g, uint32_t world,
-                                                                uint4 *bnd, uint64_t nreq) {
+                                                                uint4 *bnd, uint64_t nreq, uint64_t cap) {
     for (uint64_t k = (uint64_t)blockIdx.x * kTB + threadIdx.x; k < nsent; k += (uint64_t)gridDim.x * kTB) {
         const uint32_t p = tier_seg(sq, world, k);
         const uint32_t tag = sent[k].tag;
         const uint64_t i = tag >> 1;
         if (i >= nreq) continue;
-        const uint64_t b = sq[p + 1] + g[k];
-        reinterpret_cast<uint2 *>(&bnd[i])[tag & 1u] = make_uint2((uint32_t)b, (uint32_t)(b + (g[k + 1] - g[k])));
+        const uint64_t b = sq[p + 1] + g[k], e = b + (g[k + 1] - g[k]);
+        reinterpret_cast<uint2 *>(&bnd[i])[tag & 1u] = e <= cap ? make_uint2((uint32_t)b, (uint32_t)e) : make_uint2(0u, 0u);
     }
 }
 
@@ -4101,6 +4124,11 @@ void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *t
                 first_bad, stage);
 }
 
+void launch_query_pairs(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n, Query *out,
+                        unsigned long long *first_bad, uint32_t *stage, hipStream_t s) {
+    if (n) KLAUNCH(tier_pair_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, roots, targets, n, out, first_bad, stage);
+}
+
 void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
                           unsigned long long *cursor, Query *out, hipStream_t s) {
     if (n) KLAUNCH(tier_query_scatter_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, roots, targets, n, cursor, out);
@@ -4139,9 +4167,10 @@ void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq,
 }
 
 void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
-                         uint4 *bnd, uint64_t nreq, hipStream_t s) {
+                         uint4 *bnd, uint64_t nreq, uint64_t cap, hipStream_t s) {
     if (nsent)
-        KLAUNCH(tier_label_bounds_kernel, dim3(tier_grid(nsent, kTB)), dim3(kTB), 0, s, sent, nsent, sq, g, world, bnd, nreq);
+        KLAUNCH(tier_label_bounds_kernel, dim3(tier_grid(nsent, kTB)), dim3(kTB), 0, s, sent, nsent, sq, g, world, bnd, nreq,
+                cap);
 }
 
 void launch_label_eval(const Graph &g, const Eval &e, const uint32_t *recv_label, hipStream_t s) {

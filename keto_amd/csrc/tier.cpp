@@ -224,6 +224,12 @@ struct TierSteps {
     virtual uint64_t reply_unit() const { return sizeof(tier::Reply); }
     // the reply items received from each source this step (before evaluate)
     virtual void replies_from(const uint64_t *, int) {}
+    // world 1 with one host wait (TierDevice::step_world1), when the steps have it
+    virtual bool has_world1() const { return false; }
+    virtual int step_world1(const uint32_t *, const uint32_t *, uint64_t, uint64_t *, std::vector<uint32_t> &,
+                            uint64_t &) {
+        return KETOGPU_EINVAL;
+    }
 };
 
 struct VtableTier : TierSteps {
@@ -299,7 +305,8 @@ struct TierDevice : TierSteps {
             (void)hipSetDevice(dev);
             (void)hipStreamSynchronize(stream);
         }
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) b->release();
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep})
+            b->release();
         for (void *p : owned) (void)hipFree(p);
         for (hipEvent_t e : {ev0, ev1})
             if (e) (void)hipEventDestroy(e);
@@ -359,12 +366,14 @@ struct TierDevice : TierSteps {
         this->device = true;
         dev = device;
         force_overflow = getenv("KETOGPU_TEST_TIER_OVERFLOW") != nullptr;
+        const char *ow = getenv("KETOGPU_TIER_ONE_WAIT");
+        one_wait = !ow || atoi(ow) != 0;
         THIP(hipSetDevice(dev));
         THIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         THIP(hipEventCreate(&ev0));
         THIP(hipEventCreate(&ev1));
         THIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2]}) {
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep}) {
             b->device = true;
             b->dev = dev;
         }
@@ -597,6 +606,90 @@ struct TierDevice : TierSteps {
     }
 
     uint64_t reply_unit() const override { return G.label ? 4 : sizeof(tier::Reply); }
+
+    // World 1 through the exchange path's kernels with ONE host wait per step (plan label;
+    // KETOGPU_TIER_ONE_WAIT=0: the general protocol).  With one owner the counts the
+    // general protocol waits for are known or not needed: request i's queries take slots 2i
+    // and 2i + 1 (no counting pass), the reply segment is the whole buffer, and the asker's
+    // list lengths are the owner's (the same scan).  The reply buffer's capacity is the
+    // last step's; a step whose replies outgrow it (known at the wait) is evaluated again
+    // with a larger buffer.
+    bool one_wait = true;  // KETOGPU_TIER_ONE_WAIT when the engine is made
+    bool has_world1() const override { return G.label && one_wait; }
+    Buf d_q, d_rep;
+    int step_world1(const uint32_t *r, const uint32_t *t, uint64_t n, uint64_t *bits, std::vector<uint32_t> &overflow,
+                    uint64_t &reply_words) override {
+        overflow.clear();
+        return guarded("two-tier step", [&] {
+            THIP(hipSetDevice(dev));
+            set_requests(r, t, n, true);
+            const uint64_t nq = 2 * n, words = (n + 63) / 64;
+            tier::Query *q = (tier::Query *)d_q.ensure(sizeof(tier::Query) * std::max<uint64_t>(nq, 1));
+            uint64_t *lens = (uint64_t *)d_lens.ensure(8 * (nq + 1));
+            uint64_t *scr = (uint64_t *)d_scan.ensure(8 * (nq / 1024 + 2));
+            uint64_t *allowed = (uint64_t *)d_bits.ensure(8 * std::max<uint64_t>(words, 1));
+            uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
+            THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 16, stream));  // first bad request, bad query
+            uint32_t *stage = n && in_place && !req_hbm ? (uint32_t *)d_req.ensure(8 * n) : nullptr;
+            tier::launch_query_pairs(G, cur_r, cur_t, n, q, d_small + kFirstBad, stage, stream);
+            if (stage) {
+                cur_r = stage;
+                cur_t = stage + n;
+            }
+            tier::launch_reply_lengths(G, q, nq, lens, d_small + kBadQuery, stream);
+            tier::launch_scan(lens, nq, scr, stream);
+            h_small[kQs] = 0;
+            h_small[kQs + 1] = nq;
+            THIP(hipMemcpyAsync(d_small + kQs, h_small + kQs, 16, hipMemcpyHostToDevice, stream));
+            const uint64_t *qs = (const uint64_t *)(d_small + kQs);
+            tier::Eval E{};
+            E.roots = cur_r;
+            E.targets = cur_t;
+            E.n = n;
+            E.allowed = allowed;
+            E.stats = d_small + kStats;
+            E.first_bad = d_small + kFirstBad;
+            E.bnd = bnd;
+            for (;;) {
+                const uint64_t cap = d_rep.cap / 4;
+                uint32_t *rep = (uint32_t *)d_rep.ensure(4 * std::max<uint64_t>(nq, 1));
+                const uint64_t cap_now = std::max(cap, d_rep.cap / 4);
+                tier::launch_label_reply(G, q, nq, lens, qs, 1, rep, cap_now, stream);
+                THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
+                THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
+                tier::launch_label_bounds(q, nq, qs, lens, 1, bnd, n, cap_now, stream);
+                THIP(hipEventRecord(ev0, stream));
+                tier::launch_label_eval(G, E, rep, stream);
+                THIP(hipEventRecord(ev1, stream));
+                if (words) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
+                THIP(hipMemcpyAsync(h_small + kFirstBad, d_small + kFirstBad, 16, hipMemcpyDeviceToHost, stream));
+                THIP(hipMemcpyAsync(h_small + kLists, lens + nq, 8, hipMemcpyDeviceToHost, stream));
+                THIP(hipStreamSynchronize(stream));  // the step's one wait
+                if (h_small[kBadQuery] != ~0ull)
+                    throw Error(KETOGPU_EINVAL, "a query for a node this rank does not own (query " +
+                                                    std::to_string(h_small[kBadQuery]) + ")");
+                if (h_small[kFirstBad] != ~0ull)
+                    throw Error(KETOGPU_EINVAL, "request " + std::to_string(h_small[kFirstBad]) +
+                                                    " has an id outside the partitioned layout");
+                reply_words = nq + h_small[kLists];
+                if (reply_words >= (1ull << 32))
+                    throw Error(KETOGPU_ENOMEM, "two-tier: a step's replies reach 2^32 words (" +
+                                                    std::to_string(reply_words) + "); lower max_batch");
+                if (reply_words <= cap_now) break;
+                d_rep.ensure(4 * reply_words);  // outgrown: evaluate again with room for all of it
+            }
+            if (n) {
+                float ms = 0;
+                THIP(hipEventElapsedTime(&ms, ev0, ev1));
+                eval_ms += ms;
+                eval_launches++;
+            }
+            if (force_overflow) {
+                std::fill(bits, bits + words, 0);
+                for (uint64_t c = 0; c < n; c++) overflow.push_back((uint32_t)c);
+            }
+        });
+    }
     void replies_from(const uint64_t *from, int world) override { recv_from.assign(from, from + world); }
 
     int reply_emit(tier::Reply *send, uint64_t cap) override {
@@ -666,7 +759,7 @@ struct TierDevice : TierSteps {
                     tier::launch_scan(lens, nsent, scr, stream);
                     uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
                     THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
-                    tier::launch_label_bounds(sent, nsent, sq, lens, G.world, bnd, n, stream);
+                    tier::launch_label_bounds(sent, nsent, sq, lens, G.world, bnd, n, nrecv, stream);
                     E.bnd = bnd;
                 }
                 THIP(hipEventRecord(ev0, stream));
@@ -882,6 +975,13 @@ struct ketogpu_tier {
         if (!comm) {
             local = steps->evaluate(roots, targets, n, nullptr, 0, bits, overflow);
             if (local) throw Error(local, steps->error());
+        } else if (world == 1 && !comm->loop_self && !stage && steps->has_world1()) {
+            uint64_t words = 0;  // one rank: nothing to agree on, the exchange is the identity
+            local = steps->step_world1(roots, targets, n, bits, overflow, words);
+            if (local) throw Error(local, steps->error());
+            st.queries_sent += 2 * n;
+            st.records_sent += words;
+            st.records_received += words;
         } else {
             std::vector<uint64_t> counts(world, 0), from;
             q_send.ensure(sizeof(tier::Query) * 2 * std::max<uint64_t>(n, 1));

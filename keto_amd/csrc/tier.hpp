@@ -89,14 +89,15 @@ void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_li
 //   owner:  reply_lengths -> scan -> launch_label_reply (lengths and lists in one pass)
 //   asker:  launch_label_lens (the lengths out of the received segments, rp[p] = segment
 //           p's first word) -> scan -> launch_label_bounds (per request the bounds of its P
-//           list (x, y) and S list (z, w); bnd cleared by the caller) -> launch_label_eval
+//           list (x, y) and S list (z, w); bnd cleared by the caller; a list ending past
+//           cap received words: left empty) -> launch_label_eval
 // launch_label_eval: recv_label null: the rank owns every node and reads its own lists
 void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
                         uint32_t world, uint32_t *out, uint64_t cap, hipStream_t s);
 void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
                        uint64_t *lens, hipStream_t s);
 void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
-                         uint4 *bnd, uint64_t nreq, hipStream_t s);
+                         uint4 *bnd, uint64_t nreq, uint64_t cap, hipStream_t s);
 void launch_label_eval(const Graph &g, const Eval &e, const uint32_t *recv_label, hipStream_t s);
 int stage_units_per_cu(int stage);
 
@@ -105,6 +106,9 @@ int stage_units_per_cu(int stage);
 // so later passes read them from HBM instead of host memory again
 void launch_query_count(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
                         unsigned long long *counts, unsigned long long *first_bad, uint32_t *stage, hipStream_t s);
+// world 1: request i's queries at slots 2i, 2i + 1 (NONE nodes: no answer); no counting
+void launch_query_pairs(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n, Query *out,
+                        unsigned long long *first_bad, uint32_t *stage, hipStream_t s);
 void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t *targets, uint64_t n,
                           unsigned long long *cursor, Query *out, hipStream_t s);
 // replies: the rows the received queries ask for, in query order (so grouped like the

@@ -317,14 +317,19 @@ def randgraph_want(w):
 
 @pytest.mark.gpu
 @LABEL
-@pytest.mark.parametrize("loop_self", [False, True])
-def test_tier_device_rccl_world1_matches_oracle(loop_self, label, monkeypatch):
+@pytest.mark.parametrize("loop_self,one_wait", [(False, "1"), (False, "0"), (True, "1")],
+                         ids=["copy-one-wait", "copy-general", "rccl-self"])
+def test_tier_device_rccl_world1_matches_oracle(loop_self, one_wait, label, monkeypatch):
     """a real RCCL communicator of one rank: the exchange path (queries, replies, seed
     records from the received rows) against the oracle.  By default the own segment of each
     all-to-all is a copy-engine DMA and the world-1 count gathers are skipped, so only the
     loader's ncclAllGather runs over RCCL; with KETOGPU_TEST_RCCL_SELF=1 every exchange is a
     grouped ncclSend/ncclRecv to the rank itself and every count gather an ncclAllGather —
-    the data path of a multi-GPU run, executed on one GPU (counted by the communicator)"""
+    the data path of a multi-GPU run, executed on one GPU (counted by the communicator).
+    Plan label at world 1 without loop_self runs the one-wait step (TierDevice::step_world1:
+    pair slots, no counts; its first step outgrows the reply buffer and is evaluated again)
+    unless KETOGPU_TIER_ONE_WAIT=0 (the general protocol, buffers swapped)"""
+    monkeypatch.setenv("KETOGPU_TIER_ONE_WAIT", one_wait)
     if loop_self:
         monkeypatch.setenv("KETOGPU_TEST_RCCL_SELF", "1")
     _mode(monkeypatch, label)
