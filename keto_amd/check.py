@@ -259,6 +259,14 @@ class DeviceQueries:
         L.check(self.e.L.ketogpu_queries_download(self.e.h, self.h, ab.ctypes.data, fb.ctypes.data))
         return (unpack_bits(ab, self.n), unpack_bits(fb, self.n)) if with_flags else unpack_bits(ab, self.n)
 
+    def download_words(self):
+        """the raw result and flag words (ceil(n/64) each)"""
+        words = max((self.n + 63) // 64, 1)
+        ab = np.zeros(words, dtype=np.uint64)
+        fb = np.zeros(words, dtype=np.uint64)
+        L.check(self.e.L.ketogpu_queries_download(self.e.h, self.h, ab.ctypes.data, fb.ctypes.data))
+        return ab, fb
+
     def close(self):
         if getattr(self, "h", None):
             self.e.L.ketogpu_queries_free(self.h)

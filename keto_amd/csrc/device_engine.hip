@@ -2710,10 +2710,14 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     x = (x | x >> 12) & 0x000000FF000000FFull;
     x = (x | x >> 24) & 0xFFFFull;
     if (lane == 0) {
-        const uint64_t c0 = unit * 16;
-        if (x) atomicOr((unsigned long long *)&allowed[c0 >> 6], (unsigned long long)x << (c0 & 63));
-        atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
-        atomicAdd(&stat_slot(stats)[2], (unsigned long long)ent);  // u32 entries: 4 B each
+        // the unit's 16 result bits are the 16-bit word `unit` of the result array: a plain
+        // store (every unit writes its own, zeros included), so the array needs no clearing
+        // before the first stage; the later passes OR their bits in after it
+        reinterpret_cast<uint16_t *>(allowed)[unit] = (uint16_t)x;
+        if (stats) {  // (lean calls: none)
+            atomicAdd(&stat_slot(stats)[0], (unsigned long long)rows);
+            atomicAdd(&stat_slot(stats)[2], (unsigned long long)ent);  // u32 entries: 4 B each
+        }
     }
 }
 
@@ -2736,6 +2740,9 @@ __global__ __launch_bounds__(64) void label_kernel(LabelGraph L, const uint32_t 
     uint32_t r, t;
     bidi_load_rt<16>(unit, units, roots, targets, n, r, t);
     label_unit<HS, HP>(sh, L, r, t, allowed, unit, R, F, stats);
+    // the last result word's 16-bit parts past the last unit (no unit writes them)
+    if (unit + 1 == units && threadIdx.x == 0)
+        for (uint64_t u = units; u < (units + 3) / 4 * 4; u++) reinterpret_cast<uint16_t *>(allowed)[u] = 0;
 }
 
 // pinned host requests read in place: four waves per workgroup, one unit each; wave 0 reads
@@ -2774,10 +2781,16 @@ __global__ __launch_bounds__(256) void label_host_kernel(DevGraph g, LabelGraph 
 constexpr uint32_t kFullStage = 256;
 // Workgroup 0 also totals both lists' shard counts for the host (totals[0]: the rest list,
 // totals[1]: this list), so the rest stage can be launched only when it has requests.
+// Lean HBM-resident calls (plan label, timing events off, KETOGPU_LABEL_FUSE=1): the first
+// stage and this pass run without statistics atomics (stats == nullptr: the statistics are
+// diagnostics, collected by the same calls with events on), and workgroup 0 writes the two
+// list totals straight into the host-mapped mirror (`mirror`: the words stats_reduce_kernel
+// would write — zero statistics, spill counters {rest total, 0 ... 0, full total}), so the
+// call needs no statistics launch and, after a call without rest requests, no clear.
 template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *allowed, LabelRest R, LabelRest F,
                                                         unsigned int *total_rest, unsigned int *total_full,
-                                                        unsigned long long *stats) {
+                                                        unsigned long long *stats, unsigned long long *mirror) {
     __shared__ LabelShared<HS, HP> sh;
     __shared__ alignas(16) uint32_t stage[16][kFullStage];
     const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
@@ -2789,6 +2802,8 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
     if (blockIdx.x == 0) {
         const uint32_t tr = wave_sum_all(R.count[lane * kRestStride]), tf = wave_sum_all(c);
         if (lane == 0) *total_rest = tr, *total_full = tf;
+        if (mirror && lane < 12)  // u32 spill counters at words 8..11: [0] rest total, [7] full total
+            mirror[lane] = lane == 8 ? (unsigned long long)tr : lane == 11 ? (unsigned long long)tf << 32 : 0ull;
     }
     uint64_t ent = 0;
     for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
@@ -2840,7 +2855,7 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
         wave_sync();  // (the LDS rows are rewritten by the next unit)
     }
     const uint32_t e = wave_sum_all((uint32_t)ent);
-    if (lane == 0 && e) atomicAdd(&stat_slot(stats)[2], (unsigned long long)e);
+    if (stats && lane == 0 && e) atomicAdd(&stat_slot(stats)[2], (unsigned long long)e);
 }
 
 // the second stage: plan lite's traversal over the requests the labels did not answer
@@ -4211,6 +4226,9 @@ struct ketogpu_queries {
     uint64_t *d_dyn_int_off = nullptr, *d_dyn_full_off = nullptr;
     uint32_t *d_dyn_int = nullptr, *d_dyn_full = nullptr, *d_dyn_amb = nullptr;
     bool has_dyn = false;
+    // the flag words are all zero (the last run on this batch was a plan-label call that
+    // wrote none): with the engine's label_clean, the next such call skips the clear
+    bool flags_zero = false;
     Batch batch() const {
         Batch b;
         b.roots = d_roots;
@@ -4345,6 +4363,17 @@ struct ketogpu_engine {
                          full_rec};
     }
     uint4 *full_rec = nullptr;  // plan label's full list: {request, root, target, 0} per request (spill_cap)
+    // KETOGPU_LABEL_FUSE=0: no lean calls (statistics, their reduction and the clear in
+    // every call; A/B)
+    bool fuse_reduce = [] {
+        const char *e = getenv("KETOGPU_LABEL_FUSE");
+        return !e || atoi(e) != 0;
+    }();
+    // the statistics slots and spill counters are zero (the last call was a lean one without
+    // rest requests after a clear)
+    bool label_clean = false;
+    // this call is lean: HBM-resident plan label, timing events off, lazy rest stage
+    bool lean_call = false;
     uint64_t full_prev = 1024 * 16;  // the previous call's full-list requests (the pass's grid)
     uint32_t label_hs = 16, label_hp = 8;  // head words of S and P
     double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
@@ -5567,6 +5596,15 @@ struct ketogpu_engine {
             u_prev = 1;
         }
         const int cur = (int)(stages.size() & 1);  // the list the last stage writes
+        static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
+        // (plan label: the rest stage as lazily — label_full_kernel totals the rest list)
+        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0;
+        const EmitReq E = emit_req;
+        emit_req = EmitReq{};
+        // a lean plan-label call (run_once: HBM-resident, events off, lazy rest stage): no
+        // statistics launch, the dense pass writes the counters' mirror itself
+        const bool fused = bidi_cfg.lite == 3 && lean_call;
+        if (fused && (!lazy || E.out)) throw Error(KETOGPU_EDEVICE, "lean label call without a lazy rest stage");
         // plan label: the dense pass over the requests with an overflowing list, always (it
         // also totals the rest list for the lazy decision below: spill_count[0]); persistent,
         // its grid from the previous call's count
@@ -5575,7 +5613,7 @@ struct ketogpu_engine {
                 const unsigned fg = (unsigned)std::min<uint64_t>(std::max<uint64_t>(full_prev / 16 + 64, 64), 16384);
                 KLAUNCH((label_full_kernel<decltype(hs)::value, decltype(hp)::value>), dim3(fg), dim3(64), 0, stream,
                         lgraph, q.allowed, label_rest(q.n), label_full(q.n), &spill_count[0], &spill_count[7],
-                        st.stats + 4 * kStatSlots);
+                        fused ? nullptr : st.stats + 4 * kStatSlots, fused ? d_hctr + 16 : nullptr);
             });
         auto launch_stages = [&](uint64_t prev0) {
             for (size_t k = 0, c = 0; k < stages.size(); k++, c ^= 1)
@@ -5587,9 +5625,6 @@ struct ketogpu_engine {
         // empty persistent launches cost ~14 us per call — but only after the synchronization
         // shows spills, followed by a second statistics pass, the result copies again and a
         // second synchronization.  KETOGPU_CASCADE_EAGER=1: always up front (A/B).
-        static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
-        // (plan label: the rest stage as lazily — label_full_kernel totals the rest list)
-        const bool lazy = !eager_env && !cascade_log && stage_prev[0] == 0;
         if (!lazy) launch_stages(stage_prev[0]);
         // b == nullptr (host batches): no event between the call's kernels (each costs ~6 us of
         // GPU idle between the launches it separates); one event after the last launch
@@ -5601,11 +5636,10 @@ struct ketogpu_engine {
         static_assert(kStatsLen == 8 + 8 * kStatSlots + 12, "statistics layout");
         // (ns <= 7: KETOGPU_CASCADE allows at most 6 stages; the block holds 8 counters)
         // a pending host-batch emit rides in the same launch (blocks >= 1)
-        const EmitReq E = emit_req;
-        emit_req = EmitReq{};
         const unsigned eb = E.out ? (unsigned)std::min<uint64_t>(blocks_for(2 * E.words + 1), 255) : 0;
-        KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16,
-                12, E);
+        if (!fused)
+            KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16,
+                    12, E);
         if (before_sync) before_sync();
         if (!b) HIP_CHECK(hipEventRecord(d, stream));
         wait_stream();
@@ -5640,6 +5674,9 @@ struct ketogpu_engine {
             rs.rest_requests = cnt[0];
             rs.full_requests = cnt[7];
             full_prev = cnt[7];
+            // a lean call without rest requests touched no statistics slot and no spill
+            // counter past [0] and [7] (both written, not added to): the next call needs no clear
+            label_clean = fused && cnt[0] == 0;
         }
         for (size_t k = 0; k < stages.size() && k < 8; k++) stage_prev[k] = (uint64_t)cnt[k] * fans[k];
         rs.push_launches += launched;
@@ -5741,7 +5778,7 @@ struct ketogpu_engine {
                 const uint64_t bunits = (q.n + bidi_cfg.u - 1) / bidi_cfg.u;
                 if (!src) {
                     launch_bidi(bidi_cfg, (unsigned)bunits, lds_pad, q, nullptr, nullptr, list[0], &spill_count[0],
-                                st.stats, stamps);
+                                lean_call ? nullptr : st.stats, stamps);  // (lean: no statistics atomics)
                 } else if (direct) {
                     // pinned requests: one launch whose units read their requests in place.
                     // (Tried: only a share f of the units reading in place while load_kernel
@@ -6104,9 +6141,18 @@ struct ketogpu_engine {
             HIP_CHECK(hipEventRecord(t_begin, stream));
             light_begin = t_begin;
         }
-        // one launch zeroes results, flags, statistics and spill counters
-        KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
-                           q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen, clear_bad);
+        // one launch zeroes results, flags, statistics and spill counters — unless this is
+        // an HBM-resident plan-label call after one that left them zero (label_kernel writes
+        // every result word itself; the last call's fused reduction zeroed the statistics)
+        const bool label_resident = !src && use_units && !wave_u && use_bidi && bidi_cfg.lite == 3 && q.n;
+        static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
+        lean_call = label_resident && fuse_reduce && light_events && !eager_env && !cascade_log && stage_prev[0] == 0;
+        const bool skip_clear = lean_call && label_clean && qq.flags_zero && !clear_bad;
+        label_clean = false;
+        qq.flags_zero = false;
+        if (!skip_clear)
+            KLAUNCH(clear_kernel, dim3(64), dim3(kBlock), 0, stream, q.allowed, std::max<uint64_t>(words, 1),
+                    q.flags, std::max<uint64_t>(words, 1), st.stats, (uint64_t)kStatsLen, clear_bad);
         clear_bad = nullptr;
         // A timing event costs ~5.6 us of GPU idle between the kernels it separates
         // (kernel trace of config #2): with the bidi first stage the run starts at that
@@ -6188,6 +6234,8 @@ struct ketogpu_engine {
         HIP_CHECK(hipEventElapsedTime(&ms, t_begin, t_end));
         rs.ms_total = ms;
         last = rs;
+        // no rest request: nothing wrote a flag word (and they were zero when it started)
+        qq.flags_zero = label_resident && label_clean;
         if (stamps && use_units && !wave_u) report_stamps();
     }
 

@@ -130,6 +130,58 @@ def test_label_heads_match_oracle(heads, permille, monkeypatch):
     np.testing.assert_array_equal(check.unpack_bits(out.array.copy(), len(roots)), want)
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("n_req", [0, 1000, 1001])
+def test_label_resident_calls_repeat(n_req, fuse, monkeypatch):
+    """HBM-resident plan-label calls back to back.  After the first, a call skips the clear:
+    label_kernel writes every result word itself (16 bits per unit, the last word's tail
+    zeroed), no statistics atomics run and the dense pass writes the list totals the host
+    reads
+    (lean calls; KETOGPU_LABEL_FUSE=0: statistics, their reduction and the clear in every
+    call).  Every call's answers, the bits past n, the flag words and the per-call
+    statistics stay equal — with a host call, another batch and calls with second-stage
+    requests in between"""
+    monkeypatch.setenv("KETOGPU_UNITS", "label")
+    monkeypatch.setenv("KETOGPU_LABEL_FUSE", fuse)
+    namespaces, rows, reqs = randgraph.make_family_graph(92)
+    snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    want = np.asarray(randgraph.oracle_store(namespaces, rows).check_batch(reqs), dtype=bool)
+    roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(x)) for ns, o, r, x in reqs])
+    if n_req:
+        reps = -(-n_req // len(roots))
+        roots, targets, want = (np.tile(x, reps)[:n_req] for x in (roots, targets, want))
+    n = len(roots)
+    eng = check.Engine(snap)
+
+    def resident_ok(q, w):
+        stats = []
+        for _ in range(4):
+            q.run()
+            ab, fb = q.download_words()
+            np.testing.assert_array_equal(check.unpack_bits(ab, q.n), w)
+            if q.n % 64:
+                assert int(ab[-1]) >> (q.n % 64) == 0  # no bit past n
+            assert not fb.any()
+            st = eng.last_stats()
+            assert st["plan"] == 7
+            stats.append((st["unit_rows"], st["unit_rev"], st["rest_requests"]))
+        # (lean calls collect no statistics: with KETOGPU_LABEL_FUSE=1 every call after the
+        # first is one, so compare those)
+        assert len(set(stats if fuse == "0" else stats[1:])) == 1, stats
+    q = eng.upload(roots, targets)
+    resident_ok(q, want)
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)  # a host call in between
+    q2 = eng.upload(roots[::-1].copy(), targets[::-1].copy())
+    resident_ok(q2, want[::-1])
+    resident_ok(q, want)
+    # second-stage requests (a quarter of the S heads unlabelled): the clear is never skipped
+    monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", "250")
+    eng = check.Engine(snap)
+    q3 = eng.upload(roots, targets)
+    resident_ok(q3, want)
+    assert eng.last_stats()["rest_requests"] > 0 and n > 0
+
+
 @pytest.fixture
 def global_path(monkeypatch):
     """engines created while active use only the global multi-word path"""
