@@ -38,7 +38,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)  # ~4 ms of resident calls: the barrier inside the timed region stays small
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--small", action="store_true", help="1/100-size graph for quick runs (not the metric)")
     p.add_argument("--no-cpu-baseline", action="store_true")

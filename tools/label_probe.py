@@ -53,9 +53,14 @@ def main():
     for _ in range(2):
         q.run()
     t0 = time.perf_counter()
+    calls, gpu = [], []
     for _ in range(a.steps):
+        c0 = time.perf_counter()
         q.run()
+        calls.append(time.perf_counter() - c0)
+        gpu.append(eng.last_stats()["ms_total"])
     dt = (time.perf_counter() - t0) / a.steps
+    lean = eng.last_stats()
     eng.set_events(True)  # the first stage's own time (events between the kernels)
     ms = []
     for _ in range(a.steps):
@@ -66,7 +71,13 @@ def main():
     out = {"load_s": round(t_load, 1), "engine_s": round(t_eng, 2), "plan": st["plan"],
            "hbm_checks_per_s": round(len(roots) / dt, 1), "main_ms_median": round(float(np.median(ms)), 4),
            "main_bytes": st["main_bytes"], "label_build_ms": round(st["label_build_ms"], 1),
-           "allowed": int(q.download().sum())}
+           "allowed": int(q.download().sum()),
+           # per call: host wall time vs the GPU span between the call's first and last event
+           "call_us_median": round(float(np.median(calls)) * 1e6, 1),
+           "gpu_span_us_median": round(float(np.median(gpu)) * 1e3, 1),
+           "full_requests": st["full_requests"], "rest_requests": st["rest_requests"],
+           "lean_full_requests": lean["full_requests"],
+           "heads": f'{st["label_s_head"]},{st["label_p_head"]}', "label_bytes": st["label_bytes"]}
     if a.host:
         pr, pt = check.pinned(roots), check.pinned(targets)
         out_b = check.PinnedBuffer((len(roots) + 63) // 64, np.uint64)
