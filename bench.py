@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--small", action="store_true", help="1/100-size graph for quick runs (not the metric)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU work of the baseline sample")
+    p.add_argument("--r2-sample", type=int, default=0,
+                   help="partitioned: also diff this many uniform requests of rank 0 against oracle/r2_check.c "
+                        "(the independent R2 checker) fed from the same stream")
     p.add_argument("--parity", choices=["full", "sample"], default="full",
                    help="full: every request of the timed batch is diffed against the oracle (about 90 s of "
                         "16-thread CPU work at config #2); sample: only the baseline sample")
@@ -563,6 +566,8 @@ def main_partitioned(a, rank, world, local):
         cpu, parity = None, None
         if not a.no_cpu_baseline:
             cpu, parity = cpu_baseline_stream(w, got, a.cpu_seconds, world)
+            if a.r2_sample:
+                parity = dict(parity or {}, r2_check=r2_stream(w, got, a.r2_sample))
         pos = np.asarray(w.chk_pos, dtype=bool)[:len(got)]
         parity = dict(parity or {}, constructed_positives=int(pos.sum()),
                       constructed_positives_denied=int((pos & ~got.astype(bool)).sum()))
@@ -640,6 +645,27 @@ def cpu_baseline_stream(w, got, seconds, world):
                          f"streamed graph on {threads} threads; store build {t_build:.1f}s"}
     return cpu, {"checked": m, "of": int(len(got)), "mismatches": mism,
                  "against": "oracle/keto_oracle.c (exact restatement of internal/check/engine.go)"}
+
+
+def r2_stream(w, got, m):
+    """oracle/r2_check.c (its own interning, adjacency and bitset BFS; no code shared with
+    libketogpu) over the same row stream, on m uniform requests of `got`"""
+    from oracle import oracle as O
+    threads = host_cores()[0]
+    idx = np.random.default_rng(7).permutation(len(got))[:m]
+    t0 = time.time()
+    r2c = O.R2Checker(w.namespaces, w.requests(idx))
+    for cols in w.batches(1 << 20):
+        r2c.add_columnar(cols)
+    build = time.time() - t0
+    t0 = time.time()
+    want, ok = r2c.check(nthreads=threads)
+    out = {"against": "oracle/r2_check.c (independent R2 checker over the same stream)", "sample": int(ok.sum()),
+           "requested": int(len(idx)), "mismatches": int((want[ok] != got[idx][ok]).sum()),
+           "build_s": round(build, 1), "check_s": round(time.time() - t0, 1), "threads": threads}
+    r2c.close()
+    log(f"R2 checker: {out}")
+    return out
 
 
 def sql_baseline(seconds):
