@@ -2845,8 +2845,21 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
         const uint32_t *O = !l_over ? (walk_p ? Sl : Pl) + kHeadFixed : nl <= kFullStage ? stage[q] : Lg;
         const uint32_t *W = w_over ? Wg : (walk_p ? Pl : Sl) + kHeadFixed;
         bool hit = false;
-        if (valid)
-            for (uint32_t k = sub; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
+        if (valid) {
+            // the walked entries this lane takes (k = sub, sub + 4, ...) fetched together up
+            // front: a walked list in the overflow region costs one round trip, not one per entry
+            constexpr int kPre = 16;
+            uint32_t wk[kPre];
+#pragma unroll
+            for (int i = 0; i < kPre; i++) {
+                const uint32_t k = sub + 4 * i;
+                wk[i] = k < nw ? W[k] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < kPre; i++)
+                if (!hit && sub + 4 * i < nw) hit = label_find_n(O, nl, wk[i]);
+            for (uint32_t k = sub + 4 * kPre; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
+        }
         const uint64_t bits = __ballot(hit);
         if (valid && sub == 0) {
             if ((bits >> lane) & 0xF) atomicOr((unsigned long long *)&allowed[idx >> 6], 1ull << (idx & 63));

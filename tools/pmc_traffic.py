@@ -56,6 +56,9 @@ FAMILIES = [
     ("part_reset_kernel", r"part_reset_kernel"),
     ("part_pull_answer_kernel", r"part_pull_answer_kernel"),
     # two-tier partitioned engine (config #5)
+    ("tier_label_kernel", r"tier_label_kernel"),
+    ("tier_label exchange kernels (pairs, replies, lengths, bounds)",
+     r"tier_pair_kernel|tier_label_reply|tier_label_lens|tier_label_bounds"),
     ("tier_eval_kernel", r"tier_eval_kernel"),
     ("tier_cascade_kernel", r"tier_cascade_kernel"),
     ("tier_seed_kernel", r"tier_seed_kernel"),
