@@ -3544,10 +3544,13 @@ __device__ __forceinline__ uint32_t tier_seg(const uint64_t *first, uint32_t wor
 // the lists' lengths scanned over all received queries) writes its length at
 // j + off[qs[p]] and its list at qs[p + 1] + off[j] — the segment layout above, with no
 // per-segment pass.  One wave per 64 queries, lanes over consecutive words (like
-// tier_reply_copy_kernel).
+// tier_reply_copy_kernel), four words per lane in flight.  bnd (world 1, may be null): the
+// asker is this rank and its layout this one, so each query also writes its request's list
+// bounds (tier_label_bounds_kernel's result, no separate pass and no clearing: every request
+// has both slots)
 __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
                                                                const uint64_t *off, const uint64_t *qs, uint32_t world,
-                                                               uint32_t *out, uint64_t cap) {
+                                                               uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq) {
     __shared__ uint64_t s_pre[kTB / 64][65];
     __shared__ uint64_t s_src[kTB / 64][64];
     __shared__ uint64_t s_dst[kTB / 64][64];
@@ -3566,6 +3569,11 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
             const uint64_t h = j + off[qs[p]];
             if (h < cap) out[h] = (uint32_t)(e - b);
             dst = qs[p + 1] + off[j];
+            if (bnd && (qq.tag >> 1) < nreq) {
+                const uint64_t end = dst + (e - b);
+                reinterpret_cast<uint2 *>(&bnd[qq.tag >> 1])[side] =
+                    end <= cap ? make_uint2((uint32_t)dst, (uint32_t)end) : make_uint2(0u, 0u);
+            }
         }
         const uint64_t o0 = off[j0];
         s_pre[wv][lane] = (j < n ? off[j] : off[n]) - o0;
@@ -3575,19 +3583,32 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
         const uint64_t total = (j0 + 64 < n ? off[j0 + 64] : off[n]) - o0;
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (uint64_t o = lane; o < total; o += 64) {
-            int lo = 0, hi = 64;  // the last query whose offset is <= o owns it (empty lists never win)
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (s_pre[wv][mid] <= o)
-                    lo = mid;
-                else
-                    hi = mid;
+        for (uint64_t ob = 0; ob < total; ob += 256) {
+            uint32_t v[4];
+            uint64_t d[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t o = ob + 64 * u + lane;
+                d[u] = ~0ull;
+                v[u] = 0;
+                if (o < total) {
+                    int lo = 0, hi = 64;  // the last query whose offset is <= o owns it (empty lists never win)
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_pre[wv][mid] <= o)
+                            lo = mid;
+                        else
+                            hi = mid;
+                    }
+                    const uint64_t w = o - s_pre[wv][lo];
+                    const uint32_t *src = s_side[wv][lo] ? G.ls_col : G.lp_col;
+                    d[u] = s_dst[wv][lo] + w;
+                    v[u] = src[s_src[wv][lo] + w];
+                }
             }
-            const uint64_t w = o - s_pre[wv][lo];
-            const uint32_t *src = s_side[wv][lo] ? G.ls_col : G.lp_col;
-            const uint64_t d = s_dst[wv][lo] + w;
-            if (d < cap) out[d] = src[s_src[wv][lo] + w];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (d[u] < cap) out[d[u]] = v[u];
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -3655,8 +3676,22 @@ __global__ __launch_bounds__(64) void tier_label_kernel(tier::Graph G, tier::Eva
             ns = b.w - b.z;
         }
     }
-    for (uint32_t j = sub; j < min(np, kTierLab); j += 4) L[q][0][j] = lp[j];
-    for (uint32_t j = sub; j < min(ns, kTierLab); j += 4) L[q][1][j] = ls[j];
+    {  // both lists' first kTierLab words, every load in flight before the LDS stores
+        constexpr int kStg = kTierLab / 4;
+        uint32_t vp[kStg], vs[kStg];
+#pragma unroll
+        for (int i = 0; i < kStg; i++) {
+            const uint32_t j = sub + 4 * i;
+            vp[i] = j < np ? lp[j] : 0u;
+            vs[i] = j < ns ? ls[j] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kStg; i++) {
+            const uint32_t j = sub + 4 * i;
+            if (j < np) L[q][0][j] = vp[i];
+            if (j < ns) L[q][1][j] = vs[i];
+        }
+    }
     __syncthreads();
     bool hit = false;
     const bool valid = np >= 2 && ns >= 2;
@@ -4185,8 +4220,10 @@ void launch_seed_records(const Graph &g, const Reply *recv, uint64_t n, Rec *see
 }
 
 void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
-                        uint32_t world, uint32_t *out, uint64_t cap, hipStream_t s) {
-    if (n) KLAUNCH(tier_label_reply_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, qs, world, out, cap);
+                        uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq, hipStream_t s) {
+    if (n)
+        KLAUNCH(tier_label_reply_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, qs, world, out, cap, bnd,
+                nreq);
 }
 
 void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
@@ -5654,7 +5691,7 @@ struct ketogpu_engine {
             KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(), d_hctr + 16,
                     12, E);
         if (before_sync) before_sync();
-        if (!b) HIP_CHECK(hipEventRecord(d, stream));
+        if (!b && !lean_call) HIP_CHECK(hipEventRecord(d, stream));
         wait_stream();
         const unsigned int *cnt = (const unsigned int *)(h_ctr + 24);
         size_t launched = lazy ? 1 : stages.size() + 1;
@@ -5664,7 +5701,7 @@ struct ketogpu_engine {
             KLAUNCH(stats_reduce_kernel, dim3(1 + eb), dim3(kBlock), 0, stream, st.stats + 8, 2, stat_out(),
                     d_hctr + 16, 12, E);
             if (before_sync) before_sync();
-            HIP_CHECK(hipEventRecord(d, stream));
+            if (!lean_call) HIP_CHECK(hipEventRecord(d, stream));
             wait_stream();
             launched = stages.size() + 2;
         }
@@ -5672,7 +5709,7 @@ struct ketogpu_engine {
         if (b) {
             unit_ev.push_back({a, b});
             unit_ev.push_back({b, d});
-        } else {
+        } else if (!lean_call) {
             unit_ev.push_back({a, d});
         }
         const uint64_t *t = (const uint64_t *)h_ctr + 16;
@@ -6149,17 +6186,20 @@ struct ketogpu_engine {
         uint64_t words = (q.n + 63) / 64;
         // host batches: the run's begin event ahead of the clear launch (no event between
         // the call's kernels, KETOGPU_EVENTS=all restores them)
-        light_begin = nullptr;
-        if (light_events && (src || (use_units && !wave_u && use_bidi && q.n && bidi_cfg.lite == 3))) {
-            HIP_CHECK(hipEventRecord(t_begin, stream));
-            light_begin = t_begin;
-        }
-        // one launch zeroes results, flags, statistics and spill counters — unless this is
-        // an HBM-resident plan-label call after one that left them zero (label_kernel writes
-        // every result word itself; the last call's fused reduction zeroed the statistics)
+        // a lean call (HBM-resident plan label, events off: see lean_call) records no timing
+        // event at all; its ms_total is the host's clock around the call
         const bool label_resident = !src && use_units && !wave_u && use_bidi && bidi_cfg.lite == 3 && q.n;
         static const bool eager_env = getenv("KETOGPU_CASCADE_EAGER") != nullptr;
         lean_call = label_resident && fuse_reduce && light_events && !eager_env && !cascade_log && stage_prev[0] == 0;
+        const auto h0 = std::chrono::steady_clock::now();
+        light_begin = nullptr;
+        if (light_events && (src || (use_units && !wave_u && use_bidi && q.n && bidi_cfg.lite == 3))) {
+            if (!lean_call) HIP_CHECK(hipEventRecord(t_begin, stream));
+            light_begin = t_begin;  // (lean: never recorded, never read)
+        }
+        // one launch zeroes results, flags, statistics and spill counters — unless this is
+        // a lean call after one that left them zero (label_kernel writes every result word
+        // itself, a lean call adds no statistics)
         const bool skip_clear = lean_call && label_clean && qq.flags_zero && !clear_bad;
         label_clean = false;
         qq.flags_zero = false;
@@ -6175,7 +6215,7 @@ struct ketogpu_engine {
         std::vector<std::pair<hipEvent_t, hipEvent_t>> unit_ev;
         if (use_units && q.n) {
             uint64_t ns = run_units(q, rs, unit_ev, src, before_sync);
-            if (bidi_first) {
+            if (bidi_first && !lean_call) {
                 if (!unit_ev.empty())
                     t_begin = unit_ev.front().first;
                 else
@@ -6244,7 +6284,10 @@ struct ketogpu_engine {
             HIP_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
             rs.ms_pull += ms;
         }
-        HIP_CHECK(hipEventElapsedTime(&ms, t_begin, t_end));
+        if (lean_call)
+            ms = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+        else
+            HIP_CHECK(hipEventElapsedTime(&ms, t_begin, t_end));
         rs.ms_total = ms;
         last = rs;
         // no rest request: nothing wrote a flag word (and they were zero when it started)

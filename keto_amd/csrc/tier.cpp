@@ -654,10 +654,9 @@ struct TierDevice : TierSteps {
                 const uint64_t cap = d_rep.cap / 4;
                 uint32_t *rep = (uint32_t *)d_rep.ensure(4 * std::max<uint64_t>(nq, 1));
                 const uint64_t cap_now = std::max(cap, d_rep.cap / 4);
-                tier::launch_label_reply(G, q, nq, lens, qs, 1, rep, cap_now, stream);
+                // (the replies' pass also writes every request's bounds: one owner, one layout)
+                tier::launch_label_reply(G, q, nq, lens, qs, 1, rep, cap_now, bnd, n, stream);
                 THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
-                THIP(hipMemsetAsync(bnd, 0, 16 * std::max<uint64_t>(n, 1), stream));
-                tier::launch_label_bounds(q, nq, qs, lens, 1, bnd, n, cap_now, stream);
                 THIP(hipEventRecord(ev0, stream));
                 tier::launch_label_eval(G, E, rep, stream);
                 THIP(hipEventRecord(ev1, stream));
@@ -697,7 +696,7 @@ struct TierDevice : TierSteps {
             THIP(hipSetDevice(dev));
             if (G.label)
                 tier::launch_label_reply(G, rq, rq_n, (const uint64_t *)d_lens.p, (const uint64_t *)(d_small + kQs), G.world,
-                                         (uint32_t *)send, cap, stream);
+                                         (uint32_t *)send, cap, nullptr, 0, stream);
             else
                 tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
         });

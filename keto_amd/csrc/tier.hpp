@@ -92,8 +92,9 @@ void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_li
 //           list (x, y) and S list (z, w); bnd cleared by the caller; a list ending past
 //           cap received words: left empty) -> launch_label_eval
 // launch_label_eval: recv_label null: the rank owns every node and reads its own lists
+// bnd (world 1, else null): the replies' own bounds per request, written by the same pass
 void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
-                        uint32_t world, uint32_t *out, uint64_t cap, hipStream_t s);
+                        uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq, hipStream_t s);
 void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
                        uint64_t *lens, hipStream_t s);
 void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
