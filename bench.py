@@ -463,7 +463,9 @@ def main_partitioned(a, rank, world, local):
         dev_req = [torch.from_numpy(np.ascontiguousarray(x[mine]).view(np.int32)).to(f"cuda:{local}")
                    for x in (roots, targets)]
         torch.cuda.synchronize()
-        bits = np.zeros((per_gpu + 63) // 64, dtype=np.uint64)
+        # answers into pinned words (ketogpu_host_alloc), as the serving integration hands over
+        bits_buf = check.PinnedBuffer((per_gpu + 63) // 64, np.uint64)
+        bits = bits_buf.array
 
         def step():
             eng.check_ids_ptr(dev_req[0].data_ptr(), dev_req[1].data_ptr(), per_gpu, bits)

@@ -3366,14 +3366,17 @@ __device__ __forceinline__ void tier_row(const tier::Graph &G, const tier::Query
     }
 }
 
+// srcb (may be null): each row's / list's first entry too, so the copy pass reads it
+// sequentially instead of looking the owned node's offsets up again
 __global__ __launch_bounds__(kTB) void tier_reply_len_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
-                                                             uint64_t *lens, unsigned long long *bad) {
+                                                             uint64_t *lens, unsigned long long *bad, uint64_t *srcb) {
     for (uint64_t j = (uint64_t)blockIdx.x * kTB + threadIdx.x; j < n; j += (uint64_t)gridDim.x * kTB) {
         uint64_t b, e;
         bool miss;
         tier_row(G, q[j], b, e, miss);
         if (miss) atomicMin(bad, (unsigned long long)j);
         lens[j] = e - b;
+        if (srcb) srcb[j] = b;
     }
 }
 
@@ -3549,8 +3552,9 @@ __device__ __forceinline__ uint32_t tier_seg(const uint64_t *first, uint32_t wor
 // bounds (tier_label_bounds_kernel's result, no separate pass and no clearing: every request
 // has both slots)
 __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, const tier::Query *q, uint64_t n,
-                                                               const uint64_t *off, const uint64_t *qs, uint32_t world,
-                                                               uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq) {
+                                                               const uint64_t *off, const uint64_t *srcb, const uint64_t *qs,
+                                                               uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd,
+                                                               uint64_t nreq) {
     __shared__ uint64_t s_pre[kTB / 64][65];
     __shared__ uint64_t s_src[kTB / 64][64];
     __shared__ uint64_t s_dst[kTB / 64][64];
@@ -3561,9 +3565,9 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
         uint64_t b = 0, e = 0, dst = 0;
         uint32_t side = 0;
         if (j < n) {
-            bool miss;
             const tier::Query qq = q[j];
-            tier_row(G, qq, b, e, miss);
+            b = srcb[j];  // (tier_reply_len_kernel's lookup of the list)
+            e = b + (off[j + 1] - off[j]);
             side = qq.tag & 1u;
             const uint32_t p = tier_seg(qs, world, j);
             const uint64_t h = j + off[qs[p]];
@@ -4198,8 +4202,26 @@ void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t 
 }
 
 void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *lens, unsigned long long *bad,
-                          hipStream_t s) {
-    if (n) KLAUNCH(tier_reply_len_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, q, n, lens, bad);
+                          hipStream_t s, uint64_t *srcb) {
+    if (n) KLAUNCH(tier_reply_len_kernel, dim3(tier_grid(n, kTB * 4)), dim3(kTB), 0, s, g, q, n, lens, bad, srcb);
+}
+
+// the step's answers and status words straight into host-mapped memory (one launch instead
+// of a copy each): bits (may be null) the caller's pinned answer words, h_* device views of
+// the steps' pinned status words (total may be null)
+__global__ __launch_bounds__(kTB) void tier_emit_kernel(const uint64_t *allowed, uint64_t words, uint64_t *bits,
+                                                        const unsigned long long *status, const uint64_t *total,
+                                                        unsigned long long *h_status, uint64_t *h_total) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kTB)
+        bits[i] = allowed[i];
+    if (blockIdx.x == 0 && threadIdx.x < 2) h_status[threadIdx.x] = status[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 2 && total) *h_total = *total;
+}
+
+void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, const unsigned long long *status,
+                 const uint64_t *total, unsigned long long *h_status, uint64_t *h_total, hipStream_t s) {
+    KLAUNCH(tier_emit_kernel, dim3(tier_grid(std::max<uint64_t>(words, 1), kTB, 64)), dim3(kTB), 0, s, allowed,
+            bits ? words : 0, bits, status, total, h_status, h_total);
 }
 
 void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s) {
@@ -4219,11 +4241,12 @@ void launch_seed_records(const Graph &g, const Reply *recv, uint64_t n, Rec *see
     if (n) KLAUNCH(tier_seed_kernel, dim3(tier_grid(n, kTB * kSeedPer)), dim3(kTB), 0, s, g, recv, n, seed, bnd, nreq);
 }
 
-void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
-                        uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq, hipStream_t s) {
+void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *srcb,
+                        const uint64_t *qs, uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq,
+                        hipStream_t s) {
     if (n)
-        KLAUNCH(tier_label_reply_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, qs, world, out, cap, bnd,
-                nreq);
+        KLAUNCH(tier_label_reply_kernel, dim3(tier_grid(n, kTB)), dim3(kTB), 0, s, g, q, n, off, srcb, qs, world, out, cap,
+                bnd, nreq);
 }
 
 void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
@@ -4315,7 +4338,8 @@ namespace ketogpu {
 // hipHostMalloc / hipHostRegister; or device memory of `device`), else nullptr (the
 // caller has made `device` current)
 // (pageable memory goes through DMA copies).
-const void *host_view(const void *p, int device, bool query) {
+const void *host_view(const void *p, int device, bool query, bool *is_device) {
+    if (is_device) *is_device = false;
     if (!p) return nullptr;
     {  // buffers of ketogpu_host_alloc (portable + mapped): the view of THIS device,
        // known without a runtime query (~10 us per call) after its first use here
@@ -4352,6 +4376,7 @@ const void *host_view(const void *p, int device, bool query) {
     }
     if (!at.devicePointer) return nullptr;
     if (at.type == hipMemoryTypeDevice && at.device != device) return nullptr;
+    if (is_device) *is_device = at.type == hipMemoryTypeDevice;
     if (at.type != hipMemoryTypeHost && at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeUnified &&
         at.type != hipMemoryTypeManaged)
         return nullptr;

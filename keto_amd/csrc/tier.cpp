@@ -271,10 +271,11 @@ struct TierDevice : TierSteps {
     bool force_overflow = false;
     std::string err;
     // per-step scratch (grown on demand)
-    Buf d_req, d_lens, d_scan, d_bnd, d_seed, d_bits, d_list[3];
+    Buf d_req, d_lens, d_scan, d_bnd, d_seed, d_bits, d_list[3], d_srcb;
     unsigned long long *d_small = nullptr;  // [0..63] counts, [64..127] cursors, [128] first_bad, [129] bad query,
                                             // [130..132] list counts, [136..] stats, [kSeg..] label segments
     uint64_t *h_small = nullptr;            // pinned mirror
+    uint64_t *d_hsmall = nullptr;           // its device view (tier_emit_kernel writes the status words there)
     // the current step's requests (device-readable) and replies in flight
     const uint32_t *cur_r = nullptr, *cur_t = nullptr, *src_r = nullptr, *src_t = nullptr;
     uint64_t cur_n = 0;
@@ -305,7 +306,8 @@ struct TierDevice : TierSteps {
             (void)hipSetDevice(dev);
             (void)hipStreamSynchronize(stream);
         }
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep})
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep,
+                       &d_srcb})
             b->release();
         for (void *p : owned) (void)hipFree(p);
         for (hipEvent_t e : {ev0, ev1})
@@ -373,13 +375,15 @@ struct TierDevice : TierSteps {
         THIP(hipEventCreate(&ev0));
         THIP(hipEventCreate(&ev1));
         THIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep}) {
+        for (Buf *b : {&d_req, &d_lens, &d_scan, &d_bnd, &d_seed, &d_bits, &d_list[0], &d_list[1], &d_list[2], &d_q, &d_rep,
+                       &d_srcb}) {
             b->device = true;
             b->dev = dev;
         }
         THIP(hipMalloc(&d_small, kSmall * 8));
         THIP(hipMemset(d_small, 0, kSmall * 8));
         THIP(hipHostMalloc((void **)&h_small, kSmall * 8, hipHostMallocDefault));
+        THIP(hipHostGetDevicePointer((void **)&d_hsmall, h_small, 0));
         G.world = v.world;
         G.rank = v.rank;
         G.Ni = v.num_interior;
@@ -504,10 +508,11 @@ struct TierDevice : TierSteps {
         src_r = r;
         src_t = t;
         cur_n = n;
-        cur_r = (const uint32_t *)host_view(r, dev, true);
-        cur_t = cur_r ? (const uint32_t *)host_view(t, dev, true) : nullptr;
+        bool dr = false, dt = false;
+        cur_r = (const uint32_t *)host_view(r, dev, true, &dr);
+        cur_t = cur_r ? (const uint32_t *)host_view(t, dev, true, &dt) : nullptr;
         in_place = cur_r && cur_t;
-        req_hbm = in_place && device_memory(r) && device_memory(t);
+        req_hbm = in_place && dr && dt;
         if (!in_place) {
             uint32_t *d = (uint32_t *)d_req.ensure(8 * std::max<uint64_t>(n, 1));
             if (n) {
@@ -572,7 +577,8 @@ struct TierDevice : TierSteps {
             uint64_t *lens = (uint64_t *)d_lens.ensure(8 * (n + 1));
             uint64_t *scr = (uint64_t *)d_scan.ensure(8 * (n / 1024 + 2));
             THIP(hipMemsetAsync(d_small + kBadQuery, 0xFF, 8, stream));
-            tier::launch_reply_lengths(G, recv, n, lens, d_small + kBadQuery, stream);
+            tier::launch_reply_lengths(G, recv, n, lens, d_small + kBadQuery, stream,
+                                       G.label ? (uint64_t *)d_srcb.ensure(8 * std::max<uint64_t>(n, 1)) : nullptr);
             tier::launch_scan(lens, n, scr, stream);
             // the offsets at the sources' boundaries: records per destination
             uint64_t at = 0;
@@ -636,7 +642,8 @@ struct TierDevice : TierSteps {
                 cur_r = stage;
                 cur_t = stage + n;
             }
-            tier::launch_reply_lengths(G, q, nq, lens, d_small + kBadQuery, stream);
+            uint64_t *srcb = (uint64_t *)d_srcb.ensure(8 * std::max<uint64_t>(nq, 1));
+            tier::launch_reply_lengths(G, q, nq, lens, d_small + kBadQuery, stream, srcb);
             tier::launch_scan(lens, nq, scr, stream);
             h_small[kQs] = 0;
             h_small[kQs + 1] = nq;
@@ -655,14 +662,17 @@ struct TierDevice : TierSteps {
                 uint32_t *rep = (uint32_t *)d_rep.ensure(4 * std::max<uint64_t>(nq, 1));
                 const uint64_t cap_now = std::max(cap, d_rep.cap / 4);
                 // (the replies' pass also writes every request's bounds: one owner, one layout)
-                tier::launch_label_reply(G, q, nq, lens, qs, 1, rep, cap_now, bnd, n, stream);
+                tier::launch_label_reply(G, q, nq, lens, srcb, qs, 1, rep, cap_now, bnd, n, stream);
                 THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
                 THIP(hipEventRecord(ev0, stream));
                 tier::launch_label_eval(G, E, rep, stream);
                 THIP(hipEventRecord(ev1, stream));
-                if (words) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
-                THIP(hipMemcpyAsync(h_small + kFirstBad, d_small + kFirstBad, 16, hipMemcpyDeviceToHost, stream));
-                THIP(hipMemcpyAsync(h_small + kLists, lens + nq, 8, hipMemcpyDeviceToHost, stream));
+                // answers (into pinned caller words in place, else one copy) and the status
+                // words by one launch
+                uint64_t *vbits = words ? (uint64_t *)host_view(bits, dev, false) : nullptr;
+                tier::launch_emit(allowed, words, vbits, d_small + kFirstBad, lens + nq,
+                                  (unsigned long long *)d_hsmall + kFirstBad, d_hsmall + kLists, stream);
+                if (words && !vbits) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
                 THIP(hipStreamSynchronize(stream));  // the step's one wait
                 if (h_small[kBadQuery] != ~0ull)
                     throw Error(KETOGPU_EINVAL, "a query for a node this rank does not own (query " +
@@ -695,8 +705,9 @@ struct TierDevice : TierSteps {
         return guarded("two-tier replies", [&] {
             THIP(hipSetDevice(dev));
             if (G.label)
-                tier::launch_label_reply(G, rq, rq_n, (const uint64_t *)d_lens.p, (const uint64_t *)(d_small + kQs), G.world,
-                                         (uint32_t *)send, cap, nullptr, 0, stream);
+                tier::launch_label_reply(G, rq, rq_n, (const uint64_t *)d_lens.p, (const uint64_t *)d_srcb.p,
+                                         (const uint64_t *)(d_small + kQs), G.world, (uint32_t *)send, cap, nullptr, 0,
+                                         stream);
             else
                 tier::launch_reply_copy(G, rq, rq_n, (const uint64_t *)d_lens.p, send, cap, stream);  // stream-ordered
         });

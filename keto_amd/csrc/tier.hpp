@@ -23,7 +23,8 @@ namespace ketogpu {
 
 // device_engine.hip: `device`'s view of host memory it can read in place (pinned), else
 // nullptr
-const void *host_view(const void *p, int device, bool query);
+// is_device (may be null): set when p is memory of `device` itself (HBM)
+const void *host_view(const void *p, int device, bool query, bool *is_device = nullptr);
 
 namespace tier {
 
@@ -93,8 +94,10 @@ void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_li
 //           cap received words: left empty) -> launch_label_eval
 // launch_label_eval: recv_label null: the rank owns every node and reads its own lists
 // bnd (world 1, else null): the replies' own bounds per request, written by the same pass
-void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *qs,
-                        uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq, hipStream_t s);
+// srcb: each list's first word in lp_col / ls_col (launch_reply_lengths)
+void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *srcb,
+                        const uint64_t *qs, uint32_t world, uint32_t *out, uint64_t cap, uint4 *bnd, uint64_t nreq,
+                        hipStream_t s);
 void launch_label_lens(const uint32_t *recv, uint64_t nsent, const uint64_t *sq, const uint64_t *rp, uint32_t world,
                        uint64_t *lens, hipStream_t s);
 void launch_label_bounds(const Query *sent, uint64_t nsent, const uint64_t *sq, const uint64_t *g, uint32_t world,
@@ -115,8 +118,13 @@ void launch_query_scatter(const Graph &g, const uint32_t *roots, const uint32_t 
 // replies: the rows the received queries ask for, in query order (so grouped like the
 // queries' sources); `lens` scratch of n + 1 entries, *total the number of records
 // (device word), written with pad = the query's tag
+// srcb (may be null): each row's / list's first entry (label replies read it back)
 void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *lens, unsigned long long *bad,
-                          hipStream_t s);
+                          hipStream_t s, uint64_t *srcb = nullptr);
+// answers into the caller's pinned words (bits may be null) and the status words into the
+// steps' pinned ones, one launch (tier_emit_kernel)
+void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, const unsigned long long *status,
+                 const uint64_t *total, unsigned long long *h_status, uint64_t *h_total, hipStream_t s);
 void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s);  // exclusive, in place, v[n] = total
 void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Reply *out, uint64_t cap,
                        hipStream_t s);

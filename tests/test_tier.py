@@ -347,6 +347,11 @@ def test_tier_device_rccl_world1_matches_oracle(loop_self, one_wait, label, monk
     roots, targets, status = sh.resolve_batch(w.request_batch(), comm)
     eng = TieredEngine(sh, device=0, comm=comm, max_batch=4096)
     np.testing.assert_array_equal(eng.check_ids(roots, targets), want)
+    # answers into pinned words (written in place by the emit launch at world 1)
+    from keto_amd import check
+    pb = check.PinnedBuffer((len(roots) + 63) // 64, np.uint64)
+    eng.check_ids_raw(np.ascontiguousarray(roots, np.uint32), np.ascontiguousarray(targets, np.uint32), pb.array)
+    np.testing.assert_array_equal(check.unpack_bits(pb.array.copy(), len(roots)), want)
     s = eng.stats()
     assert s["queries_sent"] > 0 and s["records_sent"] == s["records_received"] > 0
     _check_mode(s, label)
