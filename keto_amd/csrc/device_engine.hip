@@ -2531,7 +2531,8 @@ struct LabelRest {
     uint32_t *list;                    // request indices (the rest list)
     unsigned int *count, *next_count;  // this call's counters, the next call's (cleared here)
     uint64_t cap;                      // entries per region
-    uint4 *rec = nullptr;              // the full list: {request, root, target, 0} records
+    uint4 *rec = nullptr;              // the full list: two records per request, {request, root, target,
+                                       // |S|} and {|P|, S overflow start / 16, P overflow start / 16, 0}
 };
 // A request's two heads in LDS, as read (word k of the head at position k; the entries
 // from word 4), rows of HS + 4 / HP + 4 words: 16-byte aligned, and the 16 requests' rows
@@ -2688,13 +2689,19 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
             hit = label_meet<SW>(Pl + kHeadFixed, ep, c);
         }
     }
-    // 2. a request with an overflowing list and no hit yet: listed for label_full_kernel
+    // 2. a request with an overflowing list and no hit yet: listed for label_full_kernel,
+    //    with both counts and overflow starts (the dense pass then needs no head again)
     {
         const uint64_t hb = __ballot(hit);
+        const uint32_t os = label_word<SW, 1>(sw), op = label_word<PW, 1>(pw);
         const bool full = sub == 0 && labelled && !((hb >> (lane & ~3u)) & 0xF) &&
                           (ns > (uint32_t)(HS - kHeadFixed) || np > (uint32_t)(HP - kHeadFixed));
         const uint32_t at = lds_append(full, F.count + shard * kRestStride);
-        if (full) F.rec[shard * F.cap + at] = make_uint4((uint32_t)(unit * 16 + q), r, t, 0u);
+        if (full) {
+            uint4 *rec = F.rec + 2 * (shard * F.cap + at);
+            rec[0] = make_uint4((uint32_t)(unit * 16 + q), r, t, ns);
+            rec[1] = make_uint4(np, os, op, 0u);
+        }
     }
     uint32_t looked = 0;
     const uint64_t bits = __ballot(hit);
@@ -2774,14 +2781,15 @@ __global__ __launch_bounds__(256) void label_host_kernel(DevGraph g, LabelGraph 
 }
 
 // The dense second pass over the requests the first stage left open with an overflowing
-// list (F, request indices): gathered 16 to a wave, four lanes per request, persistent.
-// Each request's heads are read again, its longer list is staged in LDS (up to
-// kFullStage words; one dependent read: the four lanes' loads are independent) and the
-// shorter one walked and binary-searched in it.
+// list (F: two records per request carrying both counts and overflow starts): gathered 16
+// to a wave, four lanes per request, persistent.  Both lists' places are known from the
+// records, so one dependent read follows them: the longer list is staged in LDS (up to
+// kFullStage words, from its overflow region or its head's inline entries) while the
+// shorter one's entries are fetched into registers, then binary-searched.
 constexpr uint32_t kFullStage = 256;
 // Workgroup 0 also totals both lists' shard counts for the host (totals[0]: the rest list,
 // totals[1]: this list), so the rest stage can be launched only when it has requests.
-// Lean HBM-resident calls (plan label, timing events off, KETOGPU_LABEL_FUSE=1): the first
+// Lean resident calls (plan label, timing events off, KETOGPU_LABEL_FUSE=1): the first
 // stage and this pass run without statistics atomics (stats == nullptr: the statistics are
 // diagnostics, collected by the same calls with events on), and workgroup 0 writes the two
 // list totals straight into the host-mapped mirror (`mirror`: the words stats_reduce_kernel
@@ -2791,10 +2799,8 @@ template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *allowed, LabelRest R, LabelRest F,
                                                         unsigned int *total_rest, unsigned int *total_full,
                                                         unsigned long long *stats, unsigned long long *mirror) {
-    __shared__ LabelShared<HS, HP> sh;
     __shared__ alignas(16) uint32_t stage[16][kFullStage];
     const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
-    constexpr int SW = HS / 4, PW = HP / 4;
     const uint32_t c = F.count[lane * kRestStride];
     const uint32_t nu = (c + 15) / 16;
     const uint32_t incl = wave_incl_sum_u32(nu);
@@ -2811,50 +2817,40 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
         const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)(incl - nu), (int)shard);
         const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)shard);
         const uint64_t j = (u - first) * 16 + (lane & 15);
-        uint4 rec = make_uint4(KETOGPU_NODE_NONE, 0, 0, 0);
-        if (lane < 16 && j < cs) rec = F.rec[shard * F.cap + j];
-        const uint32_t idx = (uint32_t)__shfl((int)rec.x, (int)q, 64);
-        const uint32_t rr = (uint32_t)__shfl((int)rec.y, (int)q, 64), tt = (uint32_t)__shfl((int)rec.z, (int)q, 64);
-        const bool valid = idx != KETOGPU_NODE_NONE;
-        uint32_t sw[SW], pw[PW];
-#pragma unroll
-        for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
-#pragma unroll
-        for (int k = 0; k < PW; k++) pw[k] = 0xFFFFFFFFu;
-        if (valid) {
-            label_head_load<SW>(L.S + (uint64_t)tt * HS, sub, sw);
-            label_head_load<PW>(L.P + (uint64_t)rr * HP, sub, pw);
+        uint4 r0 = make_uint4(KETOGPU_NODE_NONE, 0, 0, 0), r1 = make_uint4(0, 0, 0, 0);
+        if (lane < 16 && j < cs) {
+            const uint4 *rec = F.rec + 2 * (shard * F.cap + j);
+            r0 = rec[0];
+            r1 = rec[1];
         }
-        const uint32_t ns = label_word<SW, 0>(sw), np = label_word<PW, 0>(pw);
-        const uint32_t *Sg = L.S + (uint64_t)label_word<SW, 1>(sw) * 16;
-        const uint32_t *Pg = L.P + (uint64_t)label_word<PW, 1>(pw) * 16;
-        uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
-        label_to_lds<SW>(Sl, sw, sub);
-        label_to_lds<PW>(Pl, pw, sub);
+        const uint32_t idx = (uint32_t)__shfl((int)r0.x, (int)q, 64);
+        const uint32_t rr = (uint32_t)__shfl((int)r0.y, (int)q, 64), tt = (uint32_t)__shfl((int)r0.z, (int)q, 64);
+        const uint32_t ns = (uint32_t)__shfl((int)r0.w, (int)q, 64), np = (uint32_t)__shfl((int)r1.x, (int)q, 64);
+        const uint32_t os = (uint32_t)__shfl((int)r1.y, (int)q, 64), op = (uint32_t)__shfl((int)r1.z, (int)q, 64);
+        const bool valid = idx != KETOGPU_NODE_NONE;
+        // each list: its overflow region when it overflows its head, else the head's entries
+        const bool s_over = ns > (uint32_t)(HS - kHeadFixed), p_over = np > (uint32_t)(HP - kHeadFixed);
+        const uint32_t *Sg = s_over ? L.S + (uint64_t)os * 16 : L.S + (uint64_t)tt * HS + kHeadFixed;
+        const uint32_t *Pg = p_over ? L.P + (uint64_t)op * 16 : L.P + (uint64_t)rr * HP + kHeadFixed;
         const bool walk_p = np <= ns;
         const uint32_t nw = walk_p ? np : ns, nl = walk_p ? ns : np;
-        const bool l_over = walk_p ? ns > (uint32_t)(HS - kHeadFixed) : np > (uint32_t)(HP - kHeadFixed);
-        const bool w_over = walk_p ? np > (uint32_t)(HP - kHeadFixed) : ns > (uint32_t)(HS - kHeadFixed);
-        const uint32_t *Lg = walk_p ? Sg : Pg, *Wg = walk_p ? Pg : Sg;
-        // the longer list: staged from its overflow region (whole 16-word units: the uint4
-        // reads stay inside), else its head image
-        if (valid && l_over && nl <= kFullStage)
+        const uint32_t *Lg = walk_p ? Sg : Pg, *W = walk_p ? Pg : Sg;
+        // (16-byte units: an overflow region is 16-word aligned, a head's entries start 16
+        // bytes into a 32-byte aligned head and are padded to a multiple of 4 words)
+        if (valid && nl <= kFullStage)
             for (uint32_t i = sub; i * 4 < nl; i += 4)
                 reinterpret_cast<uint4 *>(stage[q])[i] = reinterpret_cast<const uint4 *>(Lg)[i];
+        constexpr int kPre = 16;  // the walked entries this lane takes, fetched together
+        uint32_t wk[kPre];
+#pragma unroll
+        for (int i = 0; i < kPre; i++) {
+            const uint32_t k = sub + 4 * i;
+            wk[i] = valid && k < nw ? W[k] : 0u;
+        }
         wave_sync();
-        const uint32_t *O = !l_over ? (walk_p ? Sl : Pl) + kHeadFixed : nl <= kFullStage ? stage[q] : Lg;
-        const uint32_t *W = w_over ? Wg : (walk_p ? Pl : Sl) + kHeadFixed;
+        const uint32_t *O = nl <= kFullStage ? stage[q] : Lg;
         bool hit = false;
         if (valid) {
-            // the walked entries this lane takes (k = sub, sub + 4, ...) fetched together up
-            // front: a walked list in the overflow region costs one round trip, not one per entry
-            constexpr int kPre = 16;
-            uint32_t wk[kPre];
-#pragma unroll
-            for (int i = 0; i < kPre; i++) {
-                const uint32_t k = sub + 4 * i;
-                wk[i] = k < nw ? W[k] : 0u;
-            }
 #pragma unroll
             for (int i = 0; i < kPre; i++)
                 if (!hit && sub + 4 * i < nw) hit = label_find_n(O, nl, wk[i]);
@@ -4437,7 +4433,7 @@ struct ketogpu_engine {
                          rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards),
                          full_rec};
     }
-    uint4 *full_rec = nullptr;  // plan label's full list: {request, root, target, 0} per request (spill_cap)
+    uint4 *full_rec = nullptr;  // plan label's full list: two records per request (2 x spill_cap, LabelRest::rec)
     // KETOGPU_LABEL_FUSE=0: no lean calls (statistics, their reduction and the clear in
     // every call; A/B)
     bool fuse_reduce = [] {
@@ -5619,7 +5615,7 @@ struct ketogpu_engine {
         spill_cap = std::max<uint64_t>(n + 2048, 1024);
         spill_units = dalloc<uint32_t>(2 * spill_cap);  // two ping-pong lists
         if (full_rec) (void)hipFree(full_rec);
-        full_rec = dalloc<uint4>(spill_cap);
+        full_rec = dalloc<uint4>(2 * spill_cap);  // two records per listed request
         spill_roots = dalloc<uint32_t>(spill_cap);
         spill_targets = dalloc<uint32_t>(spill_cap);
         spill_allowed = dalloc<uint64_t>(spill_cap / 64 + 1);
