@@ -3543,7 +3543,7 @@ __device__ __forceinline__ uint32_t tier_seg(const uint64_t *first, uint32_t wor
 // the lists' lengths scanned over all received queries) writes its length at
 // j + off[qs[p]] and its list at qs[p + 1] + off[j] — the segment layout above, with no
 // per-segment pass.  One wave per 64 queries, lanes over consecutive words (like
-// tier_reply_copy_kernel), four words per lane in flight.  bnd (world 1, may be null): the
+// tier_reply_copy_kernel), eight words per lane in flight.  bnd (world 1, may be null): the
 // asker is this rank and its layout this one, so each query also writes its request's list
 // bounds (tier_label_bounds_kernel's result, no separate pass and no clearing: every request
 // has both slots)
@@ -3583,11 +3583,12 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
         const uint64_t total = (j0 + 64 < n ? off[j0 + 64] : off[n]) - o0;
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (uint64_t ob = 0; ob < total; ob += 256) {
-            uint32_t v[4];
-            uint64_t d[4];
+        constexpr int kU = 8;  // words per lane in flight
+        for (uint64_t ob = 0; ob < total; ob += 64 * kU) {
+            uint32_t v[kU];
+            uint64_t d[kU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < kU; u++) {
                 const uint64_t o = ob + 64 * u + lane;
                 d[u] = ~0ull;
                 v[u] = 0;
@@ -3607,7 +3608,7 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < kU; u++)
                 if (d[u] < cap) out[d[u]] = v[u];
         }
         __builtin_amdgcn_wave_barrier();
@@ -3651,11 +3652,13 @@ __global__ __launch_bounds__(64) void tier_label_kernel(tier::Graph G, tier::Eva
     __shared__ uint32_t L[16][2][kTierLab];
     const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
     const uint64_t c = (uint64_t)blockIdx.x * 16 + q;
-    uint32_t r, t;
-    tier_request(G, E, c, r, t);
+    uint32_t r = KETOGPU_NODE_NONE, t = KETOGPU_NODE_NONE;
+    // exchange mode: the query passes validated the ids (first_bad) and sent nothing for a
+    // request without an answer (its bounds stay empty): the bounds are the first read
+    if constexpr (DIRECT) tier_request(G, E, c, r, t);
     const uint32_t *lp = nullptr, *ls = nullptr;
     uint32_t np = 0, ns = 0;
-    if (r != KETOGPU_NODE_NONE) {
+    if (DIRECT ? r != KETOGPU_NODE_NONE : c < E.n) {
         if constexpr (DIRECT) {
             const uint32_t lr = tier_local(G, r), lt = tier_local(G, t);
             if (lr != KETOGPU_NODE_NONE && lr < G.Nxl) {
