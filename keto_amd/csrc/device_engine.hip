@@ -3565,10 +3565,12 @@ __global__ __launch_bounds__(kTB) void tier_label_reply_kernel(tier::Graph G, co
             b = srcb[j];  // (tier_reply_len_kernel's lookup of the list)
             e = b + (off[j + 1] - off[j]);
             side = qq.tag & 1u;
-            const uint32_t p = tier_seg(qs, world, j);
-            const uint64_t h = j + off[qs[p]];
+            // (world 1: one segment, qs = {0, n} — not read from memory)
+            const uint32_t p = world == 1 ? 0u : tier_seg(qs, world, j);
+            const uint64_t q0 = world == 1 ? 0 : qs[p], q1 = world == 1 ? n : qs[p + 1];
+            const uint64_t h = j + off[q0];
             if (h < cap) out[h] = (uint32_t)(e - b);
-            dst = qs[p + 1] + off[j];
+            dst = q1 + off[j];
             if (bnd && (qq.tag >> 1) < nreq) {
                 const uint64_t end = dst + (e - b);
                 reinterpret_cast<uint2 *>(&bnd[qq.tag >> 1])[side] =
@@ -3719,8 +3721,11 @@ __global__ __launch_bounds__(64) void tier_label_kernel(tier::Graph G, tier::Eva
     uint32_t ent = sub == 0 ? np + ns : 0;
     for (int o = 32; o; o >>= 1) ent += (uint32_t)__shfl_xor((int)ent, o, 64);
     if (lane == 0) {
-        const uint64_t u0 = (uint64_t)blockIdx.x * 16;
-        if (bits) atomicOr((unsigned long long *)&E.allowed[u0 >> 6], (unsigned long long)(bits << (u0 & 63)));
+        // the unit's 16 answers are the 16-bit word blockIdx.x of the answer array: a plain
+        // store (zeros included, the last word's tail zeroed), so the array needs no clearing
+        reinterpret_cast<uint16_t *>(E.allowed)[blockIdx.x] = (uint16_t)bits;
+        if (blockIdx.x + 1 == gridDim.x)
+            for (uint32_t u = gridDim.x; u < (gridDim.x + 3) / 4 * 4; u++) reinterpret_cast<uint16_t *>(E.allowed)[u] = 0;
         if (vb) {
             atomicAdd(&stat_slot(E.stats)[0], 2ull * (unsigned long long)__popcll(vb));
             atomicAdd(&stat_slot(E.stats)[1], (unsigned long long)ent);
@@ -4208,16 +4213,20 @@ void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *
 // the step's answers and status words straight into host-mapped memory (one launch instead
 // of a copy each): bits (may be null) the caller's pinned answer words, h_* device views of
 // the steps' pinned status words (total may be null)
+// The status words are reset to "none" (~0) once copied: the next step needs no memset.
 __global__ __launch_bounds__(kTB) void tier_emit_kernel(const uint64_t *allowed, uint64_t words, uint64_t *bits,
-                                                        const unsigned long long *status, const uint64_t *total,
+                                                        unsigned long long *status, const uint64_t *total,
                                                         unsigned long long *h_status, uint64_t *h_total) {
     for (uint64_t i = (uint64_t)blockIdx.x * kTB + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kTB)
         bits[i] = allowed[i];
-    if (blockIdx.x == 0 && threadIdx.x < 2) h_status[threadIdx.x] = status[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < 2) {
+        h_status[threadIdx.x] = status[threadIdx.x];
+        status[threadIdx.x] = ~0ull;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 2 && total) *h_total = *total;
 }
 
-void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, const unsigned long long *status,
+void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, unsigned long long *status,
                  const uint64_t *total, unsigned long long *h_status, uint64_t *h_total, hipStream_t s) {
     KLAUNCH(tier_emit_kernel, dim3(tier_grid(std::max<uint64_t>(words, 1), kTB, 64)), dim3(kTB), 0, s, allowed,
             bits ? words : 0, bits, status, total, h_status, h_total);

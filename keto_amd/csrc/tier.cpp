@@ -543,6 +543,7 @@ struct TierDevice : TierSteps {
     int queries(const uint32_t *r, const uint32_t *t, uint64_t n, tier::Query *send, uint64_t *counts) override {
         return guarded("two-tier queries", [&] {
             THIP(hipSetDevice(dev));
+            w1_status_ok = false;
             set_requests(r, t, n, true);
             THIP(hipMemsetAsync(d_small, 0, 128 * 8, stream));
             THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 8, stream));
@@ -621,6 +622,7 @@ struct TierDevice : TierSteps {
     // last step's; a step whose replies outgrow it (known at the wait) is evaluated again
     // with a larger buffer.
     bool one_wait = true;  // KETOGPU_TIER_ONE_WAIT when the engine is made
+    bool w1_status_ok = false;  // the status words are "none" (the last one-wait step reset them)
     bool has_world1() const override { return G.label && one_wait; }
     Buf d_q, d_rep;
     int step_world1(const uint32_t *r, const uint32_t *t, uint64_t n, uint64_t *bits, std::vector<uint32_t> &overflow,
@@ -635,7 +637,9 @@ struct TierDevice : TierSteps {
             uint64_t *scr = (uint64_t *)d_scan.ensure(8 * (nq / 1024 + 2));
             uint64_t *allowed = (uint64_t *)d_bits.ensure(8 * std::max<uint64_t>(words, 1));
             uint4 *bnd = (uint4 *)d_bnd.ensure(16 * std::max<uint64_t>(n, 1));
-            THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 16, stream));  // first bad request, bad query
+            // first bad request, bad query: "none" — left so by the last one-wait step's emit
+            if (!w1_status_ok) THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 16, stream));
+            w1_status_ok = false;
             uint32_t *stage = n && in_place && !req_hbm ? (uint32_t *)d_req.ensure(8 * n) : nullptr;
             tier::launch_query_pairs(G, cur_r, cur_t, n, q, d_small + kFirstBad, stage, stream);
             if (stage) {
@@ -645,10 +649,7 @@ struct TierDevice : TierSteps {
             uint64_t *srcb = (uint64_t *)d_srcb.ensure(8 * std::max<uint64_t>(nq, 1));
             tier::launch_reply_lengths(G, q, nq, lens, d_small + kBadQuery, stream, srcb);
             tier::launch_scan(lens, nq, scr, stream);
-            h_small[kQs] = 0;
-            h_small[kQs + 1] = nq;
-            THIP(hipMemcpyAsync(d_small + kQs, h_small + kQs, 16, hipMemcpyHostToDevice, stream));
-            const uint64_t *qs = (const uint64_t *)(d_small + kQs);
+            const uint64_t *qs = (const uint64_t *)(d_small + kQs);  // (world 1: {0, nq}, not read)
             tier::Eval E{};
             E.roots = cur_r;
             E.targets = cur_t;
@@ -663,14 +664,13 @@ struct TierDevice : TierSteps {
                 const uint64_t cap_now = std::max(cap, d_rep.cap / 4);
                 // (the replies' pass also writes every request's bounds: one owner, one layout)
                 tier::launch_label_reply(G, q, nq, lens, srcb, qs, 1, rep, cap_now, bnd, n, stream);
-                THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
                 THIP(hipEventRecord(ev0, stream));
                 tier::launch_label_eval(G, E, rep, stream);
                 THIP(hipEventRecord(ev1, stream));
                 // answers (into pinned caller words in place, else one copy) and the status
                 // words by one launch
                 uint64_t *vbits = words ? (uint64_t *)host_view(bits, dev, false) : nullptr;
-                tier::launch_emit(allowed, words, vbits, d_small + kFirstBad, lens + nq,
+                tier::launch_emit(allowed, words, vbits, (unsigned long long *)d_small + kFirstBad, lens + nq,
                                   (unsigned long long *)d_hsmall + kFirstBad, d_hsmall + kLists, stream);
                 if (words && !vbits) THIP(hipMemcpyAsync(bits, allowed, 8 * words, hipMemcpyDeviceToHost, stream));
                 THIP(hipStreamSynchronize(stream));  // the step's one wait
@@ -693,6 +693,7 @@ struct TierDevice : TierSteps {
                 eval_ms += ms;
                 eval_launches++;
             }
+            w1_status_ok = true;  // (the emit reset the status words)
             if (force_overflow) {
                 std::fill(bits, bits + words, 0);
                 for (uint64_t c = 0; c < n; c++) overflow.push_back((uint32_t)c);
@@ -723,8 +724,11 @@ struct TierDevice : TierSteps {
             uint64_t *allowed = (uint64_t *)d_bits.ensure(8 * std::max<uint64_t>(words, 1));
             uint32_t *lists[3];
             for (int k = 0; k < 3; k++) lists[k] = (uint32_t *)d_list[k].ensure(4 * std::max<uint64_t>(units, 1));
-            THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
-            THIP(hipMemsetAsync(d_small + kLists, 0, 6 * 8, stream));
+            w1_status_ok = false;
+            if (!G.label) {  // (label: every unit stores its own answer word)
+                THIP(hipMemsetAsync(allowed, 0, 8 * std::max<uint64_t>(words, 1), stream));
+                THIP(hipMemsetAsync(d_small + kLists, 0, 6 * 8, stream));
+            }
             if (!recv) THIP(hipMemsetAsync(d_small + kFirstBad, 0xFF, 8, stream));
             tier::Eval E{};
             E.roots = cur_r;

@@ -92,7 +92,8 @@ void launch_eval(int stage, const Graph &g, const Eval &e, const uint32_t *in_li
 //           p's first word) -> scan -> launch_label_bounds (per request the bounds of its P
 //           list (x, y) and S list (z, w); bnd cleared by the caller; a list ending past
 //           cap received words: left empty) -> launch_label_eval
-// launch_label_eval: recv_label null: the rank owns every node and reads its own lists
+// launch_label_eval: recv_label null: the rank owns every node and reads its own lists; the
+// answer array needs no clearing (each unit stores its 16-bit word); world 1: qs not read
 // bnd (world 1, else null): the replies' own bounds per request, written by the same pass
 // srcb: each list's first word in lp_col / ls_col (launch_reply_lengths)
 void launch_label_reply(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, const uint64_t *srcb,
@@ -123,7 +124,8 @@ void launch_reply_lengths(const Graph &g, const Query *q, uint64_t n, uint64_t *
                           hipStream_t s, uint64_t *srcb = nullptr);
 // answers into the caller's pinned words (bits may be null) and the status words into the
 // steps' pinned ones, one launch (tier_emit_kernel)
-void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, const unsigned long long *status,
+// (status reset to ~0 once copied)
+void launch_emit(const uint64_t *allowed, uint64_t words, uint64_t *bits, unsigned long long *status,
                  const uint64_t *total, unsigned long long *h_status, uint64_t *h_total, hipStream_t s);
 void launch_scan(uint64_t *v, uint64_t n, uint64_t *scratch, hipStream_t s);  // exclusive, in place, v[n] = total
 void launch_reply_copy(const Graph &g, const Query *q, uint64_t n, const uint64_t *off, Reply *out, uint64_t cap,
