@@ -371,7 +371,15 @@ def test_check_ids_and_device_queries_match_oracle():
         q.run()
         np.testing.assert_array_equal(q.download(), want)
     st = eng.last_stats()
-    assert st["checks"] == len(reqs) and st["bytes_unit"] > 0 and st["ms_unit"] > 0
+    assert st["checks"] == len(reqs) and st["bytes_unit"] > 0 and st["ms_total"] > 0
+    # (plan label's lean resident calls collect no per-kernel timings or statistics: with
+    # timing events on, the same call reports both)
+    eng.set_events(True)
+    q.run()
+    eng.set_events(False)
+    np.testing.assert_array_equal(q.download(), want)
+    st = eng.last_stats()
+    assert st["ms_unit"] > 0 and st["unit_rows"] + st["unit_edges"] + st["unit_rev"] > 0
 
 
 def test_deep_chain_has_no_depth_cutoff():
