@@ -5293,7 +5293,7 @@ struct ketogpu_engine {
                     uint32_t *cnt = dalloc<uint32_t>(std::max<uint32_t>(n, 1)), *off16 = dalloc<uint32_t>(std::max<uint32_t>(n, 1));
                     tmp.push_back(cnt);
                     tmp.push_back(off16);
-                    const uint32_t big_cap = std::max<uint32_t>(4096, n / 32);
+                    uint32_t big_cap = std::max<uint32_t>(4096, n / 32);
                     uint32_t *big = dalloc<uint32_t>(big_cap);
                     tmp.push_back(big);
                     HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
@@ -5309,8 +5309,25 @@ struct ketogpu_engine {
                     unsigned long long hist[5];
                     HIP_CHECK(hipMemcpyAsync(hist, ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
                     HIP_CHECK(hipStreamSynchronize(stream));
-                    const uint32_t nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
-                    if (nbig > big_cap) throw Error(KETOGPU_ENOMEM, "plan label: too many lists of more than 64 entries");
+                    uint32_t nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
+                    if (nbig > big_cap && n) {
+                        // more long lists than the first guess held (config #3's deep folder
+                        // chains): the count pass again with room for all of them
+                        big_cap = nbig;
+                        big = dalloc<uint32_t>(big_cap);
+                        tmp.push_back(big);
+                        HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
+                        if (side == 0)
+                            KLAUNCH(label_count_kernel<false>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
+                                    (unsigned int *)(ctr + 4), big_cap);
+                        else
+                            KLAUNCH(label_count_kernel<true>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
+                                    (unsigned int *)(ctr + 4), big_cap);
+                        HIP_CHECK(hipMemcpyAsync(hist, ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+                        HIP_CHECK(hipStreamSynchronize(stream));
+                        nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
+                        if (nbig > big_cap) throw Error(KETOGPU_EDEVICE, "plan label: long-list count changed between passes");
+                    }
                     // the host's nodes: their lists (label_list), their counts into cnt
                     std::vector<uint32_t> hbig(nbig), hcnt(nbig);
                     std::vector<std::vector<uint32_t>> blist(nbig);
