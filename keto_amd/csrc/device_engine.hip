@@ -5294,6 +5294,8 @@ struct ketogpu_engine {
                     tmp.push_back(cnt);
                     tmp.push_back(off16);
                     uint32_t big_cap = std::max<uint32_t>(4096, n / 32);
+                    if (const char *e = getenv("KETOGPU_TEST_LABEL_BIG_CAP"))  // (tests: the regrow below)
+                        big_cap = std::max(1, atoi(e));
                     uint32_t *big = dalloc<uint32_t>(big_cap);
                     tmp.push_back(big);
                     HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
