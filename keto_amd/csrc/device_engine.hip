@@ -2837,9 +2837,21 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
         const uint32_t *Lg = walk_p ? Sg : Pg, *W = walk_p ? Pg : Sg;
         // (16-byte units: an overflow region is 16-word aligned, a head's entries start 16
         // bytes into a 32-byte aligned head and are padded to a multiple of 4 words)
-        if (valid && nl <= kFullStage)
-            for (uint32_t i = sub; i * 4 < nl; i += 4)
-                reinterpret_cast<uint4 *>(stage[q])[i] = reinterpret_cast<const uint4 *>(Lg)[i];
+        {  // every staging load in flight before the LDS stores (a quad covers kFullStage words)
+            constexpr int kSt = kFullStage / 16;  // 16-byte loads per lane
+            const bool st = valid && nl <= kFullStage;
+            uint4 v[kSt];
+#pragma unroll
+            for (int k = 0; k < kSt; k++) {
+                const uint32_t i = sub + 4 * k;
+                v[k] = st && i * 4 < nl ? reinterpret_cast<const uint4 *>(Lg)[i] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int k = 0; k < kSt; k++) {
+                const uint32_t i = sub + 4 * k;
+                if (st && i * 4 < nl) reinterpret_cast<uint4 *>(stage[q])[i] = v[k];
+            }
+        }
         constexpr int kPre = 16;  // the walked entries this lane takes, fetched together
         uint32_t wk[kPre];
 #pragma unroll
