@@ -13,7 +13,7 @@ shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 B="bench.py --no-cpu-baseline --parity sample --steps 5 --warmup 2 $*"
-KRX="bidi_kernel|bidi_host_kernel|lite_kernel|lite_host_kernel|label_kernel|label_host_kernel|label_rest_kernel|unit2_kernel|expand_kernel|pull_kernel|part_|tier_"
+KRX="bidi_kernel|bidi_host_kernel|lite_kernel|lite_host_kernel|label_kernel|label_host_kernel|label_rest_kernel|label_full_kernel|unit2_kernel|expand_kernel|pull_kernel|part_|tier_"
 echo "[profile] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 $B > "$OUT/trace.log" 2>&1 || { echo "trace failed"; tail -20 "$OUT/trace.log"; exit 1; }
