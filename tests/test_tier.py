@@ -368,16 +368,21 @@ def test_tier_device_rccl_world1_matches_oracle(loop_self, one_wait, label, monk
 
 @pytest.mark.gpu
 @LABEL
-def test_tier_device_two_ranks_share_gpu(label, monkeypatch):
-    """two ranks on the box's GPU over gloo: device steps, host transport (staged)"""
+@pytest.mark.parametrize("world", [2, 3])
+def test_tier_device_two_ranks_share_gpu(label, world, monkeypatch):
+    """two (three) ranks on the box's GPU over gloo: device steps, host transport (staged);
+    with three ranks every label reply segment layout has a middle segment"""
     _need_gpu()
     _mode(monkeypatch, label)
     namespaces, rows, reqs = _case(85)
     want = _want(namespaces, rows, reqs)
-    got, stats, _ = _run_tier(2, 85, 29790, device_steps=True)
+    got, stats, _ = _run_tier(world, 85, 29790 + world, device_steps=True)
     for idx, ans in got:
         np.testing.assert_array_equal(ans.astype(bool), want[idx])
-    assert all(s[0] > 0 for s in stats)
+    # every rank with requests sent queries; at world 3 the last rank has none (_tier_worker)
+    # and still answers the others' queries as an owner
+    assert all(s[0] > 0 for s in (stats if world == 2 else stats[:-1]))
+    assert world == 2 or (stats[-1][0] == 0 and stats[-1][1] > 0)
 
 
 @pytest.mark.gpu
