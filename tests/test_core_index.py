@@ -219,6 +219,33 @@ def test_labels_answer_like_the_oracle(seed, poison, heads):
         assert li["s_overflow"] > 0
 
 
+@pytest.mark.parametrize("seed", [81, 82])
+def test_label_raw_entries_are_the_one_edge_test(seed):
+    """the design note of DESIGN.md (f) "Kernel work next": a list's RAW entries (node ids >=
+    Ni, not landmarks) matter only for the one-edge path r -> t — P(r)'s only raw entry is r
+    itself (none for an interior r) — so allowed(r, t) = [r in raw S(t)] or the landmark lists
+    meet (or the masks), every request exactly as the oracle"""
+    namespaces, rows = randgraph.make_graph(seed, n_rows=900, n_obj=40, n_users=50, poison=True)
+    snap = Snapshot.from_rows(namespaces, rows, page_size=4, sort=True)
+    reqs = randgraph.make_requests(seed, namespaces, rows, n=1500, wildcard=False)
+    want = randgraph.oracle_store(namespaces, rows, 4).check_batch(reqs)
+    li = snap.label_index(0, 0)
+    ni = int(snap.stats()["num_interior"])
+    roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs])
+    for i in range(len(reqs)):
+        r, t = int(roots[i]), int(targets[i])
+        if r == NONE_ or t == NONE_:
+            assert not want[i]
+            continue
+        s_, sm = label_list(li["S"], li["s_head_words"], t)
+        p_, pm = label_list(li["P"], li["p_head_words"], r)
+        p_raw = p_[p_ >= ni].tolist()
+        assert p_raw == ([r] if r >= ni else [])
+        edge = r >= ni and r in set(s_[s_ >= ni].tolist())
+        meet = bool(sm & pm) or bool(np.isin(p_[p_ < ni], s_[s_ < ni]).any())
+        assert (edge or meet) == bool(want[i]), (reqs[i], want[i])
+
+
 @pytest.mark.parametrize("kind", ["rbac", "folders", "social"])
 def test_labels_on_synthetic_configs(kind):
     """configs #2, #3 and #4 (the power-law shape that closure labels could not reach):
