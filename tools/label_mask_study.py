@@ -45,6 +45,8 @@ def main():
     p.add_argument("--tuples", type=int, default=5_000_000)
     p.add_argument("--sample", type=int, default=20000)
     p.add_argument("--extra", default="0,64,192,448,960", help="landmarks moved into the masks beyond the first 64")
+    p.add_argument("--inline", default="", help="inline entries per head to replay instead of the built heads' "
+                                                "(e.g. 60,28: 64-word S heads, 32-word P heads)")
     a = p.parse_args()
     w = make(a.workload, a.tuples, a.sample)
     snap = Snapshot.from_columns(w.namespaces, w.columns)
@@ -61,7 +63,8 @@ def main():
         if pl is None or sl is None:
             continue
         cases.append((pl, pm, sl, sm))
-    for m, raw in [(int(x), True) for x in a.extra.split(",")] + [(0, False)]:
+    cap_s, cap_p = (int(x) for x in a.inline.split(",")) if a.inline else (hs - HEAD_FIXED, hp - HEAD_FIXED)
+    for m, raw in [(int(x), True) for x in a.extra.split(",")] + [(0, False), (448, False)]:
         bound = 64 + m
         dense = answered = 0
         lp = ls = 0
@@ -85,15 +88,16 @@ def main():
             ls += len(sk)
             hit = (pm & sm) != 0 or bool(pmk & smk)
             if not hit:
-                hit = bool(np.intersect1d(pk[:hp - HEAD_FIXED], sk[:hs - HEAD_FIXED]).size)
+                hit = bool(np.intersect1d(pk[:cap_p], sk[:cap_s]).size)
             if hit:
                 answered += 1
-            elif len(pk) > hp - HEAD_FIXED or len(sk) > hs - HEAD_FIXED:
+            elif len(pk) > cap_p or len(sk) > cap_s:
                 dense += 1
             else:
                 answered += 1
         n = max(len(cases), 1)
-        print(json.dumps({"workload": a.workload, "tuples": a.tuples, "heads": [hs, hp], "mask_bits": bound,
+        print(json.dumps({"workload": a.workload, "tuples": a.tuples, "heads": [hs, hp], "inline": [cap_s, cap_p],
+                          "mask_bits": bound,
                           "raw_entries_in_lists": raw,
                           "requests": len(cases), "dense_pass_share": round(dense / n, 4),
                           "first_stage_share": round(answered / n, 4), "mean_p_entries": round(lp / n, 2),
