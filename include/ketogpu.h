@@ -389,6 +389,17 @@ int ketogpu_queries_upload(ketogpu_engine *e, const uint32_t *roots, const uint3
 int ketogpu_queries_run(ketogpu_engine *e, ketogpu_queries *q);
 int ketogpu_queries_download(ketogpu_engine *e, const ketogpu_queries *q, uint64_t *allowed_bits,
                              uint64_t *flagged_bits);
+/* the same call as ketogpu_queries_run, enqueued on the engine's stream without waiting for
+ * the device when the engine can prove that no request of the batch needs the second stage
+ * (plan label, no head marked unlabelled, no wildcard root): batches are then pipelined, the
+ * way a server enqueues batch k+1 while batch k runs (Keto's check handler answers each
+ * request when its batch's bits are back: internal/check/handler.go).  *queued = 1 when the
+ * call returned before the device finished — its results are complete once
+ * ketogpu_queries_download or ketogpu_engine_wait returns, and a device error of the call is
+ * reported by that later call; 0: it ran as ketogpu_queries_run.  (queued may be NULL.) */
+int ketogpu_queries_run_async(ketogpu_engine *e, ketogpu_queries *q, int *queued);
+/* waits for every call enqueued on the engine (ketogpu_queries_run_async) */
+int ketogpu_engine_wait(ketogpu_engine *e);
 void ketogpu_queries_free(ketogpu_queries *q);
 
 /* statistics of the last run on this engine (for the roofline report) */

@@ -336,6 +336,8 @@ SIGNATURES = {
     "ketogpu_check_ids": (C.c_int, [vp, vp, vp, sz, vp, vp]),
     "ketogpu_queries_upload": (C.c_int, [vp, vp, vp, sz, C.POINTER(vp)]),
     "ketogpu_queries_run": (C.c_int, [vp, vp]),
+    "ketogpu_queries_run_async": (C.c_int, [vp, vp, C.POINTER(C.c_int)]),
+    "ketogpu_engine_wait": (C.c_int, [vp]),
     "ketogpu_queries_download": (C.c_int, [vp, vp, vp, vp]),
     "ketogpu_queries_free": (None, [vp]),
     "ketogpu_engine_last_stats": (C.c_int, [vp, C.POINTER(RunStats)]),

@@ -134,6 +134,10 @@ class Engine:
         L.check(self.L.ketogpu_engine_last_stats(self.h, C.byref(st)))
         return st.as_dict()
 
+    def wait(self):
+        """waits for the calls enqueued on this engine (DeviceQueries.run(pipelined=True))"""
+        L.check(self.L.ketogpu_engine_wait(self.h))
+
     def set_events(self, every_kernel):
         """host-to-host batches: a timing event between the call's kernels (main_ms = the
         first stage's own time) or only around the call (default)"""
@@ -249,8 +253,15 @@ class DeviceQueries:
                                                 C.byref(h)))
         self.h = h
 
-    def run(self):
-        L.check(self.e.L.ketogpu_queries_run(self.e.h, self.h))
+    def run(self, pipelined=False):
+        """one batch call; pipelined: ketogpu_queries_run_async — returns True when the call
+        was only enqueued (results complete after download() or Engine.wait())"""
+        if not pipelined:
+            L.check(self.e.L.ketogpu_queries_run(self.e.h, self.h))
+            return False
+        q = C.c_int(0)
+        L.check(self.e.L.ketogpu_queries_run_async(self.e.h, self.h, C.byref(q)))
+        return bool(q.value)
 
     def download(self, with_flags=False):
         words = max((self.n + 63) // 64, 1)

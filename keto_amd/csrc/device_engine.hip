@@ -2511,15 +2511,17 @@ __global__ __launch_bounds__(64) void lite_host_kernel(DevGraph g, const FRec *f
 // 2-hop reachability labels (labels.hpp): per request one S list (target t) and one P list
 // (root r), each behind a fixed-size HEAD of HS / HP words [count | overflow start / 16 |
 // mask lo | mask hi | entries ascending | 0xFFFFFFFF pad]; allowed <=> the masks share a
-// bit or the lists share an entry.  One wave per 16-request unit: four lanes per request
-// read its two heads (one dependent HBM read each, both in flight at once), the S entries
-// go to LDS, and every P entry is looked up in them by a branchless binary search.  Lists
-// longer than their head lie whole in the overflow region and are searched / read there.
-// A request without labels (a wildcard root, or the KETOGPU_LABEL_REST_PERMILLE test knob)
-// is listed (one request index each) for the second stage, label_rest_kernel: plan lite's
-// traversal over the listed requests, gathered 16 to a unit.
+// bit, the lists share a landmark, or r (not interior) is among S's raw entries (the
+// one-edge test).  One wave per 16-request unit: four lanes per request read its two heads
+// (one dependent HBM read each, both in flight at once), and the shorter inline landmark
+// list is looked up in the other by a branchless binary search in LDS.  A request the heads
+// cannot settle (labels.hpp: the prefix rules) goes to the dense pass over the overflow
+// lists.  A request without labels (a wildcard root, or the KETOGPU_LABEL_REST_PERMILLE test
+// knob) is listed (one request index each) for the second stage, label_rest_kernel: plan
+// lite's traversal over the listed requests, gathered 16 to a unit.
 struct LabelGraph {
     const uint32_t *P, *S;  // head arrays (+ overflow lists)
+    uint32_t ni;            // interior nodes: landmark ranks are below, raw entries and non-interior roots not
 };
 // The unlabelled requests' list is sharded: unit u appends to region u % kRestShards of
 // the list (region capacity `rest_cap` = 16 x ceil(units / kRestShards)) at counter
@@ -2590,20 +2592,38 @@ __device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[W]
             reinterpret_cast<uint4 *>(L)[(W / 4) * sub + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
 }
-// the lane's head words as entries to compare: the four header words and the padding
-// become 0xFFFFFFFE, which equals neither an entry (< 2^31) nor the other list's padding
+// entries below x among the first E ascending entries at L (LDS; positions past the list
+// hold 0xFFFFFFFF or larger entries): a branchless binary search (E = head - 4, up to 60)
+template <int E>
+__device__ __forceinline__ uint32_t label_lower_e(const uint32_t *L, uint32_t x) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+        if (step <= (uint32_t)E && pos + step <= (uint32_t)E && L[pos + step - 1] < x) pos += step;
+    return pos;
+}
+// x among the first E entries at L
+template <int E>
+__device__ __forceinline__ bool label_find_e(const uint32_t *L, uint32_t x) {
+    const uint32_t pos = label_lower_e<E>(L, x);
+    return pos < (uint32_t)E && L[pos] == x;
+}
+
+// the lane's head words as comparands: the four header words and the padding become
+// 0xFFFFFFFE, which equals no entry (< 2^31) and no padding word
 template <int W>
 __device__ __forceinline__ void label_cmp_words(const uint32_t (&w)[W], uint32_t sub, uint32_t (&c)[W]) {
 #pragma unroll
     for (int k = 0; k < W; k++) c[k] = (uint32_t)(W * sub + k) < kHeadFixed || w[k] == 0xFFFFFFFFu ? 0xFFFFFFFEu : w[k];
 }
-// does one of the n entries at L (LDS, 16-byte aligned, padded with 0xFFFFFFFF to a
-// multiple of 4) equal one of the lane's words c?  Every lane of the request reads the
-// same entries (LDS broadcast) and compares them with its quarter of the other head
+// does one of the first n entries at L (LDS, 16-byte aligned, readable up to a multiple of 4
+// past n: entries or padding that equal no comparand) equal one of the lane's comparands?
+// Every lane of the request reads the same entries (an LDS broadcast) and compares them with
+// its quarter of the other head, held in registers: no dependent LDS reads
 template <int W>
 __device__ __forceinline__ bool label_meet(const uint32_t *L, uint32_t n, const uint32_t (&c)[W]) {
     bool hit = false;
-    for (uint32_t j = 0; j < n && !hit; j += 4) {
+    for (uint32_t j = 0; j < n; j += 4) {
         const uint4 x = *reinterpret_cast<const uint4 *>(L + j);
 #pragma unroll
         for (int k = 0; k < W; k++) hit |= c[k] == x.x || c[k] == x.y || c[k] == x.z || c[k] == x.w;
@@ -2611,34 +2631,52 @@ __device__ __forceinline__ bool label_meet(const uint32_t *L, uint32_t n, const 
     return hit;
 }
 
-// x among the E ascending entries at L (LDS; E = head - 4, not a power of two): a branchless
-// binary search, positions past E read as above every entry
-template <int E>
-__device__ __forceinline__ bool label_find_e(const uint32_t *L, uint32_t x) {
-    uint32_t pos = 0;
+// x among the first E ascending entries at L (LDS, 16-byte aligned) in two dependent LDS
+// rounds: the last entries of the 8-entry blocks (independent reads) give x's block, whose 8
+// entries are then read at once (two 16-byte reads) — against the binary search's chain of
+// log2(E) dependent reads.  Words at positions >= E are never compared (the image row's
+// words past the head are not written).  lower: the entries below x instead
+template <int E, bool LOWER>
+__device__ __forceinline__ uint32_t label_block8(const uint32_t *L, uint32_t x) {
+    constexpr int NB = (E + 7) / 8;
+    uint32_t blk = 0;
 #pragma unroll
-    for (uint32_t step = 16; step; step >>= 1)
-        if (step <= (uint32_t)E && pos + step <= (uint32_t)E && L[pos + step - 1] < x) pos += step;
-    return pos < (uint32_t)E && L[pos] == x;
+    for (int b = 0; b + 1 < NB; b++) blk += L[8 * b + 7] < x;
+    const uint4 u = *reinterpret_cast<const uint4 *>(L + 8 * blk), v = *reinterpret_cast<const uint4 *>(L + 8 * blk + 4);
+    const uint32_t w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    uint32_t r = LOWER ? 8 * blk : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const bool in = 8 * blk + i < (uint32_t)E;
+        if (LOWER)
+            r += in && w[i] < x;
+        else
+            r |= in && w[i] == x;
+    }
+    return r;
 }
 
-// KETO_LABEL_MEET: how the shorter of two inline lists meets the other (0: each entry,
-// round-robin over the request's four lanes, binary-searched in the other list in LDS;
-// 1: all four lanes read every entry and compare it with their quarter of the other head
-// in registers)
+// KETO_LABEL_MEET: how the shorter inline landmark list meets the other head.  0 (default):
+// the shorter list's entries round-robin over the request's four lanes, each looked up in the
+// other list in LDS by label_block8 (two dependent LDS rounds); 2: the same by a binary search
+// (log2(E) dependent rounds: config #3's long lists pay for it); 1: every lane reads the
+// shorter list's entries and compares them with its quarter of the other head in registers
+// (measured 2.8x slower at 64-word heads, profiles/r06/ab)
 #ifndef KETO_LABEL_MEET
 #define KETO_LABEL_MEET 0
 #endif
 
 // A unit of 16 requests by one wave (four lanes per request), the heads' inline entries
-// only: a request left open with an overflowing list is listed in F for the dense second
-// pass (label_full_kernel), so no wave waits on one request's second read.
+// only: a request the heads do not settle is listed in F for the dense second pass
+// (label_full_kernel), so no wave waits on one request's second read.
 template <int HS, int HP>
 __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelGraph &L, uint32_t r_lane,
                                            uint32_t t_lane, uint64_t *allowed, const uint64_t unit,
                                            const LabelRest &R, const LabelRest &F, unsigned long long *stats) {
-    static_assert((HS == 8 || HS == 16 || HS == 32) && (HP == 8 || HP == 16 || HP == 32), "heads of 8, 16 or 32 words");
-    constexpr int SW = HS / 4, PW = HP / 4;  // head words per lane
+    static_assert((HS == 8 || HS == 16 || HS == 32 || HS == 64) && (HP == 8 || HP == 16 || HP == 32 || HP == 64),
+                  "heads of 8, 16, 32 or 64 words");
+    constexpr int SW = HS / 4, PW = HP / 4;                                   // head words per lane
+    constexpr uint32_t CS = HS - kHeadFixed, CP = HP - kHeadFixed;            // inline entries
     const uint32_t lane = threadIdx.x & 63, q = lane >> 2, sub = lane & 3;
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
@@ -2659,6 +2697,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
     label_to_lds<SW>(Sl, sw, sub);
     label_to_lds<PW>(Pl, pw, sub);
+    const uint32_t *Se = Sl + kHeadFixed, *Pe = Pl + kHeadFixed;  // the inline entries
     const uint32_t shard = (uint32_t)(unit % kRestShards);
     // a request without labels (or with a wildcard root): listed for the second stage
     {
@@ -2668,34 +2707,60 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     }
     wave_sync();  // (the images: this wave's own rows)
     bool hit = labelled && (smask & pmask) != 0;
-    // 1. the heads' inline entries: whole lists, or the first entries of an overflowing one
-    //    (most hits are found there): the shorter walked, round-robin over the request's
-    //    four lanes, each entry searched in the other (KETO_LABEL_MEET 1: compared with the
-    //    other head's words in registers)
-    const uint32_t es = min(ns, (uint32_t)(HS - kHeadFixed)), ep = min(np, (uint32_t)(HP - kHeadFixed));
+    // S's inline landmarks: its inline entries below Ni (the raw entries follow them)
+    const uint32_t es = !labelled ? 0u : KETO_LABEL_MEET == 2 ? label_lower_e<CS>(Se, L.ni) : label_block8<CS, true>(Se, L.ni);
+    const uint32_t ep = min(np, CP);
+    // 1. the inline landmark prefixes: the shorter walked, round-robin over the request's
+    //    four lanes, each entry searched in the other; the one-edge test (a non-interior root
+    //    among S's inline raw entries) on the fourth lane
     if (labelled && !hit) {
-        if (!KETO_LABEL_MEET) {
+        if (KETO_LABEL_MEET == 1) {
+            if (es <= ep) {
+                uint32_t c[PW];
+                label_cmp_words<PW>(pw, sub, c);
+                hit = label_meet<PW>(Se, es, c);
+            } else {
+                uint32_t c[SW];
+                label_cmp_words<SW>(sw, sub, c);
+                hit = label_meet<SW>(Pe, ep, c);
+            }
+            if (r >= L.ni) {  // the one-edge test against the lane's S words
+#pragma unroll
+                for (int k = 0; k < SW; k++) hit |= (uint32_t)(SW * sub + k) >= kHeadFixed && sw[k] == r;
+            }
+        } else if (KETO_LABEL_MEET == 2) {
             if (es <= ep)
-                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_find_e<HP - kHeadFixed>(Pl + kHeadFixed, Sl[kHeadFixed + k]);
+                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_find_e<CP>(Pe, Se[k]);
             else
-                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_find_e<HS - kHeadFixed>(Sl + kHeadFixed, Pl[kHeadFixed + k]);
-        } else if (es <= ep) {
-            uint32_t c[PW];
-            label_cmp_words<PW>(pw, sub, c);
-            hit = label_meet<PW>(Sl + kHeadFixed, es, c);
+                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_find_e<CS>(Se, Pe[k]);
+            if (sub == 3 && !hit && r >= L.ni) hit = label_find_e<CS>(Se, r);
         } else {
-            uint32_t c[SW];
-            label_cmp_words<SW>(sw, sub, c);
-            hit = label_meet<SW>(Pl + kHeadFixed, ep, c);
+            if (es <= ep)
+                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_block8<CP, false>(Pe, Se[k]);
+            else
+                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_block8<CS, false>(Se, Pe[k]);
+            if (sub == 3 && !hit && r >= L.ni) hit = label_block8<CS, false>(Se, r);
         }
     }
-    // 2. a request with an overflowing list and no hit yet: listed for label_full_kernel,
-    //    with both counts and overflow starts (the dense pass then needs no head again)
+    // 2. a request neither hit nor settled by its heads (labels.hpp): listed for
+    //    label_full_kernel, with both counts and overflow starts (the dense pass then needs no
+    //    head again).  Settled: no landmark can be missing from the prefixes — S's landmarks
+    //    whole (its list inline, or its last inline entry raw) and P's whole, or one whole with
+    //    its largest landmark <= the other's last inline one — and the raw test settled: r
+    //    interior, S whole inline, or r <= S's last inline entry
     {
         const uint64_t hb = __ballot(hit);
         const uint32_t os = label_word<SW, 1>(sw), op = label_word<PW, 1>(pw);
-        const bool full = sub == 0 && labelled && !((hb >> (lane & ~3u)) & 0xF) &&
-                          (ns > (uint32_t)(HS - kHeadFixed) || np > (uint32_t)(HP - kHeadFixed));
+        bool full = false;
+        if (sub == 0 && labelled && !((hb >> lane) & 0xF)) {
+            const uint32_t s_end = Se[CS - 1];  // (ns > CS: the last inline entry)
+            const bool s_whole = ns <= CS || s_end >= L.ni, p_whole = np <= CP;
+            const uint32_t s_last = es ? Se[es - 1] : 0u, p_last = ep ? Pe[ep - 1] : 0u;
+            const bool lm_done = es == 0 || np == 0 || (s_whole && (p_whole || s_last <= p_last)) ||
+                                 (p_whole && p_last <= s_last);
+            const bool raw_done = r < L.ni || ns <= CS || r <= s_end;
+            full = !(lm_done && raw_done);
+        }
         const uint32_t at = lds_append(full, F.count + shard * kRestStride);
         if (full) {
             uint4 *rec = F.rec + 2 * (shard * F.cap + at);
@@ -2703,12 +2768,10 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
             rec[1] = make_uint4(np, os, op, 0u);
         }
     }
-    uint32_t looked = 0;
     const uint64_t bits = __ballot(hit);
     // statistics: 2 rows (heads) and the entries read (both lists and the masks) per request
     const uint32_t rows = wave_sum_all(labelled && sub == 0 ? 2u : 0u);
     const uint32_t ent = wave_sum_all(labelled && sub == 0 ? ns + np + kHeadFixed : 0u);
-    (void)looked;
     // bit j of the unit's result = any of the request's four lanes (scalar bit compression)
     uint64_t x = bits | bits >> 1;
     x = (x | x >> 2) & 0x1111111111111111ull;
@@ -2780,9 +2843,10 @@ __global__ __launch_bounds__(256) void label_host_kernel(DevGraph g, LabelGraph 
     label_unit<HS, HP>(sh[wave], L, rk, tk, allowed, unit, R, F, stats);
 }
 
-// The dense second pass over the requests the first stage left open with an overflowing
-// list (F: two records per request carrying both counts and overflow starts): gathered 16
-// to a wave, four lanes per request, persistent.  Both lists' places are known from the
+// The dense second pass over the requests the first stage's heads did not settle (F: two
+// records per request carrying both counts and overflow starts): gathered 16 to a wave,
+// four lanes per request, persistent.  It answers from the whole lists: the landmark
+// intersection (S's raw entries never meet P's landmarks) and the one-edge test.  Both lists' places are known from the
 // records, so one dependent read follows them: the longer list is staged in LDS (up to
 // kFullStage words, from its overflow region or its head's inline entries) while the
 // shorter one's entries are fetched into registers, then binary-searched.
@@ -2867,6 +2931,9 @@ __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *
             for (int i = 0; i < kPre; i++)
                 if (!hit && sub + 4 * i < nw) hit = label_find_n(O, nl, wk[i]);
             for (uint32_t k = sub + 4 * kPre; k < nw && !hit; k += 4) hit = label_find_n(O, nl, W[k]);
+            // the one-edge test: a non-interior root among S's raw entries (S the staged list
+            // or the walked one; a landmark never equals a non-interior node id)
+            if (sub == 0 && !hit && rr >= L.ni) hit = walk_p ? label_find_n(O, nl, rr) : label_find_n(W, nw, rr);
         }
         const uint64_t bits = __ballot(hit);
         if (valid && sub == 0) {
@@ -2921,7 +2988,7 @@ __global__ __launch_bounds__(64) void label_rest_kernel(DevGraph g, const FRec *
 // The head arrays are built on the device from the 2-hop labels (built once per snapshot on
 // the host, labels.cpp) and the graph already in HBM: one wave per node gathers the node's
 // entries (S: Lin of the interior entries of rev(x) + its other entries; P: Lout(x) for an
-// interior x, else x + Lout of every entry of fint(x)) into LDS, sorts them (bitonic over
+// interior x, else Lout of every entry of fint(x)) into LDS, sorts them (bitonic over
 // the 64 lanes) and drops duplicates.  A node with more than 64 entries before deduplication
 // (or a row of more than 64) is left to the host (label_list), which writes its head after.
 // Pass 1 counts (and a histogram picks the head size), a scan places the overflow lists,
@@ -2942,7 +3009,7 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
                                              uint32_t &v, uint64_t &keep, uint64_t &mask) {
     const uint32_t lane = threadIdx.x & 63;
     uint64_t b = 0, m;
-    bool synth = false, self_raw = false;
+    bool synth = false;
     if constexpr (!PSIDE) {
         b = g.rev_off[x];
         m = g.rev_off[(uint64_t)x + 1] - b;
@@ -2952,15 +3019,14 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
     } else {
         b = g.fint_off[x];
         m = g.fint_off[(uint64_t)x + 1] - b;
-        self_raw = true;  // + the raw entry x
     }
     if (m > 64) return false;
     uint32_t e = KETOGPU_NODE_NONE, c = 0;
     uint64_t lo = 0, mk = 0;
     if (lane < m) {
         e = synth ? x : PSIDE ? g.fint_col[b + lane] : g.rev_col[b + lane];
-        if (e == D.ph[0] || e == D.ph[1] || e == D.ph[2]) {
-            c = 0;  // a free slot
+        if (!synth && (e == D.ph[0] || e == D.ph[1] || e == D.ph[2])) {
+            c = 0;  // a free slot (a row entry; an interior placeholder's own P head is Lout(x), as the host builds it)
         } else if (e < D.Ni) {
             const uint64_t *off = PSIDE ? D.out_off : D.in_off;
             lo = off[e];
@@ -2971,7 +3037,7 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
         }
     }
     const uint32_t incl = wave_incl_sum_u32(c);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63) + (self_raw ? 1u : 0u);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > 64) return false;
     wave_sync();  // (the previous node's reads of buf are done)
     if (lane < m && c) {
@@ -2983,7 +3049,6 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
             buf[o] = e;
         }
     }
-    if (self_raw && lane == 0) buf[total - 1] = x;
     wave_sync();
     v = lane < total ? buf[lane] : 0xFFFFFFFFu;
 #pragma unroll
@@ -3004,17 +3069,18 @@ __device__ __forceinline__ bool label_gather(const DevGraph &g, const LabelDevLi
 }
 
 // pass 1: counts (kLabelBig for the host's nodes, listed in big), and per block the
-// histogram hist = {non-empty, <= 4, <= 12, <= 28 entries}
+// histogram hist = {non-empty, <= 4, <= 12, <= 28, <= 60 entries} (inline in heads of 8, 16,
+// 32, 64 words)
 template <bool PSIDE>
 __global__ __launch_bounds__(256) void label_count_kernel(DevGraph g, LabelDevLists D, uint32_t n, uint32_t *cnt,
                                                           unsigned long long *hist, uint32_t *big,
                                                           unsigned int *big_n, uint32_t big_cap) {
     __shared__ uint32_t buf[4][64];
-    __shared__ unsigned long long h[4];
+    __shared__ unsigned long long h[5];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x < 4) h[threadIdx.x] = 0;
+    if (threadIdx.x < 5) h[threadIdx.x] = 0;
     __syncthreads();
-    unsigned long long hw[4] = {0, 0, 0, 0};
+    unsigned long long hw[5] = {0, 0, 0, 0, 0};
     for (uint32_t x = blockIdx.x * 4 + wave; x < n; x += gridDim.x * 4) {
         uint32_t v;
         uint64_t keep, mask;
@@ -3033,12 +3099,13 @@ __global__ __launch_bounds__(256) void label_count_kernel(DevGraph g, LabelDevLi
             hw[1] += c != 0 && c <= 4;
             hw[2] += c != 0 && c <= 12;
             hw[3] += c != 0 && c <= 28;
+            hw[4] += c != 0 && c <= 60;
         }
     }
     if (lane == 0)
-        for (int k = 0; k < 4; k++) atomicAdd(&h[k], hw[k]);
+        for (int k = 0; k < 5; k++) atomicAdd(&h[k], hw[k]);
     __syncthreads();
-    if (threadIdx.x < 4) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+    if (threadIdx.x < 5) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
 // overflow lists, in 16-word units: a list of more than cap entries takes ceil(count / 16)
@@ -4469,6 +4536,17 @@ struct ketogpu_engine {
     bool label_clean = false;
     // this call is lean: HBM-resident plan label, timing events off, lazy rest stage
     bool lean_call = false;
+    // ketogpu_queries_run_async: this call may return before the device finishes (set per
+    // call); `queued`: the last call did
+    bool pipelined_req = false, queued = false;
+    // heads marked kNoLabel by the build (the test knob) and the knob itself: with none, and
+    // no head marked by a write (lab_invalid), no request of a batch without wildcard roots
+    // can go to the second stage
+    uint64_t label_nolabel_heads = 0;
+    uint32_t label_knob = 0;
+    bool label_rest_free(const Batch &q) const {
+        return use_label && label_nolabel_heads == 0 && label_knob == 0 && lab_invalid == 0 && !q.has_dyn;
+    }
     uint64_t full_prev = 1024 * 16;  // the previous call's full-list requests (the pass's grid)
     uint32_t label_hs = 16, label_hp = 8;  // head words of S and P
     double label_coverage = 0, label_build_ms = 0, label_pll_ms = 0;
@@ -4487,11 +4565,13 @@ struct ketogpu_engine {
         auto hp = [&](auto hs) {
             if (label_hp == 8) f(hs, std::integral_constant<int, 8>{});
             else if (label_hp == 16) f(hs, std::integral_constant<int, 16>{});
-            else f(hs, std::integral_constant<int, 32>{});
+            else if (label_hp == 32) f(hs, std::integral_constant<int, 32>{});
+            else f(hs, std::integral_constant<int, 64>{});
         };
         if (label_hs == 8) hp(std::integral_constant<int, 8>{});
         else if (label_hs == 16) hp(std::integral_constant<int, 16>{});
-        else hp(std::integral_constant<int, 32>{});
+        else if (label_hs == 32) hp(std::integral_constant<int, 32>{});
+        else hp(std::integral_constant<int, 64>{});
     }
     // plan label, host batches (4 units per workgroup)
     void launch_label_host(const Batch &q, const HostSrc *src, uint64_t bunits) {
@@ -4941,7 +5021,7 @@ struct ketogpu_engine {
     void relabel() {
         uint32_t *A[2] = {const_cast<uint32_t *>(lgraph.S), const_cast<uint32_t *>(lgraph.P)};
         release_label(A);
-        lgraph = LabelGraph{nullptr, nullptr};
+        lgraph = LabelGraph{nullptr, nullptr, 0};
         lab_R.reset();
         use_label = true;
         build_label(*snap);
@@ -5254,8 +5334,8 @@ struct ketogpu_engine {
         if (const char *e = getenv("KETOGPU_LABEL_HEADS")) sscanf(e, "%u,%u", &hs, &hp);
         if (const char *e = getenv("KETOGPU_LABEL_REST_PERMILLE")) permille = (uint32_t)std::min(1000, std::max(0, atoi(e)));
         for (uint32_t h : {hs, hp})
-            if (h && h != 8 && h != 16 && h != 32) {
-                fprintf(stderr, "[ketogpu] plan label disabled: KETOGPU_LABEL_HEADS takes 8, 16 or 32 words\n");
+            if (h && h != 8 && h != 16 && h != 32 && h != 64) {
+                fprintf(stderr, "[ketogpu] plan label disabled: KETOGPU_LABEL_HEADS takes 8, 16, 32 or 64 words\n");
                 drop_label();
                 return;
             }
@@ -5315,15 +5395,15 @@ struct ketogpu_engine {
                     if (n) {
                         if (side == 0)
                             KLAUNCH(label_count_kernel<false>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
-                                    (unsigned int *)(ctr + 4), big_cap);
+                                    (unsigned int *)(ctr + 6), big_cap);
                         else
                             KLAUNCH(label_count_kernel<true>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
-                                    (unsigned int *)(ctr + 4), big_cap);
+                                    (unsigned int *)(ctr + 6), big_cap);
                     }
-                    unsigned long long hist[5];
-                    HIP_CHECK(hipMemcpyAsync(hist, ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+                    unsigned long long hist[7];  // the histogram (label_count_kernel), [6]: the long lists
+                    HIP_CHECK(hipMemcpyAsync(hist, ctr, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
                     HIP_CHECK(hipStreamSynchronize(stream));
-                    uint32_t nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
+                    uint32_t nbig = (uint32_t)(hist[6] & 0xFFFFFFFFull);
                     if (nbig > big_cap && n) {
                         // more long lists than the first guess held (config #3's deep folder
                         // chains): the count pass again with room for all of them
@@ -5333,13 +5413,13 @@ struct ketogpu_engine {
                         HIP_CHECK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), stream));
                         if (side == 0)
                             KLAUNCH(label_count_kernel<false>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
-                                    (unsigned int *)(ctr + 4), big_cap);
+                                    (unsigned int *)(ctr + 6), big_cap);
                         else
                             KLAUNCH(label_count_kernel<true>, dim3(grid), dim3(256), 0, stream, g, D, n, cnt, ctr, big,
-                                    (unsigned int *)(ctr + 4), big_cap);
-                        HIP_CHECK(hipMemcpyAsync(hist, ctr, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+                                    (unsigned int *)(ctr + 6), big_cap);
+                        HIP_CHECK(hipMemcpyAsync(hist, ctr, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
                         HIP_CHECK(hipStreamSynchronize(stream));
-                        nbig = (uint32_t)(hist[4] & 0xFFFFFFFFull);
+                        nbig = (uint32_t)(hist[6] & 0xFFFFFFFFull);
                         if (nbig > big_cap) throw Error(KETOGPU_EDEVICE, "plan label: long-list count changed between passes");
                     }
                     // the host's nodes: their lists (label_list), their counts into cnt
@@ -5360,10 +5440,10 @@ struct ketogpu_engine {
                         KLAUNCH(label_big_io_kernel, dim3((nbig + 255) / 256), dim3(256), 0, stream, big, nbig, cnt, dc,
                                 nullptr, nullptr);
                     }
-                    uint64_t ne = hist[0], fit[3] = {hist[1], hist[2], hist[3]};
+                    uint64_t ne = hist[0], fit[4] = {hist[1], hist[2], hist[3], hist[4]};
                     for (uint32_t c : hcnt) {  // (as the host build counts them)
                         ne += c != 0;
-                        for (int k = 0; k < 3; k++) fit[k] += c != 0 && c <= (8u << k) - kHeadFixed;
+                        for (int k = 0; k < 4; k++) fit[k] += c != 0 && c <= (8u << k) - kHeadFixed;
                     }
                     if (!H[side]) H[side] = pick_head(ne, fit);
                     if (side == 0) nonempty_s = ne;
@@ -5490,7 +5570,7 @@ struct ketogpu_engine {
             owned.push_back(rest_counts);
             HIP_CHECK(hipMemset(rest_counts, 0, 4 * kRestShards * kRestStride * sizeof(unsigned int)));
         }
-        lgraph = LabelGraph{A[1], A[0]};
+        lgraph = LabelGraph{A[1], A[0], s.Ni};
         if (s.writable) {
             if (!lab_R) {  // (the host build path: labels and storage from the snapshot again)
                 lab_R = reach_labels_of(s);
@@ -5516,6 +5596,8 @@ struct ketogpu_engine {
         label_hs = H[0];
         label_hp = H[1];
         label_coverage = nonempty_s ? 1.0 - (double)nolabel / (double)nonempty_s : 1.0;
+        label_nolabel_heads = nolabel;
+        label_knob = permille;
         if (getenv("KETOGPU_LABEL_HOST")) {
             uint64_t ne = 0;
             for (uint64_t x = 0; x < s.N; x++) ne += s.rev_off[x + 1] > s.rev_off[x];
@@ -5729,6 +5811,22 @@ struct ketogpu_engine {
                         lgraph, q.allowed, label_rest(q.n), label_full(q.n), &spill_count[0], &spill_count[7],
                         fused ? nullptr : st.stats + 4 * kStatSlots, fused ? d_hctr + 16 : nullptr);
             });
+        if (fused && pipelined_req && label_rest_free(q)) {
+            // a pipelined lean call (ketogpu_queries_run_async): no request of this batch can
+            // be listed for the second stage (label_rest_free), so nothing after the dense pass
+            // depends on the lists' totals: the call returns without a host wait.  The results
+            // are complete when the stream is (ketogpu_queries_download, ketogpu_engine_wait);
+            // the counters are left as a lean call without rest requests leaves them
+            queued = true;
+            unit_end = d;
+            rs.rest_requests = 0;
+            rs.full_requests = full_prev;  // (not read back: the last synchronized call's count)
+            label_clean = true;
+            label_calls++;
+            rs.push_launches += 2;
+            rs.unit_launches += 2;
+            return 0;
+        }
         auto launch_stages = [&](uint64_t prev0) {
             for (size_t k = 0, c = 0; k < stages.size(); k++, c ^= 1)
                 launch_stage(stages[k], q, list[c], &spill_count[k], fans[k], list[c ^ 1], &spill_count[k + 1],
@@ -6559,6 +6657,34 @@ int ketogpu_queries_run(ketogpu_engine *e, ketogpu_queries *q) {
     std::lock_guard<std::mutex> lk(e->mu);
     e->sync();
     e->run(*q);
+    API_END
+}
+
+int ketogpu_queries_run_async(ketogpu_engine *e, ketogpu_queries *q, int *queued) {
+    API_BEGIN
+    if (!e || !q) throw Error(KETOGPU_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> rd(e->snap->mu);
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->sync();
+    e->pipelined_req = true;
+    e->queued = false;
+    try {
+        e->run(*q);
+    } catch (...) {
+        e->pipelined_req = false;
+        throw;
+    }
+    e->pipelined_req = false;
+    if (queued) *queued = e->queued ? 1 : 0;
+    API_END
+}
+
+int ketogpu_engine_wait(ketogpu_engine *e) {
+    API_BEGIN
+    if (!e) throw Error(KETOGPU_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_CHECK(hipSetDevice(e->device));
+    HIP_CHECK(hipStreamSynchronize(e->stream));
     API_END
 }
 

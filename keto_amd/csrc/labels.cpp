@@ -171,6 +171,9 @@ void build_reach(IAdj &a, uint32_t n, ReachLabels &out) {
     const auto t0 = Clock::now();
     out.n = n;
     if (!n) return;
+    // the searches' stamps 2r + 1 + d are u32: past 2^31 - 1 interior nodes they would wrap
+    // onto earlier stamps (a node would look visited, a search pruned) — refused instead
+    if (n >= 0x7FFFFFFFu) throw Error(KETOGPU_EINVAL, "plan label: 2^31 or more interior nodes");
     // rank: most central first ((interior out-degree + 1) x (interior in-degree + 1))
     out.order.resize(n);
     std::iota(out.order.begin(), out.order.end(), 0u);
@@ -339,7 +342,8 @@ struct Lists {
         std::sort(out.begin(), out.end());
         out.erase(std::unique(out.begin(), out.end()), out.end());
     }
-    // P(r): Lout(r) for an interior r, else {r} + Lout of every entry of fint(r)
+    // P(r): Lout(r) for an interior r, else Lout of every entry of fint(r) (the one-edge
+    // case r in rev(t) is the raw test against S(t), labels.hpp)
     void p_list(uint64_t r, std::vector<uint32_t> &out, uint64_t &mask) const {
         out.clear();
         if (r < R.n) {
@@ -348,7 +352,6 @@ struct Lists {
             return;
         }
         mask = 0;
-        out.push_back((uint32_t)r);
         const uint32_t *b = s.fint_col.data() + s.fint_off[r], *e = s.fint_col.data() + s.fint_off[r + 1];
         for (const uint32_t *p = b; p < e; p++) {
             if (s.writable && *p == s.Df) continue;  // a free slot
@@ -361,20 +364,21 @@ struct Lists {
 };
 
 uint32_t pick_head_of(const std::vector<uint32_t> &cnt) {
-    uint64_t ne = 0, fit[3] = {0, 0, 0};
+    uint64_t ne = 0, fit[4] = {0, 0, 0, 0};
     for (uint32_t c : cnt) {
         if (!c) continue;
         ne++;
-        for (int k = 0; k < 3; k++) fit[k] += c <= (8u << k) - kHeadFixed;
+        for (int k = 0; k < 4; k++) fit[k] += c <= (8u << k) - kHeadFixed;
     }
     return ketogpu::pick_head(ne, fit);
 }
 
 }  // namespace
 
-uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]) {
-    for (int k = 0; k < 3; k++)
-        if (fit[k] * 20 >= nonempty * 19) return 8u << k;
+uint32_t pick_head(uint64_t nonempty, const uint64_t fit[4]) {
+    if ((fit[3] - fit[2]) * 10 >= nonempty) return 64;
+    for (int k = 0; k < 2; k++)
+        if (fit[k] * 1000 >= fit[2] * 999) return 8u << k;
     return 32;
 }
 
@@ -397,7 +401,8 @@ void build_labels(const Snapshot &s, uint32_t hs, uint32_t hp, uint32_t rest_per
                   LabelIndex &out) {
     const auto t0 = Clock::now();
     for (uint32_t h : {hs, hp})
-        if (h && h != 8 && h != 16 && h != 32) throw Error(KETOGPU_EINVAL, "plan label: heads of 8, 16 or 32 words");
+        if (h && h != 8 && h != 16 && h != 32 && h != 64)
+            throw Error(KETOGPU_EINVAL, "plan label: heads of 8, 16, 32 or 64 words");
     out = LabelIndex{};
     ReachLabels R;
     build_reach_labels(s, R);

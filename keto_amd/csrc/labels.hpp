@@ -17,23 +17,34 @@
 //
 // Per request, with rev(t) the expandable nodes whose rows hold t and fint(r) r's interior
 // successors:
-//   S(t) = Lin(v) for every interior v in rev(t)  +  the non-interior entries of rev(t)
+//   S(t) = Lin(v) for every interior v in rev(t)  +  raw(t), the non-interior entries of rev(t)
 //   P(r) = Lout(r)                                  (r interior)
-//        = {r} + Lout(c) for every c in fint(r)     (r expandable, not interior)
-//   allowed(r, t)  <=>  P(r) and S(t) share an entry (or their masks share a bit).
+//        = Lout(c) for every c in fint(r)           (r expandable, not interior)
+//   allowed(r, t)  <=>  P(r) and S(t) share a landmark (or their masks share a bit)
+//                       or  r is not interior and r in raw(t)          (the one-edge test)
 // Proof: a path's last inner node v is in rev(t) and its first one c in fint(r) (c = v
 // possible), so c ->* v; r interior: r ->* v; a one-edge path has r in rev(t) (r interior:
-// r ->* r; r not interior: the raw entry r).  Conversely a shared landmark w gives
-// r (->c) ->* w ->* v -> t, and a shared raw entry is r in rev(t).  Landmark entries are
-// RANKS (< Ni) and raw entries node ids (>= Ni): the two never collide.
+// r ->* r, so Lin(r) in S(t) meets Lout(r); r not interior: r in raw(t)).  Conversely a shared
+// landmark w gives r (->c) ->* w ->* v -> t, and r in raw(t) is the edge r -> t.  Landmark
+// entries are RANKS (< Ni) and raw entries node ids (>= Ni): a sorted S list is its landmarks
+// then its raw entries, and a landmark never equals a raw entry or a non-interior root.
 //
 // Storage (u32 words), one fixed-size HEAD per node (S: every node, P: every expandable
-// node), hs / hp words each (8, 16 or 32: the smallest whose inline entries hold >= 95% of
-// the non-empty lists):
+// node), hs / hp words each (8, 16, 32 or 64, labels.cpp pick_head):
 //   [count | overflow start / 16 | mask lo | mask hi | entries ascending ... | 0xFFFFFFFF pad]
 // a list of more than head - 4 entries is kept whole at words 16 x (overflow start) (after
 // the heads, in the same array), its first head - 4 entries also in the head; count =
-// kNoLabel: the request goes to the second stage.
+// kNoLabel: the request goes to the second stage.  An S head's count is its whole list
+// (landmarks and raw entries); where its landmarks end is found among the entries (the
+// first entry >= Ni).
+//
+// The first stage (device_engine.hip label_unit) decides a request from the two heads alone
+// when it can: a hit among the masks, the inline landmark prefixes or (r not interior) the
+// inline raw entries; else "denied" when no landmark can be missing from the prefixes — both
+// landmark lists whole in their heads, or one whole with its largest entry <= the other's
+// last inline entry (a common landmark would then lie in both prefixes) — and the raw test
+// is settled (r interior, S whole in its head, or r <= its last inline entry).  Otherwise
+// the dense pass reads the overflow lists.
 #pragma once
 
 #include <cstdint>
@@ -76,16 +87,20 @@ std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s);
 // one node's list and mask as its head holds them (p_side: P(x), else S(x))
 void label_list(const Snapshot &s, const ReachLabels &R, bool p_side, uint64_t x, std::vector<uint32_t> &out,
                 uint64_t &mask);
-// the smallest head (8, 16 or 32 words) whose inline entries (head - 4) hold >= 95% of the
-// non-empty lists; fit[k]: lists of at most (8 << k) - 4 entries
-uint32_t pick_head(uint64_t nonempty, const uint64_t fit[3]);
+// the head size from the list lengths; fit[k]: non-empty lists of at most (8 << k) - 4
+// entries (k = 0..3: heads of 8, 16, 32, 64 words).  A random head read costs one 128-byte
+// line whether the head has 8, 16 or 32 words (profiles/r06/probe), a 64-word head two, about
+// what the dense pass spends on 8-10% of the requests (config #2, round 5): 64 words when
+// they hold >= 10% more of the non-empty lists inline than 32 words, else the smallest of 8,
+// 16, 32 words that holds (within 0.1%) as many lists inline as 32 words
+uint32_t pick_head(uint64_t nonempty, const uint64_t fit[4]);
 // S heads: every node, and on a writable snapshot every reserved id too (n_cap)
 uint64_t label_s_nodes(const Snapshot &s);
 // the KETOGPU_LABEL_REST_PERMILLE test knob: S head of x marked kNoLabel
 bool label_nolabel(uint64_t x, uint32_t permille);
 
 struct LabelIndex {
-    uint32_t hs = 16, hp = 8;            // head words of S and P
+    uint32_t hs = 16, hp = 8;            // head words of S and P (8, 16, 32 or 64)
     std::vector<uint32_t> S, P;          // heads then overflow lists
     uint64_t s_nodes = 0, p_nodes = 0;
     uint64_t s_entries = 0, p_entries = 0;    // list entries (masks not counted)

@@ -182,6 +182,45 @@ def test_label_resident_calls_repeat(n_req, fuse, monkeypatch):
     assert eng.last_stats()["rest_requests"] > 0 and n > 0
 
 
+@pytest.mark.parametrize("n_req", [1000, 5003, 70000])
+def test_label_pipelined_calls(n_req, monkeypatch):
+    """ketogpu_queries_run_async: plan-label calls enqueued back to back without a host wait
+    (no head unlabelled, no wildcard root: no request can need the second stage), two
+    batches interleaved, a host call in between; every batch's bits equal the oracle once
+    the engine is waited for.  With unlabelled heads (the test knob) or wildcard roots the
+    call runs synchronously and says so"""
+    monkeypatch.setenv("KETOGPU_UNITS", "label")
+    namespaces, rows, reqs = randgraph.make_family_graph(92)
+    snap = Snapshot.from_rows(namespaces, rows, sort=True)
+    want = np.asarray(randgraph.oracle_store(namespaces, rows).check_batch(reqs), dtype=bool)
+    roots, targets = snap.resolve_many([(ns, o, r, rt.subject_from_dict(x)) for ns, o, r, x in reqs])
+    reps = -(-n_req // len(roots))
+    roots, targets, want = (np.tile(x, reps)[:n_req] for x in (roots, targets, want))
+    eng = check.Engine(snap)
+    q = eng.upload(roots, targets)
+    q2 = eng.upload(roots[::-1].copy(), targets[::-1].copy())
+    q.run()  # (the first call: synchronized, clears)
+    queued = [q.run(pipelined=True) for _ in range(3)] + [q2.run(pipelined=True), q.run(pipelined=True)]
+    assert all(queued)
+    eng.wait()
+    np.testing.assert_array_equal(q.download(), want)
+    np.testing.assert_array_equal(q2.download(), want[::-1])
+    np.testing.assert_array_equal(eng.check_ids(roots, targets), want)  # a host call in between
+    for _ in range(4):
+        assert q2.run(pipelined=True)
+    np.testing.assert_array_equal(q2.download(), want[::-1])  # (download waits)
+    assert eng.last_stats()["plan"] == 7
+    # second-stage requests possible: synchronous calls
+    monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", "250")
+    eng2 = check.Engine(snap)
+    q3 = eng2.upload(roots, targets)
+    assert not q3.run(pipelined=True)
+    np.testing.assert_array_equal(q3.download(), want)
+    assert not q3.run(pipelined=True)
+    np.testing.assert_array_equal(q3.download(), want)
+    assert eng2.last_stats()["rest_requests"] > 0
+
+
 @pytest.fixture
 def global_path(monkeypatch):
     """engines created while active use only the global multi-word path"""

@@ -68,11 +68,23 @@ def main():
             ms.append(eng.last_stats()["main_ms"])
         dt_res = (time.perf_counter() - t0) / a.steps
         st = eng.last_stats()
+        t0 = time.perf_counter()  # pipelined: no host wait per call (ketogpu_queries_run_async)
+        for _ in range(a.steps):
+            q.run(pipelined=True)
+        eng.wait()
+        dt_pipe = (time.perf_counter() - t0) / a.steps
+        assert np.array_equal(q.download(), ref if ref is not None else got)
+        eng.set_events(True)  # the first stage's own time and the dense pass's requests
+        q.run()
+        st_ev = eng.last_stats()
+        eng.set_events(False)
         if ref is None:
             ref = got
         print(json.dumps({"heads": h, "s_head": st["label_s_head"], "p_head": st["label_p_head"],
                           "plan": st["plan"], "host_checks_per_s": round(n / dt, 1), "host_kernel_ms": round(st_h["main_ms"], 4),
-                          "hbm_checks_per_s": round(n / dt_res, 1), "hbm_kernel_ms": round(float(np.median(ms)), 4),
+                          "hbm_checks_per_s": round(n / dt_res, 1), "pipelined_checks_per_s": round(n / dt_pipe, 1),
+                          "first_stage_ms": round(st_ev["main_ms"], 4), "dense_requests": st_ev["full_requests"],
+                          "rest_requests": st_ev["rest_requests"], "after_first_stage_ms": round(st_ev["rest_ms"], 4),
                           "main_bytes": st["main_bytes"], "label_bytes": st["label_bytes"],
                           "engine_s": round(t_eng, 2), "mismatches_vs_first": int((got != ref).sum()),
                           "positives_denied": int((pos & ~got.astype(bool)).sum())}), flush=True)
