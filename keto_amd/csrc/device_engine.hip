@@ -40,6 +40,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -2661,7 +2662,8 @@ __device__ __forceinline__ uint32_t label_block8(const uint32_t *L, uint32_t x) 
 // other list in LDS by label_block8 (two dependent LDS rounds); 2: the same by a binary search
 // (log2(E) dependent rounds: config #3's long lists pay for it); 1: every lane reads the
 // shorter list's entries and compares them with its quarter of the other head in registers
-// (measured 2.8x slower at 64-word heads, profiles/r06/ab)
+// (measured 2.8x slower at 64-word heads, profiles/r06/ab).  Four lookups per lane in flight
+// at once instead of one at a time: no faster (config #3 shape), 10% slower (config #2)
 #ifndef KETO_LABEL_MEET
 #define KETO_LABEL_MEET 0
 #endif
@@ -4543,6 +4545,9 @@ struct ketogpu_engine {
     // no head marked by a write (lab_invalid), no request of a batch without wildcard roots
     // can go to the second stage
     uint64_t label_nolabel_heads = 0;
+    bool plan_auto = false;  // KETOGPU_UNITS=auto (the default)
+    // lists kept in the overflow region / non-empty lists, per side (the build's histogram)
+    double label_overflow_share[2] = {0, 0};
     uint32_t label_knob = 0;
     bool label_rest_free(const Batch &q) const {
         return use_label && label_nolabel_heads == 0 && label_knob == 0 && lab_invalid == 0 && !q.has_dyn;
@@ -4852,6 +4857,7 @@ struct ketogpu_engine {
     }
     uint64_t sync() {
         const Snapshot &s = *snap;
+        if (bg && bg->done.load(std::memory_order_acquire)) finish_relabel();  // (its rows are the synced ones)
         if (!s.writable || synced_version == s.version) return 0;
         HIP_CHECK(hipSetDevice(device));
         std::vector<uint32_t> fr, rr;
@@ -4931,6 +4937,10 @@ struct ketogpu_engine {
     void label_update(const std::vector<uint32_t> &fr, const std::vector<uint32_t> &rr) {
         const Snapshot &s = *snap;
         if (!s.writable || !lab_R) return;
+        if (bg) {  // a background relabel in flight: its swap re-applies every row changed since its copy
+            bg->fr.insert(bg->fr.end(), fr.begin(), fr.end());
+            bg->rr.insert(bg->rr.end(), rr.begin(), rr.end());
+        }
         const ReachLabels &R = *lab_R;
         std::vector<uint32_t> seeds;
         for (uint32_t v : fr)
@@ -5014,7 +5024,79 @@ struct ketogpu_engine {
         }
         uint64_t limit = 20;
         if (const char *e = getenv("KETOGPU_LABEL_RELABEL_PERMILLE")) limit = strtoull(e, nullptr, 10);
-        if (lab_invalid * 1000 > limit * std::max<uint64_t>(s.Nx, 1)) relabel();
+        if (!bg && lab_invalid * 1000 > limit * std::max<uint64_t>(s.Nx, 1)) {
+            static const bool inline_relabel = getenv("KETOGPU_LABEL_RELABEL_SYNC") != nullptr;
+            if (inline_relabel)
+                relabel();
+            else
+                start_relabel();
+        }
+    }
+
+    // Background relabel: the 2-hop labels of the current interior graph are built on a host
+    // thread from a copy of it (copy_interior), so the write that crossed the threshold — and
+    // the writes after it — return without waiting; until the swap, marked roots keep going
+    // to the second stage over the live rows.  The swap (at the first engine sync after the
+    // build finished, finish_relabel) builds the head arrays from the new labels over the
+    // current rows and then applies label_update to every row changed since the copy,
+    // against the interior successor hashes of the copy: exact by label_update's own argument
+    // (the labels are those of the copied interior graph; a root reaching an interior row
+    // changed since is marked).  KETOGPU_LABEL_RELABEL_SYNC=1: the relabel inline (A/B).
+    struct BgRelabel {
+        std::thread th;
+        std::atomic<bool> done{false};
+        std::shared_ptr<ReachLabels> R;   // the new labels (null: the build failed)
+        std::vector<uint64_t> succ;       // interior successor hashes of the copy
+        std::vector<uint32_t> fr, rr;     // rows changed since the copy
+        std::string error;
+    };
+    std::unique_ptr<BgRelabel> bg;
+    uint64_t lab_bg_started = 0;
+    void start_relabel() {
+        const Snapshot &s = *snap;
+        auto b = std::make_unique<BgRelabel>();
+        auto c = std::make_shared<InteriorCsr>();
+        copy_interior(s, *c);  // (under the caller's snapshot lock)
+        b->succ.resize(s.Ni);
+        for (uint32_t v = 0; v < s.Ni; v++) b->succ[v] = succ_hash(s, v);
+        const uint64_t version = s.version;
+        BgRelabel *bp = b.get();
+        bp->th = std::thread([bp, c, version] {
+            try {
+                auto R = std::make_shared<ReachLabels>();
+                build_reach_labels_csr(c->n, c->f_off.data(), c->f_col.data(), c->b_off.data(), c->b_col.data(), *R);
+                R->version = version;
+                bp->R = std::move(R);
+            } catch (const std::exception &e) {
+                bp->error = e.what();
+            }
+            bp->done.store(true, std::memory_order_release);
+        });
+        bg = std::move(b);
+        lab_bg_started++;
+    }
+    void finish_relabel() {
+        std::unique_ptr<BgRelabel> b = std::move(bg);
+        b->th.join();
+        if (!b->R) {  // the build failed: the relabel inline (it reports its own failure)
+            fprintf(stderr, "[ketogpu] background relabel failed (%s): relabelling inline\n", b->error.c_str());
+            relabel();
+            return;
+        }
+        uint32_t *A[2] = {const_cast<uint32_t *>(lgraph.S), const_cast<uint32_t *>(lgraph.P)};
+        release_label(A);
+        lgraph = LabelGraph{nullptr, nullptr, 0};
+        lab_R.reset();
+        use_label = true;
+        build_label(*snap, b->R);
+        if (!use_label || !lab_R) return;  // (the heads did not fit: plan lite, as build_label decided)
+        lab_succ = std::move(b->succ);  // the interior graph the labels describe
+        for (auto *v : {&b->fr, &b->rr}) {
+            std::sort(v->begin(), v->end());
+            v->erase(std::unique(v->begin(), v->end()), v->end());
+        }
+        label_update(b->fr, b->rr);
+        lab_relabels++;
     }
 
     // the labels rebuilt from the current rows (the old arrays freed first)
@@ -5029,6 +5111,7 @@ struct ketogpu_engine {
     }
 
     ~ketogpu_engine() {
+        if (bg && bg->th.joinable()) bg->th.join();  // (a background relabel reads only its own copy)
         if (snap_link) {
             std::lock_guard<std::mutex> lk(snap_link->mu);
             if (snap_link->snap) snap_link->snap->reader_gone(this);
@@ -5183,6 +5266,7 @@ struct ketogpu_engine {
         // plan label first: when its labels are built every request but wildcard roots is
         // one intersection, so neither plan core's index nor the hub index is built, and no
         // trials run (KETOGPU_UNITS=auto)
+        plan_auto = p == "auto";
         if (use_label) build_label(s);
         g.both_max = kBothMax;
         g.seed_shift = 0;
@@ -5324,7 +5408,7 @@ struct ketogpu_engine {
     // records (checked before they are allocated).  On success the plan is label without
     // trials, and plan core and the hub index are skipped; on failure the engine goes on as
     // if labels had not been asked for.
-    void build_label(const Snapshot &s) {
+    void build_label(const Snapshot &s, std::shared_ptr<const ReachLabels> given = nullptr) {
         const auto t0 = std::chrono::steady_clock::now();
         size_t free_b = 0, total_b = 0;
         HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -5364,7 +5448,7 @@ struct ketogpu_engine {
                 nolabel = li.s_nolabel;
                 s_entries = li.s_entries;
             } else {
-                const std::shared_ptr<const ReachLabels> R = reach_labels_of(s);
+                const std::shared_ptr<const ReachLabels> R = given ? given : reach_labels_of(s);
                 label_pll_ms = R->ms;
                 label_entries = R->in.size() + R->out.size();
                 auto up = [&](const auto &v) {
@@ -5542,6 +5626,7 @@ struct ketogpu_engine {
                         s_entries += tally[0];
                         nolabel += tally[1];
                     }
+                    label_overflow_share[side] = ne ? (double)(tally[2] + nbig) / (double)ne : 0.0;
                     if (cascade_log)
                         fprintf(stderr, "[label] %s heads: %u nodes, %u words each, %llu lists in overflow, %u long lists "
                                         "built on the host, %.2f GB\n",
@@ -5603,12 +5688,20 @@ struct ketogpu_engine {
             for (uint64_t x = 0; x < s.N; x++) ne += s.rev_off[x + 1] > s.rev_off[x];
             label_coverage = ne ? 1.0 - (double)nolabel / (double)ne : 1.0;
         }
-        // the plan, without trials; neither plan core nor the hubs are built
+        // the plan; neither plan core nor the hubs are built.  Without trials — unless (auto)
+        // a quarter or more of one side's lists overflow their heads: the dense pass would
+        // then answer many requests, so the first batches of >= kTrialMin requests also time
+        // plan lite (the traversal over the records, no index) and the faster one is kept
         use_core = false;
         use_bidi = true;
         bidi_cfg = BidiCfg{9, 64, kLiteF, 7, 16, 1, 3};
         trials_left = 0;
         candidates.clear();
+        if (plan_auto && use_lite && std::max(label_overflow_share[0], label_overflow_share[1]) >= 0.25) {
+            candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 3});  // plan label
+            candidates.push_back({true, 9, 64, kLiteF, 7, 0, true, 16, 1, 1});  // plan lite
+            trials_left = kTrialRuns;
+        }
         label_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (cascade_log)
             fprintf(stderr, "[label] %u landmarks, %llu label entries (%.1f ms); S heads %u words (%llu entries), P heads "
@@ -5811,7 +5904,7 @@ struct ketogpu_engine {
                         lgraph, q.allowed, label_rest(q.n), label_full(q.n), &spill_count[0], &spill_count[7],
                         fused ? nullptr : st.stats + 4 * kStatSlots, fused ? d_hctr + 16 : nullptr);
             });
-        if (fused && pipelined_req && label_rest_free(q)) {
+        if (fused && pipelined_req && !trials_left && label_rest_free(q)) {
             // a pipelined lean call (ketogpu_queries_run_async): no request of this batch can
             // be listed for the second stage (label_rest_free), so nothing after the dense pass
             // depends on the lists' totals: the call returns without a host wait.  The results

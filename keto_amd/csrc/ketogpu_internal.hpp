@@ -16,6 +16,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -221,10 +222,15 @@ struct Snapshot {
         }
     }
     mutable std::shared_mutex mu;       // writes exclusive; engine, resolve and expand calls shared
-    // derived indexes built once per snapshot and shared by its engines (labels.cpp
-    // reach_labels_of); immutable snapshots only
+    // derived indexes built once per snapshot VERSION and shared by its engines (labels.cpp
+    // reach_labels_of: a writable snapshot's writes bump the version, so a later engine sync
+    // or relabel rebuilds them).  derived_mu guards only the cache and the in-flight build's
+    // future: the build itself runs outside it, and engines asking for the same version while
+    // it runs wait on that future instead of building again
     mutable std::mutex derived_mu;
     mutable std::shared_ptr<const ReachLabels> reach_cache;
+    mutable std::shared_future<std::shared_ptr<const ReachLabels>> reach_building;
+    mutable uint64_t reach_building_version = ~0ull;
     // An engine's way back to its snapshot at teardown: the snapshot's destructor clears it,
     // so an engine freed after its snapshot (a garbage collector's order) skips the
     // deregistration instead of touching freed memory.

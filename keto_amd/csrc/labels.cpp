@@ -151,6 +151,24 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out) {
     build_reach(a, s.Ni, out);
 }
 
+void copy_interior(const Snapshot &s, InteriorCsr &out) {
+    IAdj a;
+    make_adj(s, a);
+    const uint32_t n = s.Ni;
+    out.n = n;
+    for (int d = 0; d < 2; d++) {
+        std::vector<uint64_t> &off = d == 0 ? out.f_off : out.b_off;
+        std::vector<uint32_t> &col = d == 0 ? out.f_col : out.b_col;
+        off.assign((size_t)n + 1, 0);
+        for (uint32_t v = 0; v < n; v++) off[v + 1] = off[v] + a.deg[d][v];
+        col.resize(off[n]);
+        parallel_chunks(n, 1 << 14, [&](int, uint64_t b, uint64_t e) {
+            for (uint64_t v = b; v < e; v++)
+                std::copy(a.col[d] + a.beg[d][v], a.col[d] + a.beg[d][v] + a.deg[d][v], col.begin() + (ptrdiff_t)off[v]);
+        });
+    }
+}
+
 void build_reach_labels_csr(uint32_t n, const uint64_t *f_off, const uint32_t *f_col, const uint64_t *b_off,
                             const uint32_t *b_col, ReachLabels &out) {
     out = ReachLabels{};
@@ -309,14 +327,42 @@ void build_reach(IAdj &a, uint32_t n, ReachLabels &out) {
 }  // namespace
 
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s) {
-    std::lock_guard<std::mutex> lk(s.derived_mu);
-    if (!s.reach_cache || s.reach_cache->version != s.version) {  // (a writable snapshot's writes bump it)
-        auto R = std::make_shared<ReachLabels>();
-        build_reach_labels(s, *R);
-        R->version = s.version;
-        s.reach_cache = std::move(R);
+    // (callers hold the snapshot's shared lock: the version cannot change during the build)
+    std::promise<std::shared_ptr<const ReachLabels>> mine;
+    std::shared_future<std::shared_ptr<const ReachLabels>> wait;
+    {
+        std::lock_guard<std::mutex> lk(s.derived_mu);
+        if (s.reach_cache && s.reach_cache->version == s.version) return s.reach_cache;
+        if (s.reach_building.valid() && s.reach_building_version == s.version) {
+            wait = s.reach_building;  // another engine builds this version: wait for it
+        } else {
+            s.reach_building = mine.get_future().share();
+            s.reach_building_version = s.version;
+        }
     }
-    return s.reach_cache;
+    if (wait.valid()) return wait.get();  // (rethrows the builder's error)
+    try {
+        auto R = std::make_shared<ReachLabels>();
+        build_reach_labels(s, *R);  // outside derived_mu
+        R->version = s.version;
+        std::shared_ptr<const ReachLabels> done = std::move(R);
+        {
+            std::lock_guard<std::mutex> lk(s.derived_mu);
+            s.reach_cache = done;
+            s.reach_building = {};
+            s.reach_building_version = ~0ull;
+        }
+        mine.set_value(done);
+        return done;
+    } catch (...) {
+        {
+            std::lock_guard<std::mutex> lk(s.derived_mu);
+            s.reach_building = {};
+            s.reach_building_version = ~0ull;
+        }
+        mine.set_exception(std::current_exception());
+        throw;
+    }
 }
 
 namespace {

@@ -80,6 +80,15 @@ void build_reach_labels(const Snapshot &s, ReachLabels &out);
 // below n): the two-tier partitioned mode's replicated core (tier.cpp)
 void build_reach_labels_csr(uint32_t n, const uint64_t *f_off, const uint32_t *f_col, const uint64_t *b_off,
                             const uint32_t *b_col, ReachLabels &out);
+// the interior graph as CSR copies (a writable snapshot: its real entries only, as
+// build_reach_labels sees them): what a background relabel builds from while the snapshot
+// keeps taking writes (device_engine.hip start_relabel)
+struct InteriorCsr {
+    uint32_t n = 0;
+    std::vector<uint64_t> f_off, b_off;
+    std::vector<uint32_t> f_col, b_col;
+};
+void copy_interior(const Snapshot &s, InteriorCsr &out);
 // the snapshot's labels, built once per snapshot version and shared by every engine over
 // it (ketogpu_multi_new builds one set for all devices)
 std::shared_ptr<const ReachLabels> reach_labels_of(const Snapshot &s);

@@ -217,13 +217,14 @@ def _tuple(r, id2name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("plan", ["label", "label-marks", "label-relabel", "lite"])
+@pytest.mark.parametrize("plan", ["label", "label-marks", "label-relabel", "label-relabel-sync", "lite"])
 def test_versioned_engine_writes_in_place_and_reads_them(plan, monkeypatch):
     """read-your-writes against the oracle after every batch; most batches in place, a
     batch with a new group through the rebuild.  Plan label keeps its labels exact in place
     (label_update: changed rows' heads rewritten, roots above a changed nesting edge sent to
     the second stage), relabelling past the default share of marked heads, never
-    (label-marks) or at every marked head (label-relabel); plan lite for comparison"""
+    (label-marks) or at every marked head (label-relabel: in the background, swapped in at a
+    later sync; label-relabel-sync: inline); plan lite for comparison"""
     from keto_amd.freshness import VersionedEngine
     if L.lib().ketogpu_device_count() < 1:
         pytest.fail("no HIP device visible")
@@ -231,8 +232,10 @@ def test_versioned_engine_writes_in_place_and_reads_them(plan, monkeypatch):
         monkeypatch.setenv("KETOGPU_NO_LABEL", "1")
     elif plan == "label-marks":
         monkeypatch.setenv("KETOGPU_LABEL_RELABEL_PERMILLE", "1000")
-    elif plan == "label-relabel":
+    elif plan.startswith("label-relabel"):
         monkeypatch.setenv("KETOGPU_LABEL_RELABEL_PERMILLE", "0")
+        if plan == "label-relabel-sync":
+            monkeypatch.setenv("KETOGPU_LABEL_RELABEL_SYNC", "1")
     namespaces, rows = _graph(331, n_rows=700, n_obj=25, n_users=30)
     ve = VersionedEngine(Snapshot.from_rows(namespaces, rows, sort=True, writable=True))
     id2name = {i: n for n, i in namespaces}
@@ -273,8 +276,43 @@ def test_versioned_engine_writes_in_place_and_reads_them(plan, monkeypatch):
     assert paths.count("in_place") >= 5 and "rebuild" in paths, paths
     if plan == "label-marks":
         assert marks > 0 and relabels == 0  # nesting edges changed: roots marked, never relabelled
-    if plan == "label-relabel":
+    if plan == "label-relabel-sync":
         assert relabels > 0
+
+
+@pytest.mark.gpu
+def test_checks_during_a_background_relabel(monkeypatch):
+    """a write that marks roots starts a background relabel (KETOGPU_LABEL_RELABEL_PERMILLE=0:
+    at the first mark) and returns; checks run while the labels are built (marked roots on
+    the second stage) and after the swap (the new heads, every row changed since the copy
+    re-applied), each batch equal to the oracle, until the engine reports the relabel"""
+    import time as _time
+    from keto_amd.freshness import VersionedEngine
+    monkeypatch.setenv("KETOGPU_LABEL_RELABEL_PERMILLE", "0")
+    namespaces, rows = _graph(337, n_rows=700, n_obj=25, n_users=30)
+    ve = VersionedEngine(Snapshot.from_rows(namespaces, rows, sort=True, writable=True))
+    id2name = {i: n for n, i in namespaces}
+    cur = sorted(rows, key=_sqlite_key)
+    swapped = 0
+    for step in range(4):
+        ins, dele = _writes(460 + step, namespaces, cur)
+        ve.transact(insert=[_tuple(r, id2name) for r in ins], delete=[_tuple(d, id2name) for d in dele])
+        cur = _expected(cur, ins, dele)
+        reqs = randgraph.make_requests(560 + step, namespaces, cur, n=400, wildcard=False)
+        want = [bool(x) for x in randgraph.oracle_store(namespaces, cur).check_batch(reqs)]
+        tuples = [rt.InternalRelationTuple(ns, o, r, rt.subject_from_dict(s)) for ns, o, r, s in reqs]
+        eng = ve._state[1]
+        before = eng.last_stats()["label_relabels"] if step else 0
+        for k in range(200):  # checks while the relabel runs, then after its swap
+            assert ve.check_many(tuples) == want, (step, k)
+            st = eng.last_stats()
+            assert st["plan"] == 7
+            if st["label_relabels"] > before:
+                swapped += 1
+                break
+            _time.sleep(0.01)
+        assert ve.check_many(tuples) == want
+    assert swapped > 0
 
 
 def test_hub_fanout_is_refused_past_the_budget(monkeypatch):

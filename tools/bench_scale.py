@@ -175,11 +175,21 @@ def main():
         q.run()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    got_sync = q.download()
+    # pipelined: the same steps enqueued without a host wait per call (ketogpu_queries_run_async)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    queued = sum(q.run(pipelined=True) for _ in range(a.steps))
+    eng.wait()
+    torch.cuda.synchronize()
+    dt_pipe = time.perf_counter() - t0
+    assert np.array_equal(q.download(), got_sync)
     eng.set_events(True)  # the first stage's own time: one more run with events between the kernels
     q.run()
     eng.set_events(False)
     rs = eng.last_stats()
     got = q.download()
+    assert np.array_equal(got, got_sync)
     log(f"timed: {len(roots) * a.steps / dt:.4g} checks/s, {dt / a.steps * 1e3:.3f} ms/step, plan "
         f"{check_plan(rs['plan'])}, spilled units {rs['spilled_units']}, spilled requests {rs['spilled_requests']}, "
         f"positives denied {int((pos & ~got.astype(bool)).sum())}")
@@ -198,6 +208,8 @@ def main():
     # a first result line now: a run cut short in the oracle phase still reports the timing
     print(json.dumps({"workload": f"{a.workload}_{a.tuples}", "phase": "timed", "checks": len(roots),
                       "checks_per_s": round(len(roots) * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 4),
+                      "pipelined_checks_per_s": round(len(roots) * a.steps / dt_pipe, 1),
+                      "main_kernel_ms": round(rs["main_ms"], 4), "dense_pass_requests": rs["full_requests"],
                       "plan": check_plan(rs["plan"]), "positives_denied": int((pos & ~got.astype(bool)).sum()),
                       "cross_check": {"sample": int(len(idx)), "mismatches": xmism}, "r2_check": r2}), flush=True)
     oracle = None
@@ -245,7 +257,11 @@ def main():
                                      "nodes_per_tree": round(float(np.mean(nodes)), 1), "max_nodes": int(max(nodes))}
     log(f"expand: {exp}")
     out = {"workload": f"{a.workload}_{a.tuples}", "checks": len(roots), "checks_per_s": round(len(roots) * a.steps / dt, 1),
-           "ms_per_step": round(dt / a.steps * 1e3, 4), "main_kernel_ms": round(rs["main_ms"], 4),
+           "ms_per_step": round(dt / a.steps * 1e3, 4),
+           "pipelined_checks_per_s": round(len(roots) * a.steps / dt_pipe, 1),
+           "pipelined_ms_per_step": round(dt_pipe / a.steps * 1e3, 4), "pipelined_calls_queued": int(queued),
+           "main_kernel_ms": round(rs["main_ms"], 4), "dense_pass_requests": rs["full_requests"],
+           "after_first_stage_ms": round(rs["rest_ms"], 4),
            "main_bytes": rs["main_bytes"], "spilled_units": rs["spilled_units"],
            "spilled_requests": rs["spilled_requests"], "allowed_fraction": round(float(got.mean()), 4),
            "constructed_positives": int(pos.sum()), "positives_denied": int((pos & ~got).sum()),

@@ -74,7 +74,12 @@ def main():
     p.add_argument("--sizes", default="1,10,100,1000,10000")
     p.add_argument("--sample", type=int, default=100_000)
     p.add_argument("--nest", type=int, default=20, help="nesting rows written last (the interior graph changes)")
+    p.add_argument("--relabel-permille", type=int, default=None,
+                   help="KETOGPU_LABEL_RELABEL_PERMILLE for the writable engine (e.g. 2: the nesting write crosses "
+                        "it and starts a background relabel, timed to its swap)")
     a = p.parse_args()
+    if a.relabel_permille is not None:
+        os.environ["KETOGPU_LABEL_RELABEL_PERMILLE"] = str(a.relabel_permille)
     f = a.tuples / 50e6
     w = synth.rbac(users=int(10e6 * f), groups=int(100e3 * f), docs=int(2e6 * f), tuples=a.tuples, checks=1_000_000,
                    check_seed=synth.SEED + 1)
@@ -168,6 +173,30 @@ def main():
                          label_relabels=st["label_relabels"], rest_requests=st["rest_requests"])
         out["nest_write"] = entry
         log(f"nesting write {entry}")
+        if res["applied"] and a.relabel_permille is not None:
+            # a background relabel started by the write: checks while it runs, the swap (at an
+            # engine sync once the labels are built), checks after it
+            before = st["label_relabels"]
+            t_w = time.perf_counter()
+            during = round(timed_host(ew, wroots, wtargets))
+            swap_sync_ms = None
+            while time.perf_counter() - t_w < 120:
+                t2 = time.perf_counter()
+                ew.sync()
+                ew.check_ids(wroots[:1], wtargets[:1])
+                dt2 = (time.perf_counter() - t2) * 1e3  # (the swap runs in whichever of the two syncs first)
+                if ew.last_stats()["label_relabels"] > before:
+                    swap_sync_ms = round(dt2, 3)
+                    break
+                time.sleep(0.005)
+            swap_s = round(time.perf_counter() - t_w, 3)
+            after = round(timed_host(ew, wroots, wtargets))
+            st = ew.last_stats()
+            out["background_relabel"] = {"relabel_permille": a.relabel_permille, "checks_host_during": during,
+                                         "swapped_after_s": swap_s, "swap_sync_ms": swap_sync_ms,
+                                         "checks_host_after": after, "label_relabels": st["label_relabels"],
+                                         "label_marked_after": st["label_marked"], "plan": st["plan"]}
+            log(f"background relabel {out['background_relabel']}")
 
     # the rebuild path on the compact snapshot, and the cross-check
     t0 = time.time()
