@@ -2657,13 +2657,21 @@ __device__ __forceinline__ uint32_t label_block8(const uint32_t *L, uint32_t x) 
     return r;
 }
 
+// x in the head image `row` (LDS) among its first E entries (H: the head's words)
+template <int E, int H, bool LOWER>
+__device__ __forceinline__ uint32_t label_lookup(const uint32_t *row, uint32_t x) {
+    return label_block8<E, LOWER>(row + kHeadFixed, x);
+}
+
 // KETO_LABEL_MEET: how the shorter inline landmark list meets the other head.  0 (default):
 // the shorter list's entries round-robin over the request's four lanes, each looked up in the
 // other list in LDS by label_block8 (two dependent LDS rounds); 2: the same by a binary search
 // (log2(E) dependent rounds: config #3's long lists pay for it); 1: every lane reads the
 // shorter list's entries and compares them with its quarter of the other head in registers
 // (measured 2.8x slower at 64-word heads, profiles/r06/ab).  Four lookups per lane in flight
-// at once instead of one at a time: no faster (config #3 shape), 10% slower (config #2)
+// at once instead of one at a time: no faster (config #3 shape), 10% slower (config #2); the
+// block splitters stored as a row of their own (two 16-byte reads instead of one word per
+// block): 8% slower on the config #3 shape, equal on config #2
 #ifndef KETO_LABEL_MEET
 #define KETO_LABEL_MEET 0
 #endif
@@ -2710,7 +2718,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     wave_sync();  // (the images: this wave's own rows)
     bool hit = labelled && (smask & pmask) != 0;
     // S's inline landmarks: its inline entries below Ni (the raw entries follow them)
-    const uint32_t es = !labelled ? 0u : KETO_LABEL_MEET == 2 ? label_lower_e<CS>(Se, L.ni) : label_block8<CS, true>(Se, L.ni);
+    const uint32_t es = !labelled ? 0u : KETO_LABEL_MEET == 2 ? label_lower_e<CS>(Se, L.ni) : label_lookup<CS, HS, true>(Sl, L.ni);
     const uint32_t ep = min(np, CP);
     // 1. the inline landmark prefixes: the shorter walked, round-robin over the request's
     //    four lanes, each entry searched in the other; the one-edge test (a non-interior root
@@ -2738,10 +2746,10 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
             if (sub == 3 && !hit && r >= L.ni) hit = label_find_e<CS>(Se, r);
         } else {
             if (es <= ep)
-                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_block8<CP, false>(Pe, Se[k]);
+                for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_lookup<CP, HP, false>(Pl, Se[k]);
             else
-                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_block8<CS, false>(Se, Pe[k]);
-            if (sub == 3 && !hit && r >= L.ni) hit = label_block8<CS, false>(Se, r);
+                for (uint32_t k = sub; k < ep && !hit; k += 4) hit = label_lookup<CS, HS, false>(Sl, Pe[k]);
+            if (sub == 3 && !hit && r >= L.ni) hit = label_lookup<CS, HS, false>(Sl, r);
         }
     }
     // 2. a request neither hit nor settled by its heads (labels.hpp): listed for
