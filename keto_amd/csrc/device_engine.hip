@@ -4399,6 +4399,10 @@ struct ketogpu_queries {
     // the flag words are all zero (the last run on this batch was a plan-label call that
     // wrote none): with the engine's label_clean, the next such call skips the clear
     bool flags_zero = false;
+    // the end of this batch's last call queued without a wait (ketogpu_queries_run_async):
+    // its download waits for that call alone
+    hipEvent_t done_ev = nullptr;
+    bool pending = false;
     Batch batch() const {
         Batch b;
         b.roots = d_roots;
@@ -4418,6 +4422,7 @@ struct ketogpu_queries {
         for (void *p : {(void *)d_roots, (void *)d_targets, (void *)d_allowed, (void *)d_flags, (void *)d_dyn_int_off,
                         (void *)d_dyn_full_off, (void *)d_dyn_int, (void *)d_dyn_full, (void *)d_dyn_amb})
             if (p) (void)hipFree(p);
+        if (done_ev) (void)hipEventDestroy(done_ev);
     }
 };
 
@@ -4519,22 +4524,27 @@ struct ketogpu_engine {
     // them: every request but wildcard roots is one intersection)
     bool use_label = false;
     LabelGraph lgraph{};
-    unsigned int *rest_counts = nullptr;  // rest and full lists: two sets each of kRestShards counters, one cache line each
-    uint64_t label_calls = 0;             // selects the set
+    // rest and full lists: four sets each of kRestShards counters, one cache line each; call k
+    // uses set k % 4 and clears set (k + 2) % 4 for call k + 2 — the next call on the same
+    // stream when pipelined calls alternate between two streams (ketogpu_queries_run_async),
+    // so a call's dense pass may still read its counters while the next call's first stage runs
+    static constexpr unsigned kLabelSets = 4;
+    unsigned int *rest_counts = nullptr;
+    uint64_t label_calls = 0;  // selects the set
     LabelRest label_rest(uint64_t n) {    // this call's rest list over requests [0, n)
         const uint64_t units = (n + 15) / 16;
-        const unsigned set = (unsigned)(label_calls & 1);
+        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + 2) % kLabelSets);
         return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
-                         rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
+                         rest_counts + next * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
     }
     LabelRest label_full(uint64_t n) {  // this call's list for label_full_kernel (records)
         const uint64_t units = (n + 15) / 16;
-        const unsigned set = 2 + (unsigned)(label_calls & 1);
-        return LabelRest{nullptr, rest_counts + set * kRestShards * kRestStride,
-                         rest_counts + (set ^ 1) * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards),
-                         full_rec};
+        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + 2) % kLabelSets);
+        return LabelRest{nullptr, rest_counts + (kLabelSets + set) * kRestShards * kRestStride,
+                         rest_counts + (kLabelSets + next) * kRestShards * kRestStride,
+                         16 * ((units + kRestShards - 1) / kRestShards), full_rec + (uint64_t)set * 2 * spill_cap};
     }
-    uint4 *full_rec = nullptr;  // plan label's full list: two records per request (2 x spill_cap, LabelRest::rec)
+    uint4 *full_rec = nullptr;  // plan label's full list per set: two records per request (kLabelSets x 2 x spill_cap)
     // KETOGPU_LABEL_FUSE=0: no lean calls (statistics, their reduction and the clear in
     // every call; A/B)
     bool fuse_reduce = [] {
@@ -4549,6 +4559,22 @@ struct ketogpu_engine {
     // ketogpu_queries_run_async: this call may return before the device finishes (set per
     // call); `queued`: the last call did
     bool pipelined_req = false, queued = false;
+    // pipelined calls alternate between `stream` and `stream2` (by label_calls' parity), so
+    // a call's dense pass overlaps the next call's first stage; pipe_ev: recorded after the
+    // last queued call on stream2, waited for (on `stream`, by the device) before any other
+    // work of the engine (drain_pipe)
+    hipEvent_t pipe_ev = nullptr;
+    bool pipe_pending = false;
+    // the batch each stream's last queued call ran over, and that call's end: two calls over
+    // the SAME batch never overlap (they write one result array), the second waits for the first
+    const ketogpu_queries *pipe_q[2] = {nullptr, nullptr};
+    hipEvent_t pipe_end[2] = {nullptr, nullptr};
+    void drain_pipe() {
+        pipe_q[0] = pipe_q[1] = nullptr;
+        if (!pipe_pending) return;
+        HIP_CHECK(hipStreamWaitEvent(stream, pipe_ev, 0));
+        pipe_pending = false;
+    }
     // heads marked kNoLabel by the build (the test knob) and the knob itself: with none, and
     // no head marked by a write (lab_invalid), no request of a batch without wildcard roots
     // can go to the second stage
@@ -4865,6 +4891,7 @@ struct ketogpu_engine {
     }
     uint64_t sync() {
         const Snapshot &s = *snap;
+        drain_pipe();  // (every entry point syncs first: its work orders after queued calls)
         if (bg && bg->done.load(std::memory_order_acquire)) finish_relabel();  // (its rows are the synced ones)
         if (!s.writable || synced_version == s.version) return 0;
         HIP_CHECK(hipSetDevice(device));
@@ -5131,6 +5158,9 @@ struct ketogpu_engine {
             if (x) (void)hipStreamSynchronize(x);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (wait_ev) (void)hipEventDestroy(wait_ev);
+        if (pipe_ev) (void)hipEventDestroy(pipe_ev);
+        for (hipEvent_t x : pipe_end)
+            if (x) (void)hipEventDestroy(x);
         for (void *p : owned) (void)hipFree(p);
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags, (void *)full_rec})
@@ -5659,9 +5689,9 @@ struct ketogpu_engine {
             return;
         }
         if (!rest_counts) {
-            rest_counts = dalloc<unsigned int>(4 * kRestShards * kRestStride);
+            rest_counts = dalloc<unsigned int>(2 * kLabelSets * kRestShards * kRestStride);
             owned.push_back(rest_counts);
-            HIP_CHECK(hipMemset(rest_counts, 0, 4 * kRestShards * kRestStride * sizeof(unsigned int)));
+            HIP_CHECK(hipMemset(rest_counts, 0, 2 * kLabelSets * kRestShards * kRestStride * sizeof(unsigned int)));
         }
         lgraph = LabelGraph{A[1], A[0], s.Ni};
         if (s.writable) {
@@ -5834,6 +5864,8 @@ struct ketogpu_engine {
     // used as the ping-pong lists of the cascade
     void ensure_spill(uint64_t n) {
         if (n <= spill_cap) return;
+        // (a queued call on either stream may still read the lists: let them finish first)
+        if (pipe_q[0] || pipe_q[1] || pipe_pending) HIP_CHECK(hipDeviceSynchronize());
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags})
             if (p) (void)hipFree(p);
@@ -5841,7 +5873,7 @@ struct ketogpu_engine {
         spill_cap = std::max<uint64_t>(n + 2048, 1024);
         spill_units = dalloc<uint32_t>(2 * spill_cap);  // two ping-pong lists
         if (full_rec) (void)hipFree(full_rec);
-        full_rec = dalloc<uint4>(2 * spill_cap);  // two records per listed request
+        full_rec = dalloc<uint4>(kLabelSets * 2 * spill_cap);  // two records per listed request, per set
         spill_roots = dalloc<uint32_t>(spill_cap);
         spill_targets = dalloc<uint32_t>(spill_cap);
         spill_allowed = dalloc<uint64_t>(spill_cap / 64 + 1);
@@ -5996,7 +6028,7 @@ struct ketogpu_engine {
         rs.unit_launches += launched;
         const uint64_t left = cnt[ns - 1];
         if (u_prev != 1) throw Error(KETOGPU_EINVAL, "bidi cascade must end with a single-request stage");
-        if (bidi_cfg.lite == 3) label_calls++;  // the next call uses the other rest-counter set
+        if (bidi_cfg.lite == 3) label_calls++;  // the next call uses the next counter set
         if (left && cur != 0)  // single requests for the global path, read from list[0]
             HIP_CHECK(hipMemcpyAsync(list[0], list[cur], left * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
         return left;
@@ -6685,9 +6717,20 @@ struct ketogpu_engine {
         return q.release();
     }
 
-    void download(const ketogpu_queries &q, uint64_t *allowed, uint64_t *flagged) {
+    void download(ketogpu_queries &q, uint64_t *allowed, uint64_t *flagged) {
         HIP_CHECK(hipSetDevice(device));
         uint64_t words = (q.n + 63) / 64;
+        if (q.pending) {  // after this batch's queued call only (later queued calls keep running)
+            HIP_CHECK(hipStreamWaitEvent(copy_stream, q.done_ev, 0));
+            if (words && allowed)
+                HIP_CHECK(hipMemcpyAsync(allowed, q.d_allowed, words * 8, hipMemcpyDeviceToHost, copy_stream));
+            if (words && flagged)
+                HIP_CHECK(hipMemcpyAsync(flagged, q.d_flags, words * 8, hipMemcpyDeviceToHost, copy_stream));
+            HIP_CHECK(hipStreamSynchronize(copy_stream));
+            q.pending = false;
+            return;
+        }
+        drain_pipe();
         if (words && allowed)
             HIP_CHECK(hipMemcpyAsync(allowed, q.d_allowed, words * 8, hipMemcpyDeviceToHost, stream));
         if (words && flagged)
@@ -6758,6 +6801,7 @@ int ketogpu_queries_run(ketogpu_engine *e, ketogpu_queries *q) {
     std::lock_guard<std::mutex> lk(e->mu);
     e->sync();
     e->run(*q);
+    q->pending = false;  // (ran to completion)
     API_END
 }
 
@@ -6769,11 +6813,38 @@ int ketogpu_queries_run_async(ketogpu_engine *e, ketogpu_queries *q, int *queued
     e->sync();
     e->pipelined_req = true;
     e->queued = false;
+    // odd calls on the second stream: this call's first stage may run beside the previous
+    // call's dense pass (their counter sets and record regions differ, ketogpu_engine
+    // label_rest / label_full)
+    const bool other = (e->label_calls & 1) != 0 && e->use_label && e->stream2;
+    const int si = other ? 1 : 0;
+    for (int k = 0; k < 2; k++)
+        if (!e->pipe_end[k]) HIP_CHECK(hipEventCreateWithFlags(&e->pipe_end[k], hipEventDisableTiming));
+    if (e->pipe_q[si ^ 1] == q)  // the same batch queued on the other stream: after it
+        HIP_CHECK(hipStreamWaitEvent(other ? e->stream2 : e->stream, e->pipe_end[si ^ 1], 0));
+    if (other) std::swap(e->stream, e->stream2);
     try {
         e->run(*q);
     } catch (...) {
+        if (other) std::swap(e->stream, e->stream2);
         e->pipelined_req = false;
         throw;
+    }
+    if (other) std::swap(e->stream, e->stream2);
+    if (e->queued) {
+        HIP_CHECK(hipEventRecord(e->pipe_end[si], other ? e->stream2 : e->stream));
+        if (!q->done_ev) HIP_CHECK(hipEventCreateWithFlags(&q->done_ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(q->done_ev, other ? e->stream2 : e->stream));
+        q->pending = true;
+        e->pipe_q[si] = q;
+        if (other) {
+            if (!e->pipe_ev) HIP_CHECK(hipEventCreateWithFlags(&e->pipe_ev, hipEventDisableTiming));
+            HIP_CHECK(hipEventRecord(e->pipe_ev, e->stream2));
+            e->pipe_pending = true;
+        }
+    } else {
+        e->pipe_q[si] = nullptr;  // (it ran to completion on its stream)
+        q->pending = false;
     }
     e->pipelined_req = false;
     if (queued) *queued = e->queued ? 1 : 0;
@@ -6785,6 +6856,7 @@ int ketogpu_engine_wait(ketogpu_engine *e) {
     if (!e) throw Error(KETOGPU_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_CHECK(hipSetDevice(e->device));
+    e->drain_pipe();
     HIP_CHECK(hipStreamSynchronize(e->stream));
     API_END
 }
@@ -6794,7 +6866,7 @@ int ketogpu_queries_download(ketogpu_engine *e, const ketogpu_queries *q, uint64
     API_BEGIN
     if (!e || !q) throw Error(KETOGPU_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
-    e->download(*q, allowed_bits, flagged_bits);
+    e->download(const_cast<ketogpu_queries &>(*q), allowed_bits, flagged_bits);
     API_END
 }
 

@@ -209,6 +209,10 @@ def test_label_pipelined_calls(n_req, monkeypatch):
     for _ in range(4):
         assert q2.run(pipelined=True)
     np.testing.assert_array_equal(q2.download(), want[::-1])  # (download waits)
+    for _ in range(3):  # each batch's download waits for that batch's call alone
+        assert q.run(pipelined=True) and q2.run(pipelined=True)
+        np.testing.assert_array_equal(q.download(), want)
+        np.testing.assert_array_equal(q2.download(), want[::-1])
     assert eng.last_stats()["plan"] == 7
     # second-stage requests possible: synchronous calls
     monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", "250")

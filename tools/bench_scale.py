@@ -176,14 +176,19 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     got_sync = q.download()
-    # pipelined: the same steps enqueued without a host wait per call (ketogpu_queries_run_async)
+    # pipelined: the same steps enqueued without a host wait per call (ketogpu_queries_run_async),
+    # two HBM copies of the batch alternating over two streams
+    q2 = eng.upload(roots, targets)
+    q2.run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    queued = sum(q.run(pipelined=True) for _ in range(a.steps))
+    queued = sum((q if k % 2 == 0 else q2).run(pipelined=True) for k in range(a.steps))
     eng.wait()
     torch.cuda.synchronize()
     dt_pipe = time.perf_counter() - t0
     assert np.array_equal(q.download(), got_sync)
+    assert np.array_equal(q2.download(), got_sync)
+    q2.close()
     eng.set_events(True)  # the first stage's own time: one more run with events between the kernels
     q.run()
     eng.set_events(False)
