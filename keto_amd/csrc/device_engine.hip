@@ -2593,6 +2593,57 @@ __device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[W]
             reinterpret_cast<uint4 *>(L)[(W / 4) * sub + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
 }
+// 64-word heads are two 128-byte lines, and a random read costs a whole line
+// (profiles/r06/probe): the second line is read only when the list does not fit the first
+// (count > 28 entries) — a dependent read, which the probe shows costs no time at this rate.
+// Lane `sub` holds words [8 sub, 8 sub + 8) of the first line in w[0..7] and of the second
+// in w[8..15]
+__device__ __forceinline__ void label_line_load(const uint32_t *line, uint32_t sub, uint32_t *w) {
+    const uint4 a = reinterpret_cast<const uint4 *>(line)[2 * sub], b = reinterpret_cast<const uint4 *>(line)[2 * sub + 1];
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y, w[6] = b.z, w[7] = b.w;
+}
+__device__ __forceinline__ void label_line_to_lds(uint32_t *L, const uint32_t *w, uint32_t sub) {
+    reinterpret_cast<uint4 *>(L)[2 * sub] = make_uint4(w[0], w[1], w[2], w[3]);
+    reinterpret_cast<uint4 *>(L)[2 * sub + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+// a head of H words into the lane's W = H / 4 registers: H < 64 whole (label_head_load
+// layout), H = 64 by lines (the second only when `count` of the first passes 28 entries;
+// KETO_LABEL_LINES=0: whole, A/B)
+#ifndef KETO_LABEL_LINES
+#define KETO_LABEL_LINES 1
+#endif
+template <int H>
+__device__ __forceinline__ void label_head_read(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4],
+                                                uint32_t &count) {
+#pragma unroll
+    for (int k = 0; k < H / 4; k++) w[k] = 0xFFFFFFFFu;
+    if constexpr (H < 64 || !KETO_LABEL_LINES) {
+        if (valid) label_head_load<H / 4>(head, sub, w);
+        count = label_word<H / 4, 0>(w);
+    } else {
+        if (valid) label_line_load(head, sub, w);
+        count = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[0], 0, 0xf, 0xf, false);  // word 0 from lane 0
+        if (valid && count != kNoLabel && count > 32 - kHeadFixed) label_line_load(head + 32, sub, w + 8);
+    }
+}
+// header word J (< 4) of a head read by label_head_read
+template <int H, int J>
+__device__ __forceinline__ uint32_t label_hword(const uint32_t (&w)[H / 4]) {
+    if constexpr (H < 64 || !KETO_LABEL_LINES)
+        return label_word<H / 4, J>(w);
+    else
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[J], 0, 0xf, 0xf, false);
+}
+template <int H>
+__device__ __forceinline__ void label_image(uint32_t *L, const uint32_t (&w)[H / 4], uint32_t sub) {
+    if constexpr (H < 64 || !KETO_LABEL_LINES) {
+        label_to_lds<H / 4>(L, w, sub);
+    } else {
+        label_line_to_lds(L, w, sub);
+        label_line_to_lds(L + 32, w + 8, sub);
+    }
+}
+
 // entries below x among the first E ascending entries at L (LDS; positions past the list
 // hold 0xFFFFFFFF or larger entries): a branchless binary search (E = head - 4, up to 60)
 template <int E>
@@ -2608,28 +2659,6 @@ template <int E>
 __device__ __forceinline__ bool label_find_e(const uint32_t *L, uint32_t x) {
     const uint32_t pos = label_lower_e<E>(L, x);
     return pos < (uint32_t)E && L[pos] == x;
-}
-
-// the lane's head words as comparands: the four header words and the padding become
-// 0xFFFFFFFE, which equals no entry (< 2^31) and no padding word
-template <int W>
-__device__ __forceinline__ void label_cmp_words(const uint32_t (&w)[W], uint32_t sub, uint32_t (&c)[W]) {
-#pragma unroll
-    for (int k = 0; k < W; k++) c[k] = (uint32_t)(W * sub + k) < kHeadFixed || w[k] == 0xFFFFFFFFu ? 0xFFFFFFFEu : w[k];
-}
-// does one of the first n entries at L (LDS, 16-byte aligned, readable up to a multiple of 4
-// past n: entries or padding that equal no comparand) equal one of the lane's comparands?
-// Every lane of the request reads the same entries (an LDS broadcast) and compares them with
-// its quarter of the other head, held in registers: no dependent LDS reads
-template <int W>
-__device__ __forceinline__ bool label_meet(const uint32_t *L, uint32_t n, const uint32_t (&c)[W]) {
-    bool hit = false;
-    for (uint32_t j = 0; j < n; j += 4) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(L + j);
-#pragma unroll
-        for (int k = 0; k < W; k++) hit |= c[k] == x.x || c[k] == x.y || c[k] == x.z || c[k] == x.w;
-    }
-    return hit;
 }
 
 // x among the first E ascending entries at L (LDS, 16-byte aligned) in two dependent LDS
@@ -2666,9 +2695,9 @@ __device__ __forceinline__ uint32_t label_lookup(const uint32_t *row, uint32_t x
 // KETO_LABEL_MEET: how the shorter inline landmark list meets the other head.  0 (default):
 // the shorter list's entries round-robin over the request's four lanes, each looked up in the
 // other list in LDS by label_block8 (two dependent LDS rounds); 2: the same by a binary search
-// (log2(E) dependent rounds: config #3's long lists pay for it); 1: every lane reads the
-// shorter list's entries and compares them with its quarter of the other head in registers
-// (measured 2.8x slower at 64-word heads, profiles/r06/ab).  Four lookups per lane in flight
+// (log2(E) dependent rounds: config #3's long lists pay for it).  Measured and dropped: every
+// lane reading the shorter list's entries and comparing them with its quarter of the other
+// head in registers (2.8x slower at 64-word heads, profiles/r06/ab).  Four lookups per lane in flight
 // at once instead of one at a time: no faster (config #3 shape), 10% slower (config #2); the
 // block splitters stored as a row of their own (two 16-byte reads instead of one word per
 // block): 8% slower on the config #3 shape, equal on config #2
@@ -2691,22 +2720,17 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
     const bool valid = some && r < kDynBase;
-    uint32_t sw[SW], pw[PW];
-#pragma unroll
-    for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < PW; k++) pw[k] = 0xFFFFFFFFu;
-    if (valid) {  // both heads in flight at once: one dependent HBM read per request
-        label_head_load<SW>(L.S + (uint64_t)t * HS, sub, sw);
-        label_head_load<PW>(L.P + (uint64_t)r * HP, sub, pw);
-    }
-    const uint32_t ns = label_word<SW, 0>(sw), np = label_word<PW, 0>(pw);
+    uint32_t sw[SW], pw[PW], ns, np;
+    // both heads in flight at once: one dependent HBM read per request (a 64-word head's
+    // second line, when its list needs it, one more)
+    label_head_read<HS>(L.S + (uint64_t)t * HS, valid, sub, sw, ns);
+    label_head_read<HP>(L.P + (uint64_t)r * HP, valid, sub, pw, np);
     const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
-    const uint64_t smask = (uint64_t)label_word<SW, 2>(sw) | (uint64_t)label_word<SW, 3>(sw) << 32;
-    const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw) | (uint64_t)label_word<PW, 3>(pw) << 32;
+    const uint64_t smask = (uint64_t)label_hword<HS, 2>(sw) | (uint64_t)label_hword<HS, 3>(sw) << 32;
+    const uint64_t pmask = (uint64_t)label_hword<HP, 2>(pw) | (uint64_t)label_hword<HP, 3>(pw) << 32;
     uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
-    label_to_lds<SW>(Sl, sw, sub);
-    label_to_lds<PW>(Pl, pw, sub);
+    label_image<HS>(Sl, sw, sub);
+    label_image<HP>(Pl, pw, sub);
     const uint32_t *Se = Sl + kHeadFixed, *Pe = Pl + kHeadFixed;  // the inline entries
     const uint32_t shard = (uint32_t)(unit % kRestShards);
     // a request without labels (or with a wildcard root): listed for the second stage
@@ -2724,21 +2748,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     //    four lanes, each entry searched in the other; the one-edge test (a non-interior root
     //    among S's inline raw entries) on the fourth lane
     if (labelled && !hit) {
-        if (KETO_LABEL_MEET == 1) {
-            if (es <= ep) {
-                uint32_t c[PW];
-                label_cmp_words<PW>(pw, sub, c);
-                hit = label_meet<PW>(Se, es, c);
-            } else {
-                uint32_t c[SW];
-                label_cmp_words<SW>(sw, sub, c);
-                hit = label_meet<SW>(Pe, ep, c);
-            }
-            if (r >= L.ni) {  // the one-edge test against the lane's S words
-#pragma unroll
-                for (int k = 0; k < SW; k++) hit |= (uint32_t)(SW * sub + k) >= kHeadFixed && sw[k] == r;
-            }
-        } else if (KETO_LABEL_MEET == 2) {
+        if (KETO_LABEL_MEET == 2) {
             if (es <= ep)
                 for (uint32_t k = sub; k < es && !hit; k += 4) hit = label_find_e<CP>(Pe, Se[k]);
             else
@@ -2760,7 +2770,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     //    interior, S whole inline, or r <= S's last inline entry
     {
         const uint64_t hb = __ballot(hit);
-        const uint32_t os = label_word<SW, 1>(sw), op = label_word<PW, 1>(pw);
+        const uint32_t os = label_hword<HS, 1>(sw), op = label_hword<HP, 1>(pw);
         bool full = false;
         if (sub == 0 && labelled && !((hb >> lane) & 0xF)) {
             const uint32_t s_end = Se[CS - 1];  // (ns > CS: the last inline entry)
