@@ -2700,7 +2700,9 @@ __device__ __forceinline__ uint32_t label_lookup(const uint32_t *row, uint32_t x
 // head in registers (2.8x slower at 64-word heads, profiles/r06/ab).  Four lookups per lane in flight
 // at once instead of one at a time: no faster (config #3 shape), 10% slower (config #2); the
 // block splitters stored as a row of their own (two 16-byte reads instead of one word per
-// block): 8% slower on the config #3 shape, equal on config #2
+// block): 8% slower on the config #3 shape, equal on config #2; padded rows instead of the
+// per-entry bounds test in label_block8 (fewer VALU instructions): 5-8% slower
+// (profiles/r06/ab/ab_*_pad.jsonl)
 #ifndef KETO_LABEL_MEET
 #define KETO_LABEL_MEET 0
 #endif
