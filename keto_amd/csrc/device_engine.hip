@@ -2607,26 +2607,30 @@ __device__ __forceinline__ void label_line_to_lds(uint32_t *L, const uint32_t *w
     reinterpret_cast<uint4 *>(L)[2 * sub + 1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 // a head of H words into the lane's W = H / 4 registers: H < 64 whole (label_head_load
-// layout), H = 64 by lines (the second only when `count` of the first passes 28 entries;
-// KETO_LABEL_LINES=0: whole, A/B)
+// layout), H = 64 by lines (label_head_first, then label_head_second only when the count of
+// the first passes 28 entries; KETO_LABEL_LINES=0: whole, A/B)
 #ifndef KETO_LABEL_LINES
 #define KETO_LABEL_LINES 1
 #endif
 template <int H>
-__device__ __forceinline__ void label_head_read(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4],
-                                                uint32_t &count) {
+__device__ __forceinline__ void label_head_first(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4]) {
 #pragma unroll
     for (int k = 0; k < H / 4; k++) w[k] = 0xFFFFFFFFu;
     if constexpr (H < 64 || !KETO_LABEL_LINES) {
         if (valid) label_head_load<H / 4>(head, sub, w);
-        count = label_word<H / 4, 0>(w);
     } else {
         if (valid) label_line_load(head, sub, w);
-        count = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[0], 0, 0xf, 0xf, false);  // word 0 from lane 0
+    }
+}
+// the second line of a 64-word head whose list passes the first (count: the head's word 0)
+template <int H>
+__device__ __forceinline__ void label_head_second(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4],
+                                                  uint32_t count) {
+    if constexpr (H == 64 && KETO_LABEL_LINES) {
         if (valid && count != kNoLabel && count > 32 - kHeadFixed) label_line_load(head + 32, sub, w + 8);
     }
 }
-// header word J (< 4) of a head read by label_head_read
+// header word J (< 4) of a head read by label_head_first
 template <int H, int J>
 __device__ __forceinline__ uint32_t label_hword(const uint32_t (&w)[H / 4]) {
     if constexpr (H < 64 || !KETO_LABEL_LINES)
@@ -2722,11 +2726,15 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     const uint32_t r = (uint32_t)__shfl((int)r_lane, (int)q, 64), t = (uint32_t)__shfl((int)t_lane, (int)q, 64);
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
     const bool valid = some && r < kDynBase;
-    uint32_t sw[SW], pw[PW], ns, np;
+    uint32_t sw[SW], pw[PW];
     // both heads in flight at once: one dependent HBM read per request (a 64-word head's
-    // second line, when its list needs it, one more)
-    label_head_read<HS>(L.S + (uint64_t)t * HS, valid, sub, sw, ns);
-    label_head_read<HP>(L.P + (uint64_t)r * HP, valid, sub, pw, np);
+    // second line, when its list needs it, one more — both heads' second lines at once)
+    const uint32_t *shead = L.S + (uint64_t)t * HS, *phead = L.P + (uint64_t)r * HP;
+    label_head_first<HS>(shead, valid, sub, sw);
+    label_head_first<HP>(phead, valid, sub, pw);
+    const uint32_t ns = label_hword<HS, 0>(sw), np = label_hword<HP, 0>(pw);
+    label_head_second<HS>(shead, valid, sub, sw, ns);
+    label_head_second<HP>(phead, valid, sub, pw, np);
     const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
     const uint64_t smask = (uint64_t)label_hword<HS, 2>(sw) | (uint64_t)label_hword<HS, 3>(sw) << 32;
     const uint64_t pmask = (uint64_t)label_hword<HP, 2>(pw) | (uint64_t)label_hword<HP, 3>(pw) << 32;
