@@ -52,7 +52,7 @@ def parse():
     p.add_argument("--parity", choices=["full", "sample"], default="full",
                    help="full: every request of the timed batch is diffed against the oracle (about 90 s of "
                         "16-thread CPU work at config #2); sample: only the baseline sample")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) for roofline.traffic")
     p.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated",
                    help="replicated: graph on every GPU, request batches sharded (the metric's line); "
