@@ -2593,61 +2593,6 @@ __device__ __forceinline__ void label_to_lds(uint32_t *L, const uint32_t (&w)[W]
             reinterpret_cast<uint4 *>(L)[(W / 4) * sub + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
 }
-// 64-word heads are two 128-byte lines, and a random read costs a whole line
-// (profiles/r06/probe): the second line is read only when the list does not fit the first
-// (count > 28 entries) — a dependent read, which the probe shows costs no time at this rate.
-// Lane `sub` holds words [8 sub, 8 sub + 8) of the first line in w[0..7] and of the second
-// in w[8..15]
-__device__ __forceinline__ void label_line_load(const uint32_t *line, uint32_t sub, uint32_t *w) {
-    const uint4 a = reinterpret_cast<const uint4 *>(line)[2 * sub], b = reinterpret_cast<const uint4 *>(line)[2 * sub + 1];
-    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y, w[6] = b.z, w[7] = b.w;
-}
-__device__ __forceinline__ void label_line_to_lds(uint32_t *L, const uint32_t *w, uint32_t sub) {
-    reinterpret_cast<uint4 *>(L)[2 * sub] = make_uint4(w[0], w[1], w[2], w[3]);
-    reinterpret_cast<uint4 *>(L)[2 * sub + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-// a head of H words into the lane's W = H / 4 registers: H < 64 whole (label_head_load
-// layout), H = 64 by lines (label_head_first, then label_head_second only when the count of
-// the first passes 28 entries; KETO_LABEL_LINES=0: whole, A/B)
-#ifndef KETO_LABEL_LINES
-#define KETO_LABEL_LINES 1
-#endif
-template <int H>
-__device__ __forceinline__ void label_head_first(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4]) {
-#pragma unroll
-    for (int k = 0; k < H / 4; k++) w[k] = 0xFFFFFFFFu;
-    if constexpr (H < 64 || !KETO_LABEL_LINES) {
-        if (valid) label_head_load<H / 4>(head, sub, w);
-    } else {
-        if (valid) label_line_load(head, sub, w);
-    }
-}
-// the second line of a 64-word head whose list passes the first (count: the head's word 0)
-template <int H>
-__device__ __forceinline__ void label_head_second(const uint32_t *head, bool valid, uint32_t sub, uint32_t (&w)[H / 4],
-                                                  uint32_t count) {
-    if constexpr (H == 64 && KETO_LABEL_LINES) {
-        if (valid && count != kNoLabel && count > 32 - kHeadFixed) label_line_load(head + 32, sub, w + 8);
-    }
-}
-// header word J (< 4) of a head read by label_head_first
-template <int H, int J>
-__device__ __forceinline__ uint32_t label_hword(const uint32_t (&w)[H / 4]) {
-    if constexpr (H < 64 || !KETO_LABEL_LINES)
-        return label_word<H / 4, J>(w);
-    else
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[J], 0, 0xf, 0xf, false);
-}
-template <int H>
-__device__ __forceinline__ void label_image(uint32_t *L, const uint32_t (&w)[H / 4], uint32_t sub) {
-    if constexpr (H < 64 || !KETO_LABEL_LINES) {
-        label_to_lds<H / 4>(L, w, sub);
-    } else {
-        label_line_to_lds(L, w, sub);
-        label_line_to_lds(L + 32, w + 8, sub);
-    }
-}
-
 // entries below x among the first E ascending entries at L (LDS; positions past the list
 // hold 0xFFFFFFFF or larger entries): a branchless binary search (E = head - 4, up to 60)
 template <int E>
@@ -2706,7 +2651,9 @@ __device__ __forceinline__ uint32_t label_lookup(const uint32_t *row, uint32_t x
 // block splitters stored as a row of their own (two 16-byte reads instead of one word per
 // block): 8% slower on the config #3 shape, equal on config #2; padded rows instead of the
 // per-entry bounds test in label_block8 (fewer VALU instructions): 5-8% slower
-// (profiles/r06/ab/ab_*_pad.jsonl)
+// (profiles/r06/ab/ab_*_pad.jsonl); a 64-word head's second line read only when its list
+// needs it (both heads' first lines together, then the second lines): equal traffic to the
+// kernel's bound, 5% slower (ab_f_lines2 / ab_f_whole2)
 #ifndef KETO_LABEL_MEET
 #define KETO_LABEL_MEET 0
 #endif
@@ -2727,20 +2674,21 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     const bool some = r != KETOGPU_NODE_NONE && t != KETOGPU_NODE_NONE;
     const bool valid = some && r < kDynBase;
     uint32_t sw[SW], pw[PW];
-    // both heads in flight at once: one dependent HBM read per request (a 64-word head's
-    // second line, when its list needs it, one more — both heads' second lines at once)
-    const uint32_t *shead = L.S + (uint64_t)t * HS, *phead = L.P + (uint64_t)r * HP;
-    label_head_first<HS>(shead, valid, sub, sw);
-    label_head_first<HP>(phead, valid, sub, pw);
-    const uint32_t ns = label_hword<HS, 0>(sw), np = label_hword<HP, 0>(pw);
-    label_head_second<HS>(shead, valid, sub, sw, ns);
-    label_head_second<HP>(phead, valid, sub, pw, np);
+#pragma unroll
+    for (int k = 0; k < SW; k++) sw[k] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < PW; k++) pw[k] = 0xFFFFFFFFu;
+    if (valid) {  // both heads in flight at once: one dependent HBM read per request
+        label_head_load<SW>(L.S + (uint64_t)t * HS, sub, sw);
+        label_head_load<PW>(L.P + (uint64_t)r * HP, sub, pw);
+    }
+    const uint32_t ns = label_word<SW, 0>(sw), np = label_word<PW, 0>(pw);
     const bool labelled = valid && ns != kNoLabel && np != kNoLabel;
-    const uint64_t smask = (uint64_t)label_hword<HS, 2>(sw) | (uint64_t)label_hword<HS, 3>(sw) << 32;
-    const uint64_t pmask = (uint64_t)label_hword<HP, 2>(pw) | (uint64_t)label_hword<HP, 3>(pw) << 32;
+    const uint64_t smask = (uint64_t)label_word<SW, 2>(sw) | (uint64_t)label_word<SW, 3>(sw) << 32;
+    const uint64_t pmask = (uint64_t)label_word<PW, 2>(pw) | (uint64_t)label_word<PW, 3>(pw) << 32;
     uint32_t *Sl = sh.S + q * (HS + 4), *Pl = sh.P + q * (HP + 4);
-    label_image<HS>(Sl, sw, sub);
-    label_image<HP>(Pl, pw, sub);
+    label_to_lds<SW>(Sl, sw, sub);
+    label_to_lds<PW>(Pl, pw, sub);
     const uint32_t *Se = Sl + kHeadFixed, *Pe = Pl + kHeadFixed;  // the inline entries
     const uint32_t shard = (uint32_t)(unit % kRestShards);
     // a request without labels (or with a wildcard root): listed for the second stage
@@ -2780,7 +2728,7 @@ __device__ __forceinline__ void label_unit(LabelShared<HS, HP> &sh, const LabelG
     //    interior, S whole inline, or r <= S's last inline entry
     {
         const uint64_t hb = __ballot(hit);
-        const uint32_t os = label_hword<HS, 1>(sw), op = label_hword<HP, 1>(pw);
+        const uint32_t os = label_word<SW, 1>(sw), op = label_word<PW, 1>(pw);
         bool full = false;
         if (sub == 0 && labelled && !((hb >> lane) & 0xF)) {
             const uint32_t s_end = Se[CS - 1];  // (ns > CS: the last inline entry)
