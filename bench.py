@@ -374,6 +374,7 @@ def main():
             roof["host_to_host"] = host_roof
         roof["kernels"] = {k: {"GBps": round(gbps[k], 1), "ms": round(ms, 4), "bytes": bb, "launches": nl}
                            for k, (bb, ms, nl) in fam.items() if ms > 0}
+        roof["line_ceiling"] = line_ceiling(local, e0 - b0, roof["ms_per_launch"])
         achieved = roof["achieved"]
         stream = stream_copy_gbps(local)
         roof["stream_copy_GBps"] = round(stream, 1)  # measured device-copy bandwidth
@@ -798,6 +799,26 @@ def pcie_h2d_gbps(device, nbytes=64 << 20, iters=10):
     ms = e0.elapsed_time(e1)
     del h, d
     return nbytes * iters / (ms * 1e-3) / 1e9
+
+
+def line_ceiling(device, n, kernel_ms):
+    """plan label's first stage against what its reads alone cost on this device: two random
+    128-byte lines + 8 B of request per check (ketogpu_probe_random_lines, keto_amd/csrc/
+    probe.hip), measured live over a 2 GiB table — the bound the HBM-byte fraction above
+    cannot see (a random line costs 128 B of fetch for a 64-byte head as for a 128-byte one,
+    DESIGN.md Kernels 0a)"""
+    import ctypes as C
+    from keto_amd import _lib as L
+    ms = C.c_double(0)
+    rc = L.lib().ketogpu_probe_random_lines(device, 2 << 30, n, 20, C.byref(ms))
+    if rc or ms.value <= 0:
+        return None
+    return {"bound": "random 128-byte lines (two per check)", "probe_ms_per_launch": round(ms.value, 4),
+            "kernel_ms_per_launch": kernel_ms, "frac": round(ms.value / kernel_ms, 4) if kernel_ms else None,
+            "peak_lines_per_s": round(2 * n / (ms.value * 1e-3), 1),
+            "achieved_lines_per_s": round(2 * n / (kernel_ms * 1e-3), 1) if kernel_ms else None,
+            "measured": "ketogpu_probe_random_lines: the same request count, 16 requests per wave, both lines in "
+                        "flight, 2 GiB table, hipEvents over 20 launches"}
 
 
 def cpu_baseline(w, gpu_allowed, seconds, full=True, offset=0):

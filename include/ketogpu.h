@@ -897,6 +897,12 @@ int ketogpu_abi_version(void);
 void ketogpu_free(void *p);
 /* number of visible HIP devices (0 without a GPU) */
 int ketogpu_device_count(void);
+/* diagnostics (no Keto counterpart): the random-line ceiling of plan label's first stage —
+ * `requests` requests of 16 per wave each reading two random 128-byte lines of a
+ * `table_bytes` table plus 8 bytes of request, the reads a check of plan label makes and
+ * nothing else; *ms_per_launch averaged over `reps` launches on `device` (keto_amd/csrc/
+ * probe.hip; bench.py's roofline.line_ceiling) */
+int ketogpu_probe_random_lines(int device, uint64_t table_bytes, uint64_t requests, int reps, double *ms_per_launch);
 
 #ifdef __cplusplus
 }

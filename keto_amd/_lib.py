@@ -338,6 +338,7 @@ SIGNATURES = {
     "ketogpu_queries_run": (C.c_int, [vp, vp]),
     "ketogpu_queries_run_async": (C.c_int, [vp, vp, C.POINTER(C.c_int)]),
     "ketogpu_engine_wait": (C.c_int, [vp]),
+    "ketogpu_probe_random_lines": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double)]),
     "ketogpu_queries_download": (C.c_int, [vp, vp, vp, vp]),
     "ketogpu_queries_free": (None, [vp]),
     "ketogpu_engine_last_stats": (C.c_int, [vp, C.POINTER(RunStats)]),

@@ -14,7 +14,7 @@ SYNTH_LIB = os.path.join(HERE, "libketosynth.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KETOGPU_ARCH", "gfx950")
 
-SOURCES = ["snapshot.cpp", "snapshot_write.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip", "comm.cpp", "part_round.cpp", "tier.cpp", "core_index.cpp", "labels.cpp"]
+SOURCES = ["snapshot.cpp", "snapshot_write.cpp", "snapshot_io.cpp", "host_engine.cpp", "multi_engine.cpp", "shard.cpp", "device_engine.hip", "partition.hip", "comm.cpp", "part_round.cpp", "tier.cpp", "core_index.cpp", "labels.cpp", "probe.hip"]
 HEADERS = ["ketogpu_internal.hpp", "device_util.hpp", "part_round.hpp", "tier.hpp", "core_index.hpp", "labels.hpp", os.path.join("..", "..", "include", "ketogpu.h")]
 
 
