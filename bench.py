@@ -7,7 +7,7 @@ times over); the global batch of N x 1M requests is split into contiguous 64-req
 ranges, one per GPU: no data-path collective, weak scaling.  A step = one batch call over
 a GPU's range with its requests already resident in HBM, enqueued without a host wait per
 call (ketogpu_queries_run_async: traversal, result bits left in HBM; batches pipelined as a
-server pipelines them, two HBM copies of the batch alternating over two streams) — `value`,
+server pipelines them, four HBM copies of the batch rotating over four streams) — `value`,
 K steps bracketed by a barrier and a device synchronization on both sides, the max over
 ranks.  Beside it: the same steps with one host wait per call (ketogpu_queries_run,
 `resident_call_checks_per_s`: round 5's value) and the host-to-host rate (requests H2D from
@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "permission checks/sec (batched, whole node) + traversal HBM GB/s vs roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PIPE_COPIES = 4  # HBM copies of a GPU's batch rotating in the pipelined (value) leg
 
 
 def parse():
@@ -254,18 +255,20 @@ def main():
     # pipelined: the same K steps enqueued without a host wait per call
     # (ketogpu_queries_run_async: the engine proves no request can need the second stage),
     # one wait per GPU at the end, barrier + device sync on both sides — batch k+1 enqueued
-    # while batch k runs, as a server pipelines its batches.  Two HBM copies of the GPU's
-    # batch alternate (a server's consecutive batches have their own result words): calls
-    # alternate between two streams, so a call's dense pass overlaps the next call's first
-    # stage
-    qs2 = [e_.upload(roots[b_:e_r], targets[b_:e_r]) for e_, (b_, e_r) in zip(engs, rng)]
-    for qq in qs2:
-        qq.run()
+    # while batch k runs, as a server pipelines its batches.  PIPE_COPIES HBM copies of the
+    # GPU's batch rotate (a server's consecutive batches have their own result words): calls
+    # rotate over the engine's four streams, so a call's dense pass overlaps later calls'
+    # first stages
+    copies = [[qq] + [e_.upload(roots[b_:e_r], targets[b_:e_r]) for _ in range(PIPE_COPIES - 1)]
+              for qq, e_, (b_, e_r) in zip(qs, engs, rng)]
+    for cs in copies:
+        for qq in cs[1:]:
+            qq.run()
 
-    def pipelined(qq, qq2, e_):
+    def pipelined(cs, e_):
         nq = 0
         for k in range(a.steps):
-            nq += (qq if k % 2 == 0 else qq2).run(pipelined=True)
+            nq += cs[k % len(cs)].run(pipelined=True)
         e_.wait()
         return nq
     queued = [0] * len(qs)
@@ -273,12 +276,12 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     if len(qs) == 1:
-        queued[0] = pipelined(qs[0], qs2[0], engs[0])
+        queued[0] = pipelined(copies[0], engs[0])
     else:
         import threading
 
         def _p(i):
-            queued[i] = pipelined(qs[i], qs2[i], engs[i])
+            queued[i] = pipelined(copies[i], engs[i])
         ths = [threading.Thread(target=_p, args=(i,)) for i in range(len(qs))]
         for th in ths:
             th.start()
@@ -289,10 +292,11 @@ def main():
     dt_pipe = max_over_ranks(time.perf_counter() - t0, world)
     pipe_value = len(roots_all) * a.steps / dt_pipe
     log(f"{a.steps} pipelined HBM-resident steps in {dt_pipe:.4f}s ({sum(queued)} calls queued without a wait)")
-    for qq, qq2, (b_, e_r) in zip(qs, qs2, rng):
-        assert np.array_equal(qq.download(), allowed[b_:e_r])
-        assert np.array_equal(qq2.download(), allowed[b_:e_r])
-        qq2.close()
+    for cs, (b_, e_r) in zip(copies, rng):
+        for qq in cs:
+            assert np.array_equal(qq.download(), allowed[b_:e_r])
+        for qq in cs[1:]:
+            qq.close()
     b0, e0 = rng[0]
     q = qs[0]
     # the kernels' own times: the same runs again with a timing event between the call's
@@ -404,10 +408,11 @@ def main():
                                                                  else " (one process per GPU)" if world > 1 else ""))},
             "timing": ("value: requests resident in HBM, PCIe legs excluded: per step one batch call per GPU over "
                        "its range, enqueued without a host wait per call (ketogpu_queries_run_async: validation at "
-                       "upload, traversal, result bits left in HBM; two HBM copies of the batch alternate, calls "
-                       "alternate between two streams), one wait per GPU after the K steps, barrier + device sync "
+                       f"upload, traversal, result bits left in HBM; {PIPE_COPIES} HBM copies of the batch rotate, "
+                       "calls rotate over the engine's four streams), one wait per GPU after the K steps, barrier + "
+                       "device sync "
                        f"on both sides, max over ranks; {sum(queued)} of {a.steps * len(qs)} calls queued without a "
-                       "wait; both copies' bits checked after; snapshot build and upload excluded.  SURVEY 8(d)'s "
+                       "wait; every copy's bits checked after; snapshot build and upload excluded.  SURVEY 8(d)'s "
                        "number is host_to_host_checks_per_s"),
             "resident_call_checks_per_s": round(value, 1),
             "resident_call_ms_per_step": round(dt_res / a.steps * 1e3, 4),

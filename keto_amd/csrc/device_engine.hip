@@ -4492,22 +4492,24 @@ struct ketogpu_engine {
     // them: every request but wildcard roots is one intersection)
     bool use_label = false;
     LabelGraph lgraph{};
-    // rest and full lists: four sets each of kRestShards counters, one cache line each; call k
-    // uses set k % 4 and clears set (k + 2) % 4 for call k + 2 — the next call on the same
-    // stream when pipelined calls alternate between two streams (ketogpu_queries_run_async),
-    // so a call's dense pass may still read its counters while the next call's first stage runs
-    static constexpr unsigned kLabelSets = 4;
+    // rest and full lists: kLabelSets sets each of kRestShards counters, one cache line each;
+    // call k uses set k mod kLabelSets and clears set (k + kPipe) mod kLabelSets for call
+    // k + kPipe — the next call on the same stream when pipelined calls rotate over kPipe
+    // streams (ketogpu_queries_run_async), so a call's dense pass may still read its counters
+    // while later calls' first stages run
+    static constexpr unsigned kPipe = 4;  // streams pipelined calls rotate over (ketogpu_queries_run_async)
+    static constexpr unsigned kLabelSets = 2 * kPipe;
     unsigned int *rest_counts = nullptr;
     uint64_t label_calls = 0;  // selects the set
     LabelRest label_rest(uint64_t n) {    // this call's rest list over requests [0, n)
         const uint64_t units = (n + 15) / 16;
-        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + 2) % kLabelSets);
+        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + kPipe) % kLabelSets);
         return LabelRest{spill_units, rest_counts + set * kRestShards * kRestStride,
                          rest_counts + next * kRestShards * kRestStride, 16 * ((units + kRestShards - 1) / kRestShards)};
     }
     LabelRest label_full(uint64_t n) {  // this call's list for label_full_kernel (records)
         const uint64_t units = (n + 15) / 16;
-        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + 2) % kLabelSets);
+        const unsigned set = (unsigned)(label_calls % kLabelSets), next = (unsigned)((label_calls + kPipe) % kLabelSets);
         return LabelRest{nullptr, rest_counts + (kLabelSets + set) * kRestShards * kRestStride,
                          rest_counts + (kLabelSets + next) * kRestShards * kRestStride,
                          16 * ((units + kRestShards - 1) / kRestShards), full_rec + (uint64_t)set * 2 * spill_cap};
@@ -4527,21 +4529,27 @@ struct ketogpu_engine {
     // ketogpu_queries_run_async: this call may return before the device finishes (set per
     // call); `queued`: the last call did
     bool pipelined_req = false, queued = false;
-    // pipelined calls alternate between `stream` and `stream2` (by label_calls' parity), so
-    // a call's dense pass overlaps the next call's first stage; pipe_ev: recorded after the
-    // last queued call on stream2, waited for (on `stream`, by the device) before any other
-    // work of the engine (drain_pipe)
-    hipEvent_t pipe_ev = nullptr;
-    bool pipe_pending = false;
-    // the batch each stream's last queued call ran over, and that call's end: two calls over
-    // the SAME batch never overlap (they write one result array), the second waits for the first
-    const ketogpu_queries *pipe_q[2] = {nullptr, nullptr};
-    hipEvent_t pipe_end[2] = {nullptr, nullptr};
+    // pipelined calls rotate over kPipe streams (by label_calls: pipe_s[0] is `stream`, the
+    // others created at the first pipelined call), so one call's dense pass overlaps later
+    // calls' first stages; any other work of the engine first waits for them (drain_pipe: a
+    // host wait, paid only when non-pipelined work follows pipelined calls)
+    hipStream_t pipe_s[kPipe] = {};
+    bool pipe_used[kPipe] = {};
+    // the batch each stream's last queued call ran over (compared, never dereferenced): calls
+    // over the SAME batch never overlap (they write one result array), a call waits for the
+    // batch's previous one (its done_ev)
+    const ketogpu_queries *pipe_q[kPipe] = {};
     void drain_pipe() {
-        pipe_q[0] = pipe_q[1] = nullptr;
-        if (!pipe_pending) return;
-        HIP_CHECK(hipStreamWaitEvent(stream, pipe_ev, 0));
-        pipe_pending = false;
+        for (unsigned k = 0; k < kPipe; k++) {
+            pipe_q[k] = nullptr;
+            if (k && pipe_used[k]) HIP_CHECK(hipStreamSynchronize(pipe_s[k]));
+            pipe_used[k] = false;
+        }
+    }
+    bool pipe_busy() const {
+        for (unsigned k = 1; k < kPipe; k++)
+            if (pipe_used[k]) return true;
+        return false;
     }
     // heads marked kNoLabel by the build (the test knob) and the knob itself: with none, and
     // no head marked by a write (lab_invalid), no request of a batch without wildcard roots
@@ -4859,7 +4867,11 @@ struct ketogpu_engine {
     }
     uint64_t sync() {
         const Snapshot &s = *snap;
-        drain_pipe();  // (every entry point syncs first: its work orders after queued calls)
+        // every entry point syncs first, and its work orders after the queued calls — except a
+        // pipelined call with nothing to apply (its own stream and counter set order it)
+        if (!pipelined_req || (bg && bg->done.load(std::memory_order_acquire)) ||
+            (s.writable && synced_version != s.version))
+            drain_pipe();
         if (bg && bg->done.load(std::memory_order_acquire)) finish_relabel();  // (its rows are the synced ones)
         if (!s.writable || synced_version == s.version) return 0;
         HIP_CHECK(hipSetDevice(device));
@@ -5126,9 +5138,11 @@ struct ketogpu_engine {
             if (x) (void)hipStreamSynchronize(x);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (wait_ev) (void)hipEventDestroy(wait_ev);
-        if (pipe_ev) (void)hipEventDestroy(pipe_ev);
-        for (hipEvent_t x : pipe_end)
-            if (x) (void)hipEventDestroy(x);
+        for (unsigned k = 1; k < kPipe; k++)
+            if (pipe_s[k]) {
+                (void)hipStreamSynchronize(pipe_s[k]);
+                (void)hipStreamDestroy(pipe_s[k]);
+            }
         for (void *p : owned) (void)hipFree(p);
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags, (void *)full_rec})
@@ -5833,7 +5847,7 @@ struct ketogpu_engine {
     void ensure_spill(uint64_t n) {
         if (n <= spill_cap) return;
         // (a queued call on either stream may still read the lists: let them finish first)
-        if (pipe_q[0] || pipe_q[1] || pipe_pending) HIP_CHECK(hipDeviceSynchronize());
+        if (pipe_busy() || pipe_q[0]) HIP_CHECK(hipDeviceSynchronize());
         for (void *p : {(void *)spill_units, (void *)spill_roots, (void *)spill_targets, (void *)spill_allowed,
                         (void *)spill_flags})
             if (p) (void)hipFree(p);
@@ -6778,38 +6792,38 @@ int ketogpu_queries_run_async(ketogpu_engine *e, ketogpu_queries *q, int *queued
     if (!e || !q) throw Error(KETOGPU_EINVAL, "null argument");
     std::shared_lock<std::shared_mutex> rd(e->snap->mu);
     std::lock_guard<std::mutex> lk(e->mu);
-    e->sync();
     e->pipelined_req = true;
     e->queued = false;
-    // odd calls on the second stream: this call's first stage may run beside the previous
-    // call's dense pass (their counter sets and record regions differ, ketogpu_engine
-    // label_rest / label_full)
-    const bool other = (e->label_calls & 1) != 0 && e->use_label && e->stream2;
-    const int si = other ? 1 : 0;
-    for (int k = 0; k < 2; k++)
-        if (!e->pipe_end[k]) HIP_CHECK(hipEventCreateWithFlags(&e->pipe_end[k], hipEventDisableTiming));
-    if (e->pipe_q[si ^ 1] == q)  // the same batch queued on the other stream: after it
-        HIP_CHECK(hipStreamWaitEvent(other ? e->stream2 : e->stream, e->pipe_end[si ^ 1], 0));
-    if (other) std::swap(e->stream, e->stream2);
     try {
-        e->run(*q);
+        e->sync();
     } catch (...) {
-        if (other) std::swap(e->stream, e->stream2);
         e->pipelined_req = false;
         throw;
     }
-    if (other) std::swap(e->stream, e->stream2);
+    // calls rotate over kPipe streams: this call's first stage may run beside earlier calls'
+    // dense passes (their counter sets and record regions differ, ketogpu_engine label_rest /
+    // label_full)
+    const unsigned si = e->use_label ? (unsigned)(e->label_calls % ketogpu_engine::kPipe) : 0u;
+    if (si && !e->pipe_s[si]) HIP_CHECK(hipStreamCreateWithFlags(&e->pipe_s[si], hipStreamNonBlocking));
+    hipStream_t sq = si ? e->pipe_s[si] : e->stream;
+    bool elsewhere = false;  // the same batch queued on another stream: after it
+    for (unsigned k = 0; k < ketogpu_engine::kPipe; k++) elsewhere |= k != si && e->pipe_q[k] == q;
+    if (elsewhere && q->pending) HIP_CHECK(hipStreamWaitEvent(sq, q->done_ev, 0));
+    if (si) std::swap(e->stream, e->pipe_s[si]);
+    try {
+        e->run(*q);
+    } catch (...) {
+        if (si) std::swap(e->stream, e->pipe_s[si]);
+        e->pipelined_req = false;
+        throw;
+    }
+    if (si) std::swap(e->stream, e->pipe_s[si]);
     if (e->queued) {
-        HIP_CHECK(hipEventRecord(e->pipe_end[si], other ? e->stream2 : e->stream));
         if (!q->done_ev) HIP_CHECK(hipEventCreateWithFlags(&q->done_ev, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(q->done_ev, other ? e->stream2 : e->stream));
+        HIP_CHECK(hipEventRecord(q->done_ev, sq));
         q->pending = true;
         e->pipe_q[si] = q;
-        if (other) {
-            if (!e->pipe_ev) HIP_CHECK(hipEventCreateWithFlags(&e->pipe_ev, hipEventDisableTiming));
-            HIP_CHECK(hipEventRecord(e->pipe_ev, e->stream2));
-            e->pipe_pending = true;
-        }
+        e->pipe_used[si] = true;
     } else {
         e->pipe_q[si] = nullptr;  // (it ran to completion on its stream)
         q->pending = false;

@@ -213,6 +213,13 @@ def test_label_pipelined_calls(n_req, monkeypatch):
         assert q.run(pipelined=True) and q2.run(pipelined=True)
         np.testing.assert_array_equal(q.download(), want)
         np.testing.assert_array_equal(q2.download(), want[::-1])
+    # four batches rotating over the engine's four streams, twice around
+    qs = [q, q2, eng.upload(roots, targets), eng.upload(roots[::-1].copy(), targets[::-1].copy())]
+    wants = [want, want[::-1], want, want[::-1]]
+    for k in range(8):
+        assert qs[k % 4].run(pipelined=True)
+    for qq, w in zip(qs, wants):
+        np.testing.assert_array_equal(qq.download(), w)
     assert eng.last_stats()["plan"] == 7
     # second-stage requests possible: synchronous calls
     monkeypatch.setenv("KETOGPU_LABEL_REST_PERMILLE", "250")

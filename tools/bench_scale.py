@@ -177,18 +177,20 @@ def main():
     dt = time.perf_counter() - t0
     got_sync = q.download()
     # pipelined: the same steps enqueued without a host wait per call (ketogpu_queries_run_async),
-    # two HBM copies of the batch alternating over two streams
-    q2 = eng.upload(roots, targets)
-    q2.run()
+    # four HBM copies of the batch rotating over the engine's four streams
+    cs = [q] + [eng.upload(roots, targets) for _ in range(3)]
+    for qq in cs[1:]:
+        qq.run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    queued = sum((q if k % 2 == 0 else q2).run(pipelined=True) for k in range(a.steps))
+    queued = sum(cs[k % 4].run(pipelined=True) for k in range(a.steps))
     eng.wait()
     torch.cuda.synchronize()
     dt_pipe = time.perf_counter() - t0
-    assert np.array_equal(q.download(), got_sync)
-    assert np.array_equal(q2.download(), got_sync)
-    q2.close()
+    for qq in cs:
+        assert np.array_equal(qq.download(), got_sync)
+    for qq in cs[1:]:
+        qq.close()
     eng.set_events(True)  # the first stage's own time: one more run with events between the kernels
     q.run()
     eng.set_events(False)

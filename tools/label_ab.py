@@ -68,16 +68,18 @@ def main():
             ms.append(eng.last_stats()["main_ms"])
         dt_res = (time.perf_counter() - t0) / a.steps
         st = eng.last_stats()
-        q2 = eng.upload(roots, targets)  # pipelined: no host wait per call (ketogpu_queries_run_async),
-        q2.run()                          # two copies of the batch alternating over two streams
+        cs = [q] + [eng.upload(roots, targets) for _ in range(3)]  # pipelined: no host wait per call
+        for qq in cs[1:]:                                         # (ketogpu_queries_run_async), four
+            qq.run()                                              # copies of the batch over four streams
         t0 = time.perf_counter()
         for k in range(a.steps):
-            (q if k % 2 == 0 else q2).run(pipelined=True)
+            cs[k % 4].run(pipelined=True)
         eng.wait()
         dt_pipe = (time.perf_counter() - t0) / a.steps
-        assert np.array_equal(q.download(), ref if ref is not None else got)
-        assert np.array_equal(q2.download(), ref if ref is not None else got)
-        q2.close()
+        for qq in cs:
+            assert np.array_equal(qq.download(), ref if ref is not None else got)
+        for qq in cs[1:]:
+            qq.close()
         eng.set_events(True)  # the first stage's own time and the dense pass's requests
         q.run()
         st_ev = eng.last_stats()
