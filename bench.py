@@ -7,7 +7,7 @@ times over); the global batch of N x 1M requests is split into contiguous 64-req
 ranges, one per GPU: no data-path collective, weak scaling.  A step = one batch call over
 a GPU's range with its requests already resident in HBM, enqueued without a host wait per
 call (ketogpu_queries_run_async: traversal, result bits left in HBM; batches pipelined as a
-server pipelines them, four HBM copies of the batch rotating over four streams) — `value`,
+server pipelines them, two HBM copies of the batch rotating over two streams) — `value`,
 K steps bracketed by a barrier and a device synchronization on both sides, the max over
 ranks.  Beside it: the same steps with one host wait per call (ketogpu_queries_run,
 `resident_call_checks_per_s`: round 5's value) and the host-to-host rate (requests H2D from
@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "permission checks/sec (batched, whole node) + traversal HBM GB/s vs roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PIPE_COPIES = 4  # HBM copies of a GPU's batch rotating in the pipelined (value) leg
+PIPE_COPIES = 2  # HBM copies of a GPU's batch rotating in the pipelined (value) leg
 
 
 def parse():
@@ -257,8 +257,8 @@ def main():
     # one wait per GPU at the end, barrier + device sync on both sides — batch k+1 enqueued
     # while batch k runs, as a server pipelines its batches.  PIPE_COPIES HBM copies of the
     # GPU's batch rotate (a server's consecutive batches have their own result words): calls
-    # rotate over the engine's four streams, so a call's dense pass overlaps later calls'
-    # first stages
+    # rotate over the engine's two streams, so a call's dense pass overlaps the next call's
+    # first stage
     copies = [[qq] + [e_.upload(roots[b_:e_r], targets[b_:e_r]) for _ in range(PIPE_COPIES - 1)]
               for qq, e_, (b_, e_r) in zip(qs, engs, rng)]
     for cs in copies:
@@ -409,7 +409,7 @@ def main():
             "timing": ("value: requests resident in HBM, PCIe legs excluded: per step one batch call per GPU over "
                        "its range, enqueued without a host wait per call (ketogpu_queries_run_async: validation at "
                        f"upload, traversal, result bits left in HBM; {PIPE_COPIES} HBM copies of the batch rotate, "
-                       "calls rotate over the engine's four streams), one wait per GPU after the K steps, barrier + "
+                       "calls rotate over the engine's two streams), one wait per GPU after the K steps, barrier + "
                        "device sync "
                        f"on both sides, max over ranks; {sum(queued)} of {a.steps * len(qs)} calls queued without a "
                        "wait; every copy's bits checked after; snapshot build and upload excluded.  SURVEY 8(d)'s "

@@ -4497,7 +4497,11 @@ struct ketogpu_engine {
     // k + kPipe — the next call on the same stream when pipelined calls rotate over kPipe
     // streams (ketogpu_queries_run_async), so a call's dense pass may still read its counters
     // while later calls' first stages run
-    static constexpr unsigned kPipe = 4;  // streams pipelined calls rotate over (ketogpu_queries_run_async)
+    // streams pipelined calls rotate over (ketogpu_queries_run_async).  Two: with four, the
+    // calls' first stages share the GPU fairly, end together and leave their dense passes to
+    // run together with no first stage beside them (0.0754 vs 0.0614 ms per config #2 call,
+    // profiles/r06/pipe/)
+    static constexpr unsigned kPipe = 2;
     static constexpr unsigned kLabelSets = 2 * kPipe;
     unsigned int *rest_counts = nullptr;
     uint64_t label_calls = 0;  // selects the set
