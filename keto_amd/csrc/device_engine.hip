@@ -2826,9 +2826,14 @@ __global__ __launch_bounds__(256) void label_host_kernel(DevGraph g, LabelGraph 
 // four lanes per request, persistent.  It answers from the whole lists: the landmark
 // intersection (S's raw entries never meet P's landmarks) and the one-edge test.  Both lists' places are known from the
 // records, so one dependent read follows them: the longer list is staged in LDS (up to
-// kFullStage words, from its overflow region or its head's inline entries) while the
-// shorter one's entries are fetched into registers, then binary-searched.
-constexpr uint32_t kFullStage = 256;
+// full_stage(HS, HP) words, from its overflow region or its head's inline entries) while the
+// shorter one's entries are fetched into registers, then binary-searched.  The stage is 128
+// words per request with heads of up to 32 words (8 KB per workgroup: 20 resident per CU, so
+// config #2's ~2.8k dense waves run in one round; 256 words held 10 per CU and took two:
+// 0.023 -> 0.017 ms per call) and 256 with 64-word heads, whose graphs' longer lists would
+// otherwise be searched in global memory (config #3 shape: 7.1 vs 7.6e9 pipelined;
+// profiles/r06/stage/)
+__host__ __device__ constexpr uint32_t full_stage(int HS, int HP) { return HS >= 64 || HP >= 64 ? 256u : 128u; }
 // Workgroup 0 also totals both lists' shard counts for the host (totals[0]: the rest list,
 // totals[1]: this list), so the rest stage can be launched only when it has requests.
 // Lean resident calls (plan label, timing events off, KETOGPU_LABEL_FUSE=1): the first
@@ -2841,6 +2846,7 @@ template <int HS, int HP>
 __global__ __launch_bounds__(64) void label_full_kernel(LabelGraph L, uint64_t *allowed, LabelRest R, LabelRest F,
                                                         unsigned int *total_rest, unsigned int *total_full,
                                                         unsigned long long *stats, unsigned long long *mirror) {
+    constexpr uint32_t kFullStage = full_stage(HS, HP);
     __shared__ alignas(16) uint32_t stage[16][kFullStage];
     const uint32_t lane = threadIdx.x, q = lane >> 2, sub = lane & 3;
     const uint32_t c = F.count[lane * kRestStride];
